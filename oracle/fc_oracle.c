@@ -1,0 +1,423 @@
+/*
+ * fc_oracle.c -- CPU restatement of ytabatabaee/fastconsensus's consensus inner loop.
+ *
+ *   *** TEST INFRASTRUCTURE ONLY ***
+ *   Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ *   this library, and only as the CHECKER (or the timed CPU baseline).  The product
+ *   path (fastconsensus_amd) never links, imports or falls back to it.
+ *
+ * Parity status: the deterministic parts (consensus rule, threshold, convergence
+ * check, closure given samples, isolate repair, adjacency order) are PINNED against
+ * golden vectors produced by the reference itself (tests/golden/make_golden.py).
+ * The community-detection arithmetic (python-louvain 0.15 level 0, igraph 0.9.7 LPA)
+ * is restated from the published algorithms; those libraries are absent from the
+ * container, so that part is "parity unpinned" (statistical comparisons only).
+ *
+ * Every function cites the reference line it restates (fast_consensus.py).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef int32_t i32;
+typedef int64_t i64;
+typedef uint64_t u64;
+typedef uint8_t u8;
+
+/* ------------------------------------------------------------------ RNG (oracle's own) */
+static inline u64 splitmix64(u64* s) {
+    u64 z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline u64 rng_below(u64* s, u64 n) { /* unbiased enough for tests: 128-bit multiply */
+    return (u64)(((unsigned __int128)splitmix64(s) * n) >> 64);
+}
+static void shuffle_i32(i32* a, i64 n, u64* s) {
+    for (i64 i = n - 1; i > 0; --i) {
+        i64 j = (i64)rng_below(s, (u64)(i + 1));
+        i32 t = a[i]; a[i] = a[j]; a[j] = t;
+    }
+}
+
+/* ------------------------------------------------------------------ consensus rule
+ * Louvain branch, fast_consensus.py:150-159 (literal loop, not the closed form):
+ *   nextgraph weight starts at 0 (:145-146); if graph weight not in (0, n_p) (:153):
+ *   for each partition i: same community -> += 1 (:156-157), else -> = old weight (:159).
+ * LPM branch, fast_consensus.py:273-280: count of partitions with u, v co-clustered.
+ * labels are replica-major [n_p][N].  algo: 0 = louvain, 1 = lpm.
+ */
+void orc_consensus(int algo, i64 m, const i32* eu, const i32* ev, const i32* w_in, int n_p,
+                   i64 N, const i32* lab, i32* w_out) {
+#pragma omp parallel for schedule(static)
+    for (i64 e = 0; e < m; ++e) {
+        const i32 u = eu[e], v = ev[e];
+        i32 nw = 0;
+        if (algo == 0) {
+            const i32 w = w_in[e];
+            if (w != 0 && w != n_p) {
+                for (int i = 0; i < n_p; ++i) {
+                    if (lab[(i64)i * N + u] == lab[(i64)i * N + v]) nw += 1;
+                    else nw = w;
+                }
+            }
+        } else {
+            for (int i = 0; i < n_p; ++i) nw += (lab[(i64)i * N + u] == lab[(i64)i * N + v]);
+        }
+        w_out[e] = nw;
+    }
+}
+
+/* threshold: remove iff weight < thresh*n_p (fast_consensus.py:163-168, :284-288),
+ * Python float64 product and compare.  Returns the kept count. */
+i64 orc_threshold(i64 m, const i32* w, double tau, int n_p, u8* keep) {
+    const double cut = tau * (double)n_p;
+    i64 kept = 0;
+    for (i64 e = 0; e < m; ++e) {
+        keep[e] = !((double)w[e] < cut);
+        kept += keep[e];
+    }
+    return kept;
+}
+
+/* check_consensus_graph (fast_consensus.py:17-37): count weights not in {0, n_p};
+ * not converged iff count > delta * number_of_edges.  keep may be NULL. */
+int orc_check(i64 m, const i32* w, const u8* keep, int n_p, double delta, i64* count_out) {
+    i64 count = 0, mm = 0;
+    for (i64 e = 0; e < m; ++e) {
+        if (keep && !keep[e]) continue;
+        ++mm;
+        if (w[e] != 0 && w[e] != n_p) ++count;
+    }
+    if (count_out) *count_out = count;
+    return ((double)count > delta * (double)mm) ? 0 : 1;
+}
+
+/* ------------------------------------------------------------------ sorted edge sets */
+static inline u64 ekey(i32 u, i32 v) { return ((u64)(uint32_t)u << 32) | (uint32_t)v; }
+
+static i64 find_key(const i32* eu, const i32* ev, i64 m, u64 key) {
+    i64 lo = 0, hi = m;
+    while (lo < hi) {
+        i64 mid = (lo + hi) >> 1;
+        u64 k = ekey(eu[mid], ev[mid]);
+        if (k < key) lo = mid + 1; else hi = mid;
+    }
+    return (lo < m && ekey(eu[lo], ev[lo]) == key) ? lo : -1;
+}
+
+typedef struct { u64 key; i64 idx; } kv_t;
+static int cmp_kv(const void* a, const void* b) {
+    const kv_t* x = (const kv_t*)a; const kv_t* y = (const kv_t*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->idx < y->idx ? -1 : (x->idx > y->idx);
+}
+static int cmp_idx(const void* a, const void* b) {
+    const kv_t* x = (const kv_t*)a; const kv_t* y = (const kv_t*)b;
+    return x->idx < y->idx ? -1 : (x->idx > y->idx);
+}
+
+/* Triadic closure given the recorded sample pairs (fast_consensus.py:175-190 louvain,
+ * :292-304 lpm).  Sequential semantics: pair t adds (a,b) iff it is absent from the
+ * post-threshold graph (eu,ev sorted canonical) and from the pairs already added.
+ * Weight: louvain = #partitions with a, b co-clustered (:186-190); lpm = 0 always
+ * (`a in communities[i]` compares an int with a set of frozensets, :302-304).
+ * Output in first-occurrence order; out_first[k] = sample index t of edge k.
+ * Returns the number of new edges. */
+i64 orc_closure_pairs(int algo, i64 m, const i32* eu, const i32* ev, i64 npairs,
+                      const i32* pairs, int n_p, i64 N, const i32* lab, i32* out_u,
+                      i32* out_v, i32* out_w, i64* out_first) {
+    kv_t* kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(npairs > 0 ? npairs : 1));
+    i64 n = 0;
+    for (i64 t = 0; t < npairs; ++t) {
+        i32 a = pairs[2 * t], b = pairs[2 * t + 1];
+        i32 u = a < b ? a : b, v = a < b ? b : a;
+        if (u == v) continue;
+        kv[n].key = ekey(u, v); kv[n].idx = t; ++n;
+    }
+    qsort(kv, (size_t)n, sizeof(kv_t), cmp_kv);
+    i64 k = 0;
+    for (i64 i = 0; i < n; ++i) {
+        if (i > 0 && kv[i].key == kv[i - 1].key) continue;         /* later duplicate */
+        i32 u = (i32)(kv[i].key >> 32), v = (i32)(kv[i].key & 0xffffffffu);
+        if (find_key(eu, ev, m, kv[i].key) >= 0) continue;          /* has_edge (:183) */
+        kv[k++] = kv[i];
+        (void)u; (void)v;
+    }
+    qsort(kv, (size_t)k, sizeof(kv_t), cmp_idx);
+    for (i64 i = 0; i < k; ++i) {
+        i32 u = (i32)(kv[i].key >> 32), v = (i32)(kv[i].key & 0xffffffffu);
+        i32 w = 0;
+        if (algo == 0)
+            for (int r = 0; r < n_p; ++r) w += (lab[(i64)r * N + u] == lab[(i64)r * N + v]);
+        out_u[i] = u; out_v[i] = v; out_w[i] = w; out_first[i] = kv[i].idx;
+    }
+    free(kv);
+    return k;
+}
+
+/* ------------------------------------------------------------------ adjacency order
+ * networkx adjacency order of `graph` (always produced by Graph.copy(), :131, :198):
+ * neighbours earlier in node order first, ascending; then later neighbours in edge
+ * creation order (age).  Proven in DESIGN.md §"adjacency order"; pinned by the
+ * adj* snapshots in the golden fixtures.  Writes a CSR in that order. */
+typedef struct { i32 nbr; i64 key; i32 w; } adj_t;
+static int cmp_adj(const void* a, const void* b) {
+    const adj_t* x = (const adj_t*)a; const adj_t* y = (const adj_t*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return 0;
+}
+void orc_adjacency_order(i64 N, i64 m, const i32* eu, const i32* ev, const i32* w,
+                         const i64* age, i64* ptr, i32* nbr, i32* nw) {
+    memset(ptr, 0, sizeof(i64) * (size_t)(N + 1));
+    for (i64 e = 0; e < m; ++e) { ptr[eu[e] + 1]++; ptr[ev[e] + 1]++; }
+    for (i64 x = 0; x < N; ++x) ptr[x + 1] += ptr[x];
+    adj_t* tmp = (adj_t*)malloc(sizeof(adj_t) * (size_t)(2 * m + 1));
+    i64* fill = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    memcpy(fill, ptr, sizeof(i64) * (size_t)N);
+    for (i64 e = 0; e < m; ++e) {
+        i32 u = eu[e], v = ev[e];                 /* u < v in node order */
+        /* in row v, u is an earlier neighbour: key = u (ascending node order) */
+        adj_t a = {u, (i64)u, w[e]};
+        tmp[fill[v]++] = a;
+        /* in row u, v is a later neighbour: key = N + age (after all earlier ones) */
+        adj_t b = {v, (i64)N + age[e], w[e]};
+        tmp[fill[u]++] = b;
+    }
+    for (i64 x = 0; x < N; ++x)
+        qsort(tmp + ptr[x], (size_t)(ptr[x + 1] - ptr[x]), sizeof(adj_t), cmp_adj);
+    for (i64 j = 0; j < 2 * m; ++j) { nbr[j] = tmp[j].nbr; if (nw) nw[j] = tmp[j].w; }
+    free(tmp); free(fill);
+}
+
+/* Isolate repair (fast_consensus.py:193-195).  For each node x in node order that has
+ * degree 0 in nextgraph AT VISIT TIME (nx.isolates is a lazy generator), connect it to
+ * the neighbour y of x in the OLD graph with the minimum old weight -- stable sort, so
+ * ties go to the first neighbour in networkx adjacency order -- carrying that weight.
+ * old graph: (m_old, ou, ov, ow, oage); nextgraph degrees: deg[N] (updated in place).
+ * Returns the number of repair edges written to out_u/out_v/out_w (canonical u<v) in
+ * the order they are added. */
+i64 orc_repair(i64 N, i64 m_old, const i32* ou, const i32* ov, const i32* ow, const i64* oage,
+               i64* deg, i32* out_u, i32* out_v, i32* out_w) {
+    i64* ptr = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    i32* nbr = (i32*)malloc(sizeof(i32) * (size_t)(2 * m_old + 1));
+    i32* nw = (i32*)malloc(sizeof(i32) * (size_t)(2 * m_old + 1));
+    orc_adjacency_order(N, m_old, ou, ov, ow, oage, ptr, nbr, nw);
+    i64 k = 0;
+    for (i64 x = 0; x < N; ++x) {
+        if (deg[x] != 0) continue;
+        if (ptr[x + 1] == ptr[x]) continue;        /* reference would raise IndexError */
+        i64 best = ptr[x];
+        for (i64 j = ptr[x] + 1; j < ptr[x + 1]; ++j)
+            if (nw[j] < nw[best]) best = j;          /* strict: first minimum wins */
+        i32 y = nbr[best];
+        out_u[k] = (i32)(x < y ? x : y); out_v[k] = (i32)(x < y ? y : x); out_w[k] = nw[best];
+        ++k;
+        deg[x]++; deg[y]++;
+    }
+    free(ptr); free(nbr); free(nw);
+    return k;
+}
+
+/* Sort + merge: canonical sorted edge list from an unsorted one (stable on equal keys
+ * never happens: edge sets are simple).  perm receives the source index order. */
+void orc_sort_edges(i64 m, const i32* eu, const i32* ev, i64* perm) {
+    kv_t* kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(m > 0 ? m : 1));
+    for (i64 e = 0; e < m; ++e) { kv[e].key = ekey(eu[e], ev[e]); kv[e].idx = e; }
+    qsort(kv, (size_t)m, sizeof(kv_t), cmp_kv);
+    for (i64 e = 0; e < m; ++e) perm[e] = kv[e].idx;
+    free(kv);
+}
+
+/* ------------------------------------------------------------------ python-louvain level 0
+ * Restatement of python-louvain 0.15 `generate_dendrogram(graph, randomize=True)` level 0
+ * = `status.init` + `__one_level` (called at fast_consensus.py:148, :384), from the
+ * published package source (not vendored; not line-citable here):
+ *   passes over a freshly shuffled node order; per node: remove from own community,
+ *   incr = remove_cost + dnc - deg(com)*k_i/(2*tw) over neighbour communities in a
+ *   shuffled order, strict > best (starting at 0 = stay); stop when a pass improves
+ *   modularity by < 1e-7 (__MIN) or moves nothing.  float64 arithmetic as in Python.
+ * Output labels are renumbered 0..k-1 by first appearance in node order.
+ * CSR: symmetric, no self loops.  Returns the number of passes. */
+static double modularity_status(i64 N, const double* internals, const double* degrees, double tw) {
+    double q = 0.0;
+    if (tw <= 0) return 0.0;
+    for (i64 c = 0; c < N; ++c) {
+        if (degrees[c] == 0.0 && internals[c] == 0.0) continue;
+        q += internals[c] / tw - (degrees[c] / (2.0 * tw)) * (degrees[c] / (2.0 * tw));
+    }
+    return q;
+}
+
+static void renumber(i64 N, i32* lab, i32* map) {
+    for (i64 i = 0; i < N; ++i) map[i] = -1;
+    i32 next = 0;
+    for (i64 i = 0; i < N; ++i) {
+        if (map[lab[i]] < 0) map[lab[i]] = next++;
+        lab[i] = map[lab[i]];
+    }
+}
+
+int orc_louvain_level0(i64 N, const i64* rowptr, const i32* col, const i32* w, u64 seed,
+                       i32* lab) {
+    u64 s = seed ^ 0xD1B54A32D192ED03ull;
+    double* gdeg = (double*)calloc((size_t)N, sizeof(double));
+    double* degrees = (double*)calloc((size_t)N, sizeof(double));
+    double* internals = (double*)calloc((size_t)N, sizeof(double));
+    double* neighw = (double*)calloc((size_t)N, sizeof(double));
+    i32* order = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    i32* ncoms = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    u8* seen = (u8*)calloc((size_t)N, 1);
+    double tw = 0.0;
+    for (i64 i = 0; i < N; ++i) {
+        double d = 0.0;
+        for (i64 j = rowptr[i]; j < rowptr[i + 1]; ++j) d += (double)w[j];
+        gdeg[i] = d; degrees[i] = d; internals[i] = 0.0; lab[i] = (i32)i; order[i] = (i32)i;
+        tw += d;
+    }
+    tw *= 0.5;                       /* graph.size(weight): each edge once */
+    int passes = 0;
+    if (tw > 0.0) {
+        double new_mod = modularity_status(N, internals, degrees, tw), cur_mod;
+        int modified = 1;
+        while (modified) {
+            cur_mod = new_mod;
+            modified = 0;
+            ++passes;
+            shuffle_i32(order, N, &s);
+            for (i64 t = 0; t < N; ++t) {
+                const i32 node = order[t];
+                const i32 com_node = lab[node];
+                const double degc_totw = gdeg[node] / (tw * 2.0);
+                i64 nc = 0;
+                for (i64 j = rowptr[node]; j < rowptr[node + 1]; ++j) {
+                    const i32 c = lab[col[j]];
+                    if (col[j] == node) continue;
+                    if (!seen[c]) { seen[c] = 1; ncoms[nc++] = c; neighw[c] = 0.0; }
+                    neighw[c] += (double)w[j];
+                }
+                const double own_w = seen[com_node] ? neighw[com_node] : 0.0;
+                const double remove_cost = -own_w + (degrees[com_node] - gdeg[node]) * degc_totw;
+                degrees[com_node] -= gdeg[node];               /* __remove */
+                internals[com_node] -= own_w;
+                i32 best_com = com_node;
+                double best_inc = 0.0;
+                shuffle_i32(ncoms, nc, &s);
+                for (i64 q = 0; q < nc; ++q) {
+                    const i32 c = ncoms[q];
+                    const double incr = remove_cost + neighw[c] - degrees[c] * degc_totw;
+                    if (incr > best_inc) { best_inc = incr; best_com = c; }
+                }
+                const double bw = seen[best_com] ? neighw[best_com] : 0.0;
+                degrees[best_com] += gdeg[node];                /* __insert */
+                internals[best_com] += bw;
+                lab[node] = best_com;
+                if (best_com != com_node) modified = 1;
+                for (i64 q = 0; q < nc; ++q) seen[ncoms[q]] = 0;
+            }
+            new_mod = modularity_status(N, internals, degrees, tw);
+            if (new_mod - cur_mod < 1e-7) break;
+        }
+    }
+    renumber(N, lab, ncoms);
+    free(gdeg); free(degrees); free(internals); free(neighw); free(order); free(ncoms); free(seen);
+    return passes;
+}
+
+/* ------------------------------------------------------------------ igraph 0.9.7 LPA
+ * Restatement of igraph_community_label_propagation as called at fast_consensus.py:270
+ * (no weights => every neighbour counts 1): unique initial labels; each sweep visits
+ * nodes in a fresh random order and assigns a uniformly random dominant neighbour
+ * label; another sweep is needed iff some visited node's current label was not
+ * dominant.  Isolated nodes keep their label.  Returns the number of sweeps. */
+int orc_lpa(i64 N, const i64* rowptr, const i32* col, u64 seed, i32* lab, int max_sweeps) {
+    u64 s = seed ^ 0x8CB92BA72F3D8DD7ull;
+    i32* order = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    i32* cnt = (i32*)calloc((size_t)N, sizeof(i32));
+    i32* dom = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    i32* touched = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    for (i64 i = 0; i < N; ++i) { lab[i] = (i32)i; order[i] = (i32)i; }
+    int sweeps = 0, running = 1;
+    while (running && sweeps < max_sweeps) {
+        running = 0;
+        ++sweeps;
+        shuffle_i32(order, N, &s);
+        for (i64 t = 0; t < N; ++t) {
+            const i32 v = order[t];
+            i64 nt = 0, nd = 0;
+            i32 maxc = 0;
+            for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) {
+                const i32 l = lab[col[j]];
+                if (cnt[l] == 0) touched[nt++] = l;
+                const i32 c = ++cnt[l];
+                if (c > maxc) { maxc = c; nd = 0; dom[nd++] = l; }
+                else if (c == maxc) dom[nd++] = l;
+            }
+            if (nd > 0) {
+                if (cnt[lab[v]] != maxc) running = 1;
+                lab[v] = dom[rng_below(&s, (u64)nd)];
+            }
+            for (i64 q = 0; q < nt; ++q) cnt[touched[q]] = 0;
+        }
+    }
+    renumber(N, lab, dom);
+    free(order); free(cnt); free(dom); free(touched);
+    return sweeps;
+}
+
+/* Batch helper: n_r independent runs (replicas) in parallel over host threads.
+ * algo 0 = louvain level 0, 1 = lpa.  lab is [n_r][N]. */
+void orc_cd_batch(int algo, int n_r, i64 N, const i64* rowptr, const i32* col, const i32* w,
+                  u64 seed, i32* lab, int* sweeps, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < n_r; ++r) {
+        u64 sd = seed * 0x9E3779B97F4A7C15ull + (u64)r * 0xC2B2AE3D27D4EB4Full + 1;
+        int sw = algo == 0 ? orc_louvain_level0(N, rowptr, col, w, sd, lab + (i64)r * N)
+                           : orc_lpa(N, rowptr, col, sd, lab + (i64)r * N, 10000);
+        if (sweeps) sweeps[r] = sw;
+    }
+}
+
+/* Modularity of a labelling (for statistical tests): Q = sum_c in_c/M - (tot_c/2M)^2. */
+double orc_modularity(i64 N, const i64* rowptr, const i32* col, const i32* w, const i32* lab) {
+    double* tot = (double*)calloc((size_t)N, sizeof(double));
+    double in = 0.0, tw = 0.0;
+    for (i64 i = 0; i < N; ++i)
+        for (i64 j = rowptr[i]; j < rowptr[i + 1]; ++j) {
+            const double ww = w ? (double)w[j] : 1.0;
+            tot[lab[i]] += ww;
+            tw += ww;
+            if (lab[col[j]] == lab[i]) in += ww;
+        }
+    double q = 0.0;
+    if (tw > 0) {
+        q = in / tw;
+        for (i64 c = 0; c < N; ++c) q -= (tot[c] / tw) * (tot[c] / tw);
+    }
+    free(tot);
+    return q;
+}
+
+/* Symmetric CSR (neighbours ascending) from a canonical edge list. */
+void orc_build_csr(i64 N, i64 m, const i32* eu, const i32* ev, const i32* w, i64* rowptr,
+                   i32* col, i32* cw) {
+    memset(rowptr, 0, sizeof(i64) * (size_t)(N + 1));
+    for (i64 e = 0; e < m; ++e) { rowptr[eu[e] + 1]++; rowptr[ev[e] + 1]++; }
+    for (i64 x = 0; x < N; ++x) rowptr[x + 1] += rowptr[x];
+    i64* fill = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    memcpy(fill, rowptr, sizeof(i64) * (size_t)N);
+    /* lower neighbours first (ascending u, because eu is sorted), then upper ones */
+    for (i64 e = 0; e < m; ++e) { i64 p = fill[ev[e]]++; col[p] = eu[e]; if (cw) cw[p] = w ? w[e] : 1; }
+    for (i64 e = 0; e < m; ++e) { i64 p = fill[eu[e]]++; col[p] = ev[e]; if (cw) cw[p] = w ? w[e] : 1; }
+    free(fill);
+}

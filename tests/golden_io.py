@@ -1,0 +1,51 @@
+"""Load the golden fixtures written by tests/golden/make_golden.py (data only)."""
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = ["karate_louvain_np50", "karate_lpm_np20", "lfr1k_louvain_np20", "lfr1k_lpm_np20"]
+
+
+class Case:
+    def __init__(self, name):
+        with open(os.path.join(GOLDEN, name + ".json")) as f:
+            self.meta = json.load(f)
+        z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+        self.z = {k: z[k] for k in z.files}
+        self.name = name
+        self.algo = 0 if self.meta["algorithm"] == "louvain" else 1
+        self.n_p = self.meta["n_p"]
+        self.tau = self.meta["tau"]
+        self.delta = self.meta["delta"]
+        self.N = self.meta["N"]
+        self.edges_file = self.z["edges_file"]
+        n_p = self.n_p
+        cd = self.z["cd_labels"]
+        self.cd_batches = [cd[b * n_p:(b + 1) * n_p] for b in range(len(cd) // n_p)]
+        self.pair_batches = []
+        b = 0
+        while "pairs%d" % b in self.z:
+            self.pair_batches.append(self.z["pairs%d" % b])
+            b += 1
+        self.checks = [(self.z["check%d_edges" % c], self.meta["check_results"][c])
+                       for c in range(self.meta["n_checks"])]
+        self.adj = []
+        b = 0
+        while "adj%d_ptr" % b in self.z:
+            self.adj.append((self.z["adj%d_ptr" % b], self.z["adj%d_nbr" % b], self.z["adj%d_w" % b]))
+            b += 1
+
+    def check_dict(self, c):
+        e, _ = self.checks[c]
+        out = {}
+        for u, v, w in e:
+            u, v = int(u), int(v)
+            assert float(w).is_integer()
+            out[(min(u, v), max(u, v))] = int(w)
+        return out
+
+
+def load(name):
+    return Case(name)

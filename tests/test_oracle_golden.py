@@ -1,0 +1,128 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself.
+
+Each fixture was produced by running /root/reference/fast_consensus.py with stubbed
+community-detection libraries (tests/golden/make_golden.py); the oracle's replay of
+the same labelings + closure samples must reproduce every graph the reference passed
+to check_consensus_graph (fast_consensus.py:172, :201, :309), the convergence
+decisions, the exit point and the networkx adjacency order of `graph` at each
+iteration start (which decides the isolate-repair tie-break, :193-195).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests import golden_io
+
+CASES = golden_io.CASES
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_replay_matches_reference(name):
+    case = golden_io.load(name)
+    graphs, traces, final_b = orc.replay(case.algo, case.N, case.edges_file, case.n_p, case.tau, case.delta,
+                                         case.cd_batches, case.pair_batches)
+    assert final_b == len(case.cd_batches) - 1
+    c = 0
+    for i, tr in enumerate(traces):
+        if case.algo == orc.LOUVAIN:
+            assert tr["kept"].as_dict() == case.check_dict(c), "post-threshold graph (check #1 input)"
+            assert tr["check1"][0] == case.checks[c][1]
+            c += 1
+            if tr["check1"][0]:
+                break
+        gnew = graphs[i + 1]
+        assert gnew.as_dict() == case.check_dict(c), "post-closure/repair graph"
+        assert tr["check2"][0] == case.checks[c][1]
+        c += 1
+    assert c == len(case.checks)
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if "louvain" in n])
+def test_adjacency_order_model(name):
+    """Our age model reproduces networkx's adjacency order of `graph` at every CD batch."""
+    case = golden_io.load(name)
+    graphs, _, _ = orc.replay(case.algo, case.N, case.edges_file, case.n_p, case.tau, case.delta,
+                              case.cd_batches, case.pair_batches)
+    assert len(case.adj) == len(graphs)
+    for b, (ptr, nbr, w) in enumerate(case.adj):
+        p2, n2, w2 = graphs[b].adjacency_order()
+        np.testing.assert_array_equal(ptr, p2)
+        np.testing.assert_array_equal(nbr, n2)
+        np.testing.assert_array_equal(w.astype(np.int64), w2.astype(np.int64))
+
+
+def test_consensus_rule_closed_form_random():
+    """Literal reference loop (oracle) == closed form used by the HIP kernel:
+    w in {0,n_p} -> 0; all agree -> n_p; else w + n_p - 1 - k_last."""
+    rng = np.random.default_rng(0)
+    for n_p in (1, 2, 7, 20, 64):
+        N, m = 200, 3000
+        u = rng.integers(0, N, m).astype(np.int32)
+        v = rng.integers(0, N, m).astype(np.int32)
+        w = rng.integers(0, 2 * n_p + 2, m).astype(np.int32)
+        lab = rng.integers(0, 4, (n_p, N)).astype(np.int32)
+        g = orc.EdgeGraph(N, u, v, w, np.zeros(m, np.int64))
+        got = orc.consensus(orc.LOUVAIN, g, lab, n_p)
+        diff = lab[:, u] != lab[:, v]
+        klast = np.where(diff.any(0), n_p - 1 - np.argmax(diff[::-1], axis=0), -1)
+        exp = np.where(klast < 0, n_p, w + n_p - 1 - klast)
+        exp = np.where((w == 0) | (w == n_p), 0, exp)
+        np.testing.assert_array_equal(got, exp)
+        cnt = orc.consensus(orc.LPM, g, lab, n_p)
+        np.testing.assert_array_equal(cnt, (~diff).sum(0))
+
+
+def test_threshold_float_semantics():
+    """keep iff !(w < tau*n_p) in float64 -- e.g. 0.56*25 = 14.000000000000002."""
+    w = np.arange(0, 30, dtype=np.int32)
+    keep = orc.threshold(w, 0.56, 25)
+    assert not keep[14] and keep[15]
+    keep = orc.threshold(w, 0.58, 50)           # 28.999999999999996
+    assert keep[29] and not keep[28]
+    keep = orc.threshold(w, 0.2, 50)
+    assert keep[10] and not keep[9]
+
+
+def test_check_semantics():
+    assert orc.check(np.array([], np.int32), 5, 0.1)[0] is True
+    w = np.array([5, 0, 3, 5, 7], np.int32)            # two unconverged of five
+    assert orc.check(w, 5, 0.4)[0] is True              # 2 > 2.0 is False
+    assert orc.check(w, 5, 0.39)[0] is False
+
+
+def test_louvain_restatement_quality():
+    """The python-louvain level-0 restatement reaches networkx-like modularity (statistical)."""
+    import networkx as nx
+    case = golden_io.load("lfr1k_louvain_np20")
+    g = orc.EdgeGraph.from_lines(case.N, case.edges_file)
+    lab, sweeps = orc.cd_batch(orc.LOUVAIN, 8, g, seed=7)
+    q = [orc.modularity(g, l) for l in lab]
+    G = nx.Graph()
+    G.add_edges_from(zip(g.u.tolist(), g.v.tolist()))
+    qs = []
+    for s in range(4):
+        part = next(iter(nx.community.louvain_partitions(G, seed=s)))
+        qs.append(nx.community.modularity(G, part))
+    assert np.mean(q) > np.mean(qs) - 0.03, (q, qs)
+    assert (sweeps >= 2).all()
+    assert len({tuple(l) for l in lab}) > 1, "replicas must differ (random order)"
+
+
+def test_lpa_restatement_quality():
+    import networkx as nx
+    case = golden_io.load("lfr1k_lpm_np20")
+    g = orc.EdgeGraph.from_lines(case.N, case.edges_file)
+    lab, sweeps = orc.cd_batch(orc.LPM, 8, g, seed=3)
+    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu04_planted.npy")
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    scores = [nmi(planted, l) for l in lab]
+    G = nx.Graph()
+    G.add_edges_from(zip(g.u.tolist(), g.v.tolist()))
+    ref = []
+    for s in range(4):
+        comms = list(nx.community.asyn_lpa_communities(G, seed=s))
+        l = np.zeros(g.N, np.int32)
+        for i, c in enumerate(comms):
+            l[list(c)] = i
+        ref.append(nmi(planted, l))
+    assert np.mean(scores) > np.mean(ref) - 0.1, (scores, ref)
