@@ -1,0 +1,57 @@
+"""Build libfastconsensus_amd.so (HIP for gfx950) in-tree with hipcc.
+
+    python -m fastconsensus_amd.build      # or __graft_entry__.build()
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+OUT_DIR = os.path.join(PKG, "lib")
+LIB = os.path.join(OUT_DIR, "libfastconsensus_amd.so")
+SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "capi.cpp", "gen.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
+         "-I" + os.path.join(os.path.dirname(PKG), "include")]
+
+
+def _obj(src):
+    return os.path.join(OUT_DIR, "obj", src + ".o")
+
+
+def _deps():
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + \
+        [os.path.join(os.path.dirname(PKG), "include", "fastconsensus_amd.h")]
+
+
+def _compile(src):
+    path = os.path.join(CSRC, src)
+    obj = _obj(src)
+    newest = max(os.path.getmtime(d) for d in _deps())
+    if os.path.exists(obj) and os.path.getmtime(obj) >= newest:
+        return obj
+    lang = ["-x", "hip"] if src.endswith(".hip") else []
+    cmd = [HIPCC] + FLAGS + lang + ["-c", path, "-o", obj]
+    subprocess.check_call(cmd)
+    return obj
+
+
+def build(verbose=True, jobs=None):
+    os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
+    jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2), 8)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+    subprocess.check_call(cmd)
+    if verbose:
+        print("built", LIB, file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build()

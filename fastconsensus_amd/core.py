@@ -1,0 +1,259 @@
+"""Host side of the engine: the drop-in ``fast_consensus()`` and a thin ``Engine`` over
+the C-ABI.  Mirrors fast_consensus.py:129-411 (same names, argument meaning, defaults
+and return types); all compute runs in the HIP library.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import FC_ALGO_LOUVAIN, FC_ALGO_LPM, FastConsensusError, Stats, check, ptr
+
+ALGORITHMS = {"louvain": FC_ALGO_LOUVAIN, "lpm": FC_ALGO_LPM}
+OUT_OF_SCOPE = ("infomap", "leiden", "cnm")
+FINAL_PASS_ITER = 0x40000000  # iteration salt of the final pass (matches capi.cpp fc_run)
+
+
+def algo_id(algorithm):
+    if algorithm in ALGORITHMS:
+        return ALGORITHMS[algorithm]
+    if algorithm in OUT_OF_SCOPE:
+        raise NotImplementedError("algorithm %r is outside this engine's scope (louvain and lpm only)"
+                                  % algorithm)
+    return None
+
+
+class Engine:
+    """One device-resident consensus engine (one GPU, one host thread)."""
+
+    def __init__(self, device=0, seed=None):
+        L = _lib.load()
+        if seed is None:
+            seed = int.from_bytes(os.urandom(8), "little")  # the reference is unseeded
+        self.seed = int(seed) & (2 ** 64 - 1)
+        self._ctx = ctypes.c_void_p()
+        check(L.fc_create(int(device), self.seed, ctypes.byref(self._ctx)))
+        self._L = L
+        self.device = device
+
+    # -- lifecycle ---------------------------------------------------------------
+    def close(self):
+        if self._ctx:
+            self._L.fc_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_handle):
+        check(self._L.fc_set_stream(self._ctx, stream_handle))
+
+    def set_timing(self, on=True):
+        check(self._L.fc_set_timing(self._ctx, 1 if on else 0))
+
+    def collect_timing(self):
+        st = Stats()
+        check(self._L.fc_collect_timing(self._ctx, ctypes.byref(st)))
+        return st.as_dict()
+
+    def set_params(self, buckets=0, max_sweeps=0, max_iters=0):
+        check(self._L.fc_set_params(self._ctx, int(buckets), int(max_sweeps), int(max_iters)))
+
+    # -- graph -----------------------------------------------------------------------
+    def load_graph(self, n, u, v):
+        u = np.ascontiguousarray(u, dtype=np.int32)
+        v = np.ascontiguousarray(v, dtype=np.int32)
+        assert u.shape == v.shape
+        check(self._L.fc_load_graph(self._ctx, int(n), len(u), u, v))
+
+    def reset_graph(self):
+        check(self._L.fc_reset_graph(self._ctx))
+
+    def graph_info(self):
+        n, m, m0 = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.fc_graph_info(self._ctx, ctypes.byref(n), ctypes.byref(m), ctypes.byref(m0)))
+        return n.value, m.value, m0.value
+
+    @property
+    def n(self):
+        return self.graph_info()[0]
+
+    @property
+    def m(self):
+        return self.graph_info()[1]
+
+    def get_graph(self):
+        _, m, _ = self.graph_info()
+        u = np.empty(m, np.int32)
+        v = np.empty(m, np.int32)
+        w = np.empty(m, np.int32)
+        age = np.empty(m, np.int64)
+        check(self._L.fc_get_graph(self._ctx, ptr(u), ptr(v), ptr(w), ptr(age)))
+        return u, v, w, age
+
+    def get_nextgraph(self):
+        m = ctypes.c_int64()
+        check(self._L.fc_get_nextgraph(self._ctx, ctypes.byref(m), None, None, None, None))
+        u, v, w = (np.empty(m.value, np.int32) for _ in range(3))
+        age = np.empty(m.value, np.int64)
+        check(self._L.fc_get_nextgraph(self._ctx, ctypes.byref(m), ptr(u), ptr(v), ptr(w), ptr(age)))
+        return u, v, w, age
+
+    # -- one-shot driver ------------------------------------------------------------------
+    def run(self, algo, n_p, tau, delta):
+        n = self.n
+        labels = np.empty((n_p, n), np.int32)
+        st = Stats()
+        check(self._L.fc_run(self._ctx, int(algo), int(n_p), float(tau), float(delta), ptr(labels),
+                             ctypes.byref(st)))
+        return labels, st.as_dict()
+
+    # -- step API (distributed driver, replay) ------------------------------------------
+    def cd(self, algo, rbegin, rcount, n_p_total, iteration):
+        check(self._L.fc_cd(self._ctx, int(algo), int(rbegin), int(rcount), int(n_p_total), int(iteration)))
+
+    def set_labels(self, labels):
+        labels = np.ascontiguousarray(labels, dtype=np.int32)
+        check(self._L.fc_set_labels(self._ctx, labels.shape[0], labels))
+
+    def get_labels(self, count, renumber=False):
+        out = np.empty((count, self.n), np.int32)
+        check(self._L.fc_get_labels(self._ctx, out, 1 if renumber else 0))
+        return out
+
+    def consensus_partial(self, algo, dev_out):
+        check(self._L.fc_consensus_partial(self._ctx, int(algo), ptr(dev_out)))
+
+    def consensus_apply(self, algo, n_p, tau, delta, dev_partial):
+        conv, kept, unc = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.fc_consensus_apply(self._ctx, int(algo), int(n_p), float(tau), float(delta),
+                                         ptr(dev_partial), ctypes.byref(conv), ctypes.byref(kept),
+                                         ctypes.byref(unc)))
+        return bool(conv.value), kept.value, unc.value
+
+    def closure_sample(self, attempts, iteration):
+        nc = ctypes.c_int64()
+        check(self._L.fc_closure_sample(self._ctx, int(attempts), int(iteration), ctypes.byref(nc)))
+        return nc.value
+
+    def closure_set_pairs(self, pairs, iteration):
+        pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+        nc = ctypes.c_int64()
+        check(self._L.fc_closure_set_pairs(self._ctx, len(pairs), ptr(pairs), int(iteration), ctypes.byref(nc)))
+        return nc.value
+
+    def closure_partial(self, dev_out):
+        check(self._L.fc_closure_partial(self._ctx, ptr(dev_out)))
+
+    def closure_apply(self, algo, n_p, delta, dev_counts, iteration):
+        conv, m = ctypes.c_int(), ctypes.c_int64()
+        check(self._L.fc_closure_apply(self._ctx, int(algo), int(n_p), float(delta), ptr(dev_counts),
+                                       int(iteration), ctypes.byref(conv), ctypes.byref(m)))
+        return bool(conv.value), m.value
+
+
+# ------------------------------------------------------------------------------------ inputs
+class IdGraph:
+    """A graph in engine form: node labels in node order + edges as node-order ids, in an
+    order whose per-node first occurrences reproduce networkx adjacency order."""
+
+    def __init__(self, labels, u, v):
+        self.labels = np.asarray(labels)
+        self.u = np.ascontiguousarray(u, dtype=np.int32)
+        self.v = np.ascontiguousarray(v, dtype=np.int32)
+
+    @property
+    def n(self):
+        return len(self.labels)
+
+    @staticmethod
+    def from_networkx(G):
+        """Node order = G.nodes(); for each node x, its later neighbours are emitted in
+        G.adj[x] order (that is the order G.copy() keeps, fast_consensus.py:131)."""
+        if G.is_directed():
+            raise TypeError("fast_consensus needs an undirected graph")
+        nodes = list(G.nodes())
+        idx = {x: i for i, x in enumerate(nodes)}
+        us, vs = [], []
+        for x in nodes:
+            ix = idx[x]
+            for z in G.adj[x]:
+                iz = idx[z]
+                if iz > ix:
+                    us.append(ix)
+                    vs.append(iz)
+        return IdGraph(nodes, np.array(us, np.int32), np.array(vs, np.int32))
+
+    @staticmethod
+    def from_edgelist_file(path):
+        """Native parser (nx.read_edgelist(path, nodetype=int) semantics, :434)."""
+        L = _lib.load()
+        n, m = ctypes.c_int64(), ctypes.c_int64()
+        check(L.fc_read_edgelist(path.encode(), ctypes.byref(n), ctypes.byref(m), None, None, None))
+        labels = np.empty(n.value, np.int64)
+        u = np.empty(m.value, np.int32)
+        v = np.empty(m.value, np.int32)
+        check(L.fc_read_edgelist(path.encode(), ctypes.byref(n), ctypes.byref(m), ptr(labels), ptr(u), ptr(v)))
+        return IdGraph(labels, u, v)
+
+
+def labels_to_output(algorithm, node_labels, labels):
+    """Engine labelings [n_p][N] -> the reference's return type (fast_consensus.py:383-392):
+    louvain: list of dict node -> community (insertion order = node order, as
+    python-louvain builds it); lpm: list of set of frozenset of nodes."""
+    out = []
+    nodes = list(node_labels.tolist())
+    for lab in labels:
+        if algorithm == "louvain":
+            out.append(dict(zip(nodes, lab.tolist())))
+        else:
+            groups = {}
+            for node, c in zip(nodes, lab.tolist()):
+                groups.setdefault(c, []).append(node)
+            out.append({frozenset(g) for g in groups.values()})
+    return out
+
+
+def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, seed=None, device=0,
+                   return_stats=False):
+    """Drop-in for fast_consensus.py:129 ``fast_consensus(G, algorithm, n_p, thresh, delta)``.
+
+    G: an undirected networkx Graph (weights are ignored: the reference resets them to 1,
+    :135-136) or an ``IdGraph``.  Returns a list of n_p partitions -- dicts for louvain,
+    sets of frozensets for lpm -- or None for an unknown algorithm (the reference's loop
+    ``break``s and returns None, :380-381).  ``seed`` makes the run reproducible (the
+    reference is unseeded).
+    """
+    algo = algo_id(algorithm)
+    if algo is None:
+        return None
+    g = G if isinstance(G, IdGraph) else IdGraph.from_networkx(G)
+    with Engine(device=device, seed=seed) as eng:
+        eng.load_graph(g.n, g.u, g.v)
+        labels, stats = eng.run(algo, int(n_p), float(thresh), float(delta))
+    out = labels_to_output(algorithm, g.labels, labels)
+    return (out, stats) if return_stats else out
+
+
+def check_consensus_graph(G, n_p, delta):
+    """fast_consensus.py:17-37 on a networkx graph (host utility, not the hot path)."""
+    count = sum(1 for w in (d.get("weight") for _, _, d in G.edges(data=True)) if w != 0 and w != n_p)
+    return not (count > delta * G.number_of_edges())
+
+
+def group_to_partition(partition):
+    """fast_consensus.py:55-71: {node: community} -> communities in first-appearance order."""
+    part = {}
+    for node, c in partition.items():
+        part.setdefault(c, []).append(node)
+    return part.values()

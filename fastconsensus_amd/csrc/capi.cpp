@@ -1,0 +1,375 @@
+// capi.cpp -- extern "C" entry points (include/fastconsensus_amd.h) and the native
+// driver loop that replaces fast_consensus()'s while-loop (fast_consensus.py:138-411).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "fc_ctx.h"
+
+namespace fc {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+// ------------------------------------------------------------------ timing
+int timer_begin(Ctx& c) {
+    Timer& t = c.timer;
+    if (!t.on) return -1;
+    if (t.next >= t.pool.size()) {
+        size_t add = t.pool.empty() ? 4096 : t.pool.size();
+        for (size_t i = 0; i < add; ++i) {
+            hipEvent_t e;
+            FC_HIP(hipEventCreate(&e));
+            t.pool.push_back(e);
+        }
+    }
+    const int idx = (int)t.next++;
+    FC_HIP(hipEventRecord(t.pool[idx], c.stream));
+    return idx;
+}
+void timer_end(Ctx& c, int slot, int b) {
+    if (b < 0) return;
+    const int e = timer_begin(c);
+    c.timer.spans[slot].push_back({b, e});
+}
+void timer_collect(Ctx& c, fc_stats* st) {
+    Timer& t = c.timer;
+    double ms[5] = {0, 0, 0, 0, 0};
+    int64_t launches = 0;
+    if (!t.pool.empty()) FC_HIP(hipStreamSynchronize(c.stream));
+    for (int s = 0; s < 5; ++s) {
+        for (auto& pr : t.spans[s]) {
+            float x = 0.f;
+            FC_HIP(hipEventElapsedTime(&x, t.pool[pr.first], t.pool[pr.second]));
+            ms[s] += x;
+        }
+        if (s == 4) launches = (int64_t)t.spans[s].size();
+        t.spans[s].clear();
+    }
+    t.next = 0;
+    if (st) {
+        *st = c.prof;
+        st->cd_ms = ms[0]; st->consensus_ms = ms[1]; st->closure_ms = ms[2]; st->rebuild_ms = ms[3];
+        st->decide_ms = ms[4]; st->decide_launches = launches;
+    }
+    c.prof = fc_stats{};
+}
+
+static void bind(Ctx& c) { FC_HIP(hipSetDevice(c.device)); }
+
+}  // namespace fc
+
+using namespace fc;
+
+struct fc_ctx {
+    Ctx c;
+};
+
+#define FC_API_BEGIN try {
+#define FC_API_END                                   \
+    }                                                \
+    catch (const FcError& e) {                       \
+        set_error(e.msg);                            \
+        return e.code;                               \
+    }                                                \
+    catch (const std::exception& e) {                \
+        set_error(std::string("exception: ") + e.what()); \
+        return FC_EINVAL;                            \
+    }                                                \
+    return FC_OK;
+
+#define FC_CTX(ctx)                                              \
+    if (!(ctx)) { set_error("null context"); return FC_EINVAL; } \
+    Ctx& c = (ctx)->c;                                           \
+    bind(c);
+
+extern "C" {
+
+const char* fc_last_error(void) { return g_err.c_str(); }
+const char* fc_version(void) { return "fastconsensus_amd 0.1.0 (gfx950)"; }
+
+int fc_create(int device, uint64_t seed, fc_ctx** out) {
+    if (!out) { set_error("null out"); return FC_EINVAL; }
+    *out = nullptr;
+    FC_API_BEGIN
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        throw FcError{FC_ENODEV, "no HIP device visible (the engine has no CPU fallback)"};
+    FC_REQUIRE(device >= 0 && device < n, FC_ENODEV, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    FC_HIP(hipGetDeviceProperties(&prop, device));
+    FC_REQUIRE(std::strstr(prop.gcnArchName, "gfx950") != nullptr, FC_ENODEV,
+               std::string("engine is built for gfx950 (MI355X); device is ") + prop.gcnArchName);
+    fc_ctx* x = new fc_ctx();
+    Ctx& c = x->c;
+    c.device = device;
+    c.seed = seed;
+    try {
+        FC_HIP(hipSetDevice(device));
+        FC_HIP(hipStreamCreateWithFlags(&c.own_stream, hipStreamNonBlocking));
+        c.stream = c.own_stream;
+        FC_HIP(hipHostMalloc((void**)&c.hpin, 64 * sizeof(int64_t), hipHostMallocDefault));
+    } catch (...) {
+        delete x;
+        throw;
+    }
+    *out = x;
+    FC_API_END
+}
+
+void fc_destroy(fc_ctx* ctx) {
+    if (!ctx) return;
+    Ctx& c = ctx->c;
+    (void)hipSetDevice(c.device);
+    (void)hipStreamSynchronize(c.stream);
+    c.g.release();
+    c.g0.release();
+    DevBuf* bufs[] = {&c.lab, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
+                      &c.heavy_scratch, &c.wnew, &c.flag, &c.pos, &c.ku, &c.kv, &c.kw, &c.kage, &c.krowptr,
+                      &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
+                      &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
+                      &c.hit, &c.mkey, &c.mkey2, &c.midx, &c.midx2, &c.sort_tmp, &c.nodetmp, &c.nodetmp2,
+                      &c.nodetmp3, &c.part, &c.ccount};
+    for (auto* b : bufs) b->release();
+    for (auto e : c.timer.pool) (void)hipEventDestroy(e);
+    if (c.hpin) (void)hipHostFree(c.hpin);
+    if (c.own_stream) (void)hipStreamDestroy(c.own_stream);
+    delete ctx;
+}
+
+int fc_set_stream(fc_ctx* ctx, void* s) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_HIP(hipStreamSynchronize(c.stream));
+    c.stream = s ? (hipStream_t)s : c.own_stream;
+    FC_API_END
+}
+
+int fc_set_timing(fc_ctx* ctx, int enable) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    c.timer.on = enable != 0;
+    FC_API_END
+}
+
+int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    if (buckets > 0) c.buckets = buckets;
+    if (max_sweeps > 0) c.max_sweeps = max_sweeps;
+    if (max_iters > 0) c.max_iters = max_iters;
+    FC_API_END
+}
+
+int fc_load_graph(fc_ctx* ctx, int64_t n, int64_t m, const int32_t* u, const int32_t* v) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(m == 0 || (u && v), FC_EINVAL, "null edge arrays");
+    graph_load(c, n, m, u, v);
+    c.n_r = 0;
+    FC_API_END
+}
+
+int fc_reset_graph(fc_ctx* ctx) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
+    graph_copy(c, c.g, c.g0);
+    FC_API_END
+}
+
+int fc_graph_info(fc_ctx* ctx, int64_t* n, int64_t* m, int64_t* m0) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    if (n) *n = c.N;
+    if (m) *m = c.g.m;
+    if (m0) *m0 = c.m_original;
+    FC_API_END
+}
+
+int fc_get_graph(fc_ctx* ctx, int32_t* u, int32_t* v, int32_t* w, int64_t* age) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    const int64_t m = c.g.m;
+    if (m > 0) {
+        if (u) FC_HIP(hipMemcpyAsync(u, c.g.eu.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
+        if (v) FC_HIP(hipMemcpyAsync(v, c.g.ev.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
+        if (w) FC_HIP(hipMemcpyAsync(w, c.g.ew.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
+        if (age) FC_HIP(hipMemcpyAsync(age, c.g.eage.p, 8 * m, hipMemcpyDeviceToHost, c.stream));
+    }
+    sync(c);
+    FC_API_END
+}
+
+int fc_get_nextgraph(fc_ctx* ctx, int64_t* m_out, int32_t* u, int32_t* v, int32_t* w, int64_t* age) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    const int64_t m = c.kept_m;
+    if (m_out) *m_out = m;
+    if (m > 0) {
+        if (u) FC_HIP(hipMemcpyAsync(u, c.ku.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
+        if (v) FC_HIP(hipMemcpyAsync(v, c.kv.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
+        if (w) FC_HIP(hipMemcpyAsync(w, c.kw.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
+        if (age) FC_HIP(hipMemcpyAsync(age, c.kage.p, 8 * m, hipMemcpyDeviceToHost, c.stream));
+    }
+    sync(c);
+    FC_API_END
+}
+
+int fc_cd(fc_ctx* ctx, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(algo == FC_ALGO_LOUVAIN || algo == FC_ALGO_LPM, FC_EINVAL, "algo must be louvain or lpm");
+    cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
+    FC_API_END
+}
+
+int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
+    FC_REQUIRE(count >= 1 && labels, FC_EINVAL, "bad labelings");
+    const size_t n = (size_t)count * c.N;
+    int32_t* lab = ensure<int32_t>(c.lab, n);
+    FC_HIP(hipMemcpyAsync(lab, labels, 4 * n, hipMemcpyHostToDevice, c.stream));
+    sync(c);
+    c.n_r = count; c.rbase = 0; c.n_p_total = count;
+    c.labT_valid = false;
+    FC_API_END
+}
+
+int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings");
+    if (renumber) labels_renumber(c);
+    FC_HIP(hipMemcpyAsync(labels, c.lab.p, 4 * (size_t)c.n_r * c.N, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    FC_API_END
+}
+
+int fc_consensus_partial(fc_ctx* ctx, int algo, void* dev_out) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(dev_out || c.g.m == 0, FC_EINVAL, "null output buffer");
+    consensus_partial(c, algo, (int32_t*)dev_out);
+    FC_API_END
+}
+
+int fc_consensus_apply(fc_ctx* ctx, int algo, int n_p, double tau, double delta, const void* dev_partial,
+                       int* converged, int64_t* kept_out, int64_t* unconv_out) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(n_p >= 1, FC_EINVAL, "n_p must be >= 1");
+    int64_t kept = 0, unc = 0;
+    consensus_apply(c, algo, n_p, tau, (const int32_t*)dev_partial, &kept, &unc);
+    // check_consensus_graph (:34): not converged iff count > delta * number_of_edges
+    if (converged) *converged = (algo == FC_ALGO_LOUVAIN) ? !((double)unc > delta * (double)kept) : 0;
+    if (kept_out) *kept_out = kept;
+    if (unconv_out) *unconv_out = unc;
+    FC_API_END
+}
+
+int fc_closure_sample(fc_ctx* ctx, int64_t attempts, int iteration, int64_t* n_cand) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    if (attempts < 0) attempts = c.m_original;
+    closure_sample(c, attempts, iteration);
+    if (n_cand) *n_cand = c.n_cand;
+    FC_API_END
+}
+
+int fc_closure_set_pairs(fc_ctx* ctx, int64_t npairs, const int32_t* pairs, int iteration, int64_t* n_cand) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(npairs == 0 || pairs, FC_EINVAL, "null pairs");
+    for (int64_t i = 0; i < 2 * npairs; ++i)
+        FC_REQUIRE(pairs[i] >= 0 && pairs[i] < c.N, FC_EINVAL, "pair endpoint out of range");
+    closure_from_pairs(c, npairs, pairs, iteration);
+    if (n_cand) *n_cand = c.n_cand;
+    FC_API_END
+}
+
+int fc_closure_partial(fc_ctx* ctx, void* dev_out) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings");
+    closure_partial(c, (int32_t*)dev_out);
+    FC_API_END
+}
+
+int fc_closure_apply(fc_ctx* ctx, int algo, int n_p, double delta, const void* dev_counts, int iteration,
+                     int* converged, int64_t* m_out) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(algo != FC_ALGO_LOUVAIN || dev_counts || c.n_cand == 0, FC_EINVAL,
+               "louvain closure needs co-membership counts");
+    closure_apply(c, algo, n_p, (const int32_t*)dev_counts, iteration);
+    const int64_t unc = count_unconverged(c, c.g.ew.as<int32_t>(), c.g.m, n_p);
+    if (converged) *converged = !((double)unc > delta * (double)c.g.m);
+    if (m_out) *m_out = c.g.m;
+    FC_API_END
+}
+
+int fc_collect_timing(fc_ctx* ctx, fc_stats* st) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    timer_collect(c, st);
+    FC_API_END
+}
+
+int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* labels_out, fc_stats* st) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(algo == FC_ALGO_LOUVAIN || algo == FC_ALGO_LPM, FC_EINVAL,
+               "algorithm must be louvain or lpm (infomap/leiden/cnm are out of scope)");
+    FC_REQUIRE(n_p >= 1, FC_EINVAL, "n_p must be >= 1");
+    FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
+    const bool louv = algo == FC_ALGO_LOUVAIN;
+    graph_copy(c, c.g, c.g0);                                         // graph = G.copy() (:131)
+    c.acc = fc_stats{};
+    fc_stats& a = c.acc;
+    a.n_p = n_p;
+    int it = 0;
+    for (;;) {
+        if (it >= c.max_iters) { a.hit_iter_cap = 1; break; }
+        cd_run(c, algo, 0, n_p, n_p, it);                             // :148 / :270
+        int32_t* part = ensure<int32_t>(c.part, c.g.m + 1);
+        consensus_partial(c, algo, part);                             // :150-159 / :273-280
+        a.partition_edges += (int64_t)n_p * c.g.m;
+        int64_t kept = 0, unc = 0;
+        consensus_apply(c, algo, n_p, tau, part, &kept, &unc);        // :163-168 / :284-288
+        if (louv && !((double)unc > delta * (double)kept)) {          // check #1 (:172-173)
+            a.exit_check = 1;
+            break;
+        }
+        closure_sample(c, c.m_original, it);                          // :175-184 / :292-300
+        int32_t* cnt = nullptr;
+        if (louv && c.n_cand > 0) {
+            cnt = ensure<int32_t>(c.ccount, c.n_cand);
+            closure_partial(c, cnt);                                  // :186-190
+        }
+        closure_apply(c, algo, n_p, cnt, it);                         // :193-198 / :307
+        const int64_t unc2 = count_unconverged(c, c.g.ew.as<int32_t>(), c.g.m, n_p);
+        ++it;
+        if (!((double)unc2 > delta * (double)c.g.m)) {                // :201-202 / :309-310
+            a.exit_check = 2;
+            break;
+        }
+    }
+    a.iterations = it + (a.exit_check == 1 ? 1 : 0);
+    cd_run(c, algo, 0, n_p, n_p, 0x40000000 + it);                   // final pass :383-392
+    a.partition_edges += (int64_t)n_p * c.g.m;
+    a.m_final = c.g.m;
+    if (labels_out) {
+        labels_renumber(c);
+        FC_HIP(hipMemcpyAsync(labels_out, c.lab.p, 4 * (size_t)n_p * c.N, hipMemcpyDeviceToHost, c.stream));
+    }
+    sync(c);
+    if (st) *st = a;  // *_ms / decide_launches stay 0: fc_collect_timing() fills them
+    FC_API_END
+}
+
+}  // extern "C"

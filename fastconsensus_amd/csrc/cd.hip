@@ -1,0 +1,523 @@
+// cd.hip -- replica-batched community detection on the device-resident CSR:
+//   * Louvain level-0 local moving (python-louvain 0.15 `__one_level`, the only level the
+//     reference consumes: partition_at_level(..., 0) at fast_consensus.py:148, :384);
+//   * label propagation (igraph 0.9.7 community_label_propagation(), unweighted as called
+//     at fast_consensus.py:270, :392).
+//
+// Sequential asynchronous order -> bucketed rounds.  Each replica visits its vertices in
+// a per-(replica, iteration, sweep) random order (Feistel bijection); a sweep is split
+// into B buckets of that order; vertices of a bucket decide simultaneously against the
+// state left by the previous buckets, then their moves are applied (integer atomics:
+// deterministic).  Gains use exact int64 arithmetic on the integer edge weights:
+//     G_c = (k_v,c - k_v,own) * 2M + k_v * ((tot_own - k_v) - tot_c)      (= incr * 2M)
+// move iff max_c G_c > 0 (python-louvain's strict `incr > best_increase` from 0); ties
+// broken uniformly at random by a hash (python-louvain shuffles neighbour communities).
+// A sweep ends the run when its predicted modularity gain < 1e-7 (python-louvain __MIN)
+// or nothing moved.  LPA: random dominant label; stop after a sweep in which every
+// visited vertex already held a dominant label (igraph 0.9 `running` flag).
+//
+// Memory layout: replica-major state (lab/tot [n_r][N]), shared read-only CSR.
+// One 16-lane tile per vertex with a 128-slot LDS hash table (degree <= 64); larger
+// rows go to a workgroup-per-vertex kernel (LDS table up to 4096 slots, else global).
+#include <hipcub/hipcub.hpp>
+
+#include "fc_ctx.h"
+#include "fc_device.h"
+
+namespace fc {
+
+template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
+
+static constexpr int TB = 256;
+static constexpr int TILE = 16;
+static constexpr int TILES = TB / TILE;
+static constexpr int HCAP = 128;        // slots per tile table
+static constexpr int LIGHT_MAX_DEG = 64;
+static constexpr int HEAVY_LDS_SLOTS = 4096;
+static constexpr int HEAVY_GRID = 256;
+static constexpr double DQ_SCALE = 1099511627776.0;  // 2^40 fixed point for predicted dQ
+
+static inline unsigned nblk(int64_t n, int tb = TB) {
+    int64_t b = (n + tb - 1) / tb;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+struct CDArgs {
+    int64_t N;
+    int64_t S;          // bucket size (positions per bucket)
+    int n_r, rbase;
+    uint32_t iter;
+    uint64_t seed;
+    const int64_t* rowptr;
+    const int32_t* col;
+    const int32_t* cw;
+    const int64_t* kdeg;
+    int64_t M2;
+    int32_t* lab;
+    int64_t* tot;
+    int32_t* dec;
+    int32_t* active;
+    unsigned long long* dq;      // per replica fixed-point predicted gain (louvain)
+    unsigned long long* moves;   // per replica moves this sweep
+    unsigned long long* unstable;// per replica (lpa)
+    int32_t* heavy;              // (r, p) pairs
+    int32_t* heavy_cnt;
+    int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
+    int64_t heavy_slots;         // slots per global table (power of 2)
+    unsigned long long* stats;   // [0] vertices, [1] entries, [2] distinct candidates (light kernel)
+};
+
+// Block -> (replica, chunk) with all chunks of a replica on as few XCDs as possible
+// (blocks b and b+8 share an XCD under round-robin dispatch; speed only).
+__device__ __forceinline__ void xcd_remap(int64_t b, int64_t total, int64_t per, int* r, int64_t* chunk) {
+    const int64_t xcd = b & 7, q = total >> 3, rem = total & 7;
+    const int64_t w = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+    *r = (int)(w / per);
+    *chunk = w % per;
+}
+
+__device__ __forceinline__ void tbl_insert(int32_t* keys, int32_t* vals, uint32_t mask, int32_t c, int32_t w) {
+    uint32_t h = hash32((uint32_t)c) & mask;
+    while (true) {
+        const int32_t prev = atomicCAS(&keys[h], -1, c);
+        if (prev == -1 || prev == c) { atomicAdd(&vals[h], w); return; }
+        h = (h + 1) & mask;
+    }
+}
+
+// Lexicographic best: larger score, then larger random tie key, then smaller id.
+__device__ __forceinline__ bool better(long long s1, uint32_t h1, int32_t c1, long long s2, uint32_t h2, int32_t c2) {
+    if (s1 != s2) return s1 > s2;
+    if (h1 != h2) return h1 > h2;
+    return c1 < c2;
+}
+__device__ __forceinline__ uint32_t tie_hash(uint32_t tbk, int32_t v, int32_t c) {
+    return hash32(hash32(tbk ^ (uint32_t)v) ^ (uint32_t)c);
+}
+
+// Final decision shared by the light and heavy kernels (runs on one lane).
+// Returns the target community or -1; writes predicted dQ (fixed point) / unstable flag.
+template <bool LOUV>
+__device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t v, int32_t own, long long best_s,
+                                                int32_t best_c, long long kown, int have_best,
+                                                unsigned long long* dq_out, int* unstable_out) {
+    *dq_out = 0;
+    *unstable_out = 0;
+    if (LOUV) {
+        if (!have_best) return -1;
+        const int64_t kv = a.kdeg[v];
+        const int64_t tot_own = a.tot[(int64_t)r * a.N + own];
+        const long long G = best_s - kown * a.M2 + kv * (tot_own - kv);
+        if (G <= 0) return -1;
+        const double dq = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+        *dq_out = (unsigned long long)llrint(dq * DQ_SCALE);
+        return best_c;
+    } else {
+        if (!have_best) return -1;  // isolated vertex keeps its label
+        *unstable_out = (kown != best_s);   // own label not dominant
+        return best_c != own ? best_c : -1;
+    }
+}
+
+template <bool LOUV>
+__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep, int64_t blen,
+                                                      int64_t chunks) {
+    __shared__ int32_t s_key[TILES * HCAP];
+    __shared__ int32_t s_val[TILES * HCAP];
+    __shared__ unsigned long long s_red[TILES][5];
+    const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
+    int r;
+    int64_t chunk;
+    xcd_remap(blockIdx.x, (int64_t)gridDim.x, chunks, &r, &chunk);
+    const int64_t i = chunk * TILES + tile;                // position inside the bucket
+    const int rg = a.rbase + r;
+    const bool rep_on = r < a.n_r && a.active[r];
+    const bool valid = rep_on && i < blen;
+    const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, rg, a.iter, sweep, 1));
+    const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
+    int32_t v = 0;
+    int64_t rb = 0, d = 0;
+    if (valid) {
+        v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
+        rb = a.rowptr[v];
+        d = a.rowptr[v + 1] - rb;
+    }
+    const bool heavy = valid && d > LIGHT_MAX_DEG;
+    const bool work = valid && !heavy && d > 0;
+    int32_t* keys = s_key + tile * HCAP;
+    int32_t* vals = s_val + tile * HCAP;
+    for (int s = lane; s < HCAP; s += TILE) { keys[s] = -1; vals[s] = 0; }
+    __syncthreads();
+    const int32_t* labr = a.lab + (int64_t)r * a.N;
+    if (work) {
+        for (int64_t j = rb + lane; j < rb + d; j += TILE) {
+            const int32_t cj = labr[a.col[j]];
+            tbl_insert(keys, vals, HCAP - 1, cj, LOUV ? a.cw[j] : 1);
+        }
+    }
+    __syncthreads();
+    int32_t own = 0;
+    long long best_s = LLONG_MIN, kown = 0;
+    uint32_t best_h = 0;
+    int32_t best_c = 0x7fffffff;
+    int have = 0, ncand = 0;
+    if (work) {
+        own = labr[v];
+        const int64_t kv = a.kdeg[v];
+        const int64_t* totr = a.tot + (int64_t)r * a.N;
+        for (int s = lane; s < HCAP; s += TILE) {
+            const int32_t key = keys[s];
+            if (key < 0) continue;
+            const int32_t val = vals[s];
+            ++ncand;
+            if (key == own) kown = val;
+            long long sc;
+            if (LOUV) {
+                if (key == own) continue;
+                sc = (long long)val * a.M2 - kv * totr[key];
+            } else {
+                sc = val;
+            }
+            const uint32_t h = tie_hash(tbk, v, key);
+            if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
+        }
+    }
+#pragma unroll
+    for (int off = TILE / 2; off > 0; off >>= 1) {
+        const long long os = __shfl_xor(best_s, off, TILE);
+        const uint32_t oh = (uint32_t)__shfl_xor((int)best_h, off, TILE);
+        const int32_t oc = __shfl_xor(best_c, off, TILE);
+        const int oh_ = __shfl_xor(have, off, TILE);
+        if (oh_ && (!have || better(os, oh, oc, best_s, best_h, best_c))) { best_s = os; best_h = oh; best_c = oc; have = 1; }
+        kown += __shfl_xor(kown, off, TILE);
+        ncand += __shfl_xor(ncand, off, TILE);
+    }
+    unsigned long long dq = 0;
+    int unst = 0;
+    if (lane == 0) {
+        int32_t dcs = -1;
+        if (work) dcs = decide_final<LOUV>(a, r, v, own, best_s, best_c, kown, have, &dq, &unst);
+        if (valid) a.dec[(int64_t)r * a.S + i] = dcs;   // heavy rows: overwritten by k_decide_heavy
+        if (heavy) {
+            const int q = atomicAdd(a.heavy_cnt, 1);
+            a.heavy[2 * q] = r;
+            a.heavy[2 * q + 1] = (int32_t)i;
+        }
+        s_red[tile][0] = dq;
+        s_red[tile][1] = (unsigned long long)unst;
+        s_red[tile][2] = work ? 1ull : 0ull;
+        s_red[tile][3] = work ? (unsigned long long)d : 0ull;
+        s_red[tile][4] = work ? (unsigned long long)ncand : 0ull;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5 && rep_on) {
+        unsigned long long s = 0;
+        for (int t = 0; t < TILES; ++t) s += s_red[t][threadIdx.x];
+        if (s) {
+            if (threadIdx.x == 0) atomicAdd(&a.dq[r], s);
+            else if (threadIdx.x == 1) atomicAdd(&a.unstable[r], s);
+            else atomicAdd(&a.stats[threadIdx.x - 2], s);
+        }
+    }
+}
+
+// Workgroup per high-degree vertex.  Table in LDS when it fits, else a global slice.
+template <bool LOUV>
+__global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int sweep) {
+    __shared__ int32_t s_key[HEAVY_LDS_SLOTS];
+    __shared__ int32_t s_val[HEAVY_LDS_SLOTS];
+    __shared__ long long r_s[TB];
+    __shared__ uint32_t r_h[TB];
+    __shared__ int32_t r_c[TB];
+    __shared__ int r_have[TB];
+    __shared__ long long r_kown[TB];
+    const int cnt = *a.heavy_cnt;
+    for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
+        const int r = a.heavy[2 * item];
+        const int64_t i = a.heavy[2 * item + 1];
+        const int rg = a.rbase + r;
+        const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, rg, a.iter, sweep, 1));
+        const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
+        const int32_t v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
+        const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
+        uint32_t slots = 1;
+        while (slots < 2 * (uint32_t)d) slots <<= 1;
+        int32_t* keys;
+        int32_t* vals;
+        if (slots <= HEAVY_LDS_SLOTS) { keys = s_key; vals = s_val; }
+        else {
+            slots = (uint32_t)a.heavy_slots;
+            keys = a.heavy_scratch + (int64_t)blockIdx.x * 2 * slots;
+            vals = keys + slots;
+        }
+        for (uint32_t s = threadIdx.x; s < slots; s += TB) { keys[s] = -1; vals[s] = 0; }
+        __syncthreads();
+        const int32_t* labr = a.lab + (int64_t)r * a.N;
+        for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB)
+            tbl_insert(keys, vals, slots - 1, labr[a.col[j]], LOUV ? a.cw[j] : 1);
+        __syncthreads();
+        const int32_t own = labr[v];
+        const int64_t kv = a.kdeg[v];
+        const int64_t* totr = a.tot + (int64_t)r * a.N;
+        long long best_s = LLONG_MIN, kown = 0;
+        uint32_t best_h = 0;
+        int32_t best_c = 0x7fffffff;
+        int have = 0;
+        for (uint32_t s = threadIdx.x; s < slots; s += TB) {
+            const int32_t key = keys[s];
+            if (key < 0) continue;
+            const int32_t val = vals[s];
+            if (key == own) kown = val;
+            long long sc;
+            if (LOUV) {
+                if (key == own) continue;
+                sc = (long long)val * a.M2 - kv * totr[key];
+            } else {
+                sc = val;
+            }
+            const uint32_t h = tie_hash(tbk, v, key);
+            if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
+        }
+        r_s[threadIdx.x] = best_s; r_h[threadIdx.x] = best_h; r_c[threadIdx.x] = best_c;
+        r_have[threadIdx.x] = have; r_kown[threadIdx.x] = kown;
+        __syncthreads();
+        for (int o = TB / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) {
+                const int t2 = threadIdx.x + o;
+                if (r_have[t2] && (!r_have[threadIdx.x] ||
+                                   better(r_s[t2], r_h[t2], r_c[t2], r_s[threadIdx.x], r_h[threadIdx.x], r_c[threadIdx.x]))) {
+                    r_s[threadIdx.x] = r_s[t2]; r_h[threadIdx.x] = r_h[t2]; r_c[threadIdx.x] = r_c[t2];
+                    r_have[threadIdx.x] = 1;
+                }
+                r_kown[threadIdx.x] += r_kown[t2];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            unsigned long long dq = 0;
+            int unst = 0;
+            const int32_t dcs = decide_final<LOUV>(a, r, v, own, r_s[0], r_c[0], r_kown[0], r_have[0], &dq, &unst);
+            a.dec[(int64_t)r * a.S + i] = dcs;
+            if (dq) atomicAdd(&a.dq[r], dq);
+            if (unst) atomicAdd(&a.unstable[r], 1ull);
+        }
+        __syncthreads();
+    }
+}
+
+template <bool LOUV>
+__global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, int64_t blen) {
+    const int r = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int moved = 0;
+    if (i < blen && a.active[r]) {
+        const int32_t d = a.dec[(int64_t)r * a.S + i];
+        if (d >= 0) {
+            const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
+            const int32_t v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
+            int32_t* l = a.lab + (int64_t)r * a.N + v;
+            const int32_t old = *l;
+            *l = d;
+            if (LOUV) {
+                const long long kv = a.kdeg[v];
+                atomicAdd((unsigned long long*)&a.tot[(int64_t)r * a.N + old], (unsigned long long)(-kv));
+                atomicAdd((unsigned long long*)&a.tot[(int64_t)r * a.N + d], (unsigned long long)kv);
+            }
+            moved = 1;
+        }
+    }
+    const unsigned long long b = __ballot(moved);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&a.moves[r], (unsigned long long)__popcll(b));
+}
+
+// End of sweep: python-louvain stops a level when the pass gained < 1e-7 modularity or
+// moved nothing; igraph LPA stops when no visited vertex was unstable.
+template <bool LOUV>
+__global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
+        if (a.active[r]) {
+            bool stop;
+            if (LOUV) stop = a.moves[r] == 0 || ((double)a.dq[r] / DQ_SCALE) < 1e-7;
+            else stop = a.unstable[r] == 0;
+            if (stop) a.active[r] = 0;
+            else atomicAdd(&cnt, 1);
+        }
+        a.dq[r] = 0; a.moves[r] = 0; a.unstable[r] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *n_active_out = cnt;
+}
+
+__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab, int64_t* tot, int louv) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (v >= n) return;
+    lab[(int64_t)r * n + v] = (int32_t)v;
+    if (louv) tot[(int64_t)r * n + v] = kdeg[v];
+}
+
+void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+    FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
+    FC_REQUIRE(c.g.rowptr.p, FC_ESTATE, "no graph loaded");
+    const int sl0 = timer_begin(c);
+    const bool louv = algo == FC_ALGO_LOUVAIN;
+    const int64_t N = c.N;
+    Graph& g = c.g;
+    c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
+    c.labT_valid = false;
+    const int B = (int)std::min<int64_t>(c.buckets, N);
+    const int64_t S = (N + B - 1) / B;
+    int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
+    int64_t* tot = louv ? ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
+    int32_t* dec = ensure<int32_t>(c.dec, (size_t)rcount * S);
+    // per-replica: active i32 | dq u64 | moves u64 | unstable u64 | stats u64[4] | n_active i32
+    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * 32 + 128);
+    int32_t* active = (int32_t*)rs;
+    unsigned long long* dq = (unsigned long long*)(rs + (((size_t)rcount * 4 + 15) & ~size_t(15)));
+    unsigned long long* moves = dq + rcount;
+    unsigned long long* unstable = moves + rcount;
+    unsigned long long* stats = unstable + rcount;
+    int32_t* n_active = (int32_t*)(stats + 4);
+    const size_t zero_bytes = (char*)(n_active + 1) - (char*)dq;
+    int32_t* heavy = ensure<int32_t>(c.heavy_list, 2 * (size_t)rcount * S + 2);
+    int32_t* heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
+    int64_t heavy_slots = 1;
+    while (heavy_slots < 2 * (int64_t)g.max_deg) heavy_slots <<= 1;
+    int32_t* hscr = nullptr;
+    if (heavy_slots > HEAVY_LDS_SLOTS) hscr = ensure<int32_t>(c.heavy_scratch, (size_t)HEAVY_GRID * 2 * heavy_slots);
+
+    {
+        std::vector<int32_t> ones(rcount, (g.M2 > 0) ? 1 : 0);
+        FC_HIP(hipMemcpyAsync(active, ones.data(), sizeof(int32_t) * rcount, hipMemcpyHostToDevice, c.stream));
+        sync(c);  // `ones` is pageable host memory
+    }
+    FC_HIP(hipMemsetAsync(dq, 0, zero_bytes, c.stream));
+    dim3 ig(nblk(N), rcount);
+    k_cd_init<<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, tot, louv ? 1 : 0);
+    FC_REQUIRE(!louv || (double)g.max_kdeg * (double)g.M2 < 4.0e18, FC_ELIMIT,
+               "edge weights too large for exact int64 modularity gains");
+
+    CDArgs a;
+    a.N = N; a.S = S; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
+    a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
+    a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
+    a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
+    a.dq = dq; a.moves = moves; a.unstable = unstable;
+    a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
+    a.stats = stats;
+
+    int n_act = (g.M2 > 0) ? rcount : 0;
+    int sweep = 0;
+    for (; sweep < c.max_sweeps && n_act > 0; ++sweep) {
+        c.acc.cd_sweeps += n_act;
+        c.prof.cd_sweeps += n_act;
+        for (int k = 0; k < B; ++k) {
+            const int64_t blen = std::min<int64_t>(S, N - (int64_t)k * S);
+            if (blen <= 0) continue;
+            const int64_t chunks = (blen + TILES - 1) / TILES;
+            FC_HIP(hipMemsetAsync(heavy_cnt, 0, sizeof(int32_t), c.stream));
+            const int ev = timer_begin(c);
+            if (louv) k_decide_light<true><<<(unsigned)(chunks * rcount), TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
+            else k_decide_light<false><<<(unsigned)(chunks * rcount), TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
+            timer_end(c, 4, ev);
+            if (g.max_deg > LIGHT_MAX_DEG) {
+                if (louv) k_decide_heavy<true><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
+                else k_decide_heavy<false><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
+            }
+            dim3 ag(nblk(blen), rcount);
+            if (louv) k_apply<true><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
+            else k_apply<false><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
+        }
+        if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
+        else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
+        FC_HIP(hipMemcpyAsync(c.hpin, n_active, sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        n_act = ((int32_t*)c.hpin)[0];
+    }
+    // light-kernel traffic counters for the roofline model
+    FC_HIP(hipMemcpyAsync(c.hpin, stats, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    // algorithmic bytes of the light decide kernel: per vertex rowptr 16 + kdeg 8 + own
+    // label 4 + own tot 8 + decision 4; per adjacency entry col 4 + weight 4 + label 4;
+    // per distinct candidate community its tot 8 (louvain).
+    const int64_t db = c.hpin[0] * (louv ? 40 : 24) + c.hpin[1] * (louv ? 12 : 8) + (louv ? c.hpin[2] * 8 : 0);
+    for (fc_stats* s : {&c.acc, &c.prof}) {
+        s->cd_vertex_visits += c.hpin[0];
+        s->cd_edge_visits += c.hpin[1];
+        s->decide_bytes += db;
+    }
+    timer_end(c, 0, sl0);
+}
+
+// ------------------------------------------------------------------ transpose / renumber
+// lab [n_r][N] -> labT [N][ldT]  (64x64 tiles through LDS, both sides coalesced)
+__global__ __launch_bounds__(256) void k_transpose(int64_t N, int n_r, int ldT, const int32_t* lab, int32_t* labT) {
+    __shared__ int32_t t[64][65];
+    const int64_t v0 = (int64_t)blockIdx.x * 64;
+    const int r0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    for (int rr = ty; rr < 64; rr += 4) {
+        const int r = r0 + rr;
+        const int64_t v = v0 + tx;
+        if (r < n_r && v < N) t[rr][tx] = lab[(int64_t)r * N + v];
+    }
+    __syncthreads();
+    for (int vv = ty; vv < 64; vv += 4) {
+        const int64_t v = v0 + vv;
+        const int r = r0 + tx;
+        if (v < N && r < n_r) labT[v * ldT + r] = t[tx][vv];
+    }
+}
+void labels_transpose(Ctx& c) {
+    FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings");
+    c.ldT = (c.n_r + 3) & ~3;
+    int32_t* labT = ensure<int32_t>(c.labT, (size_t)c.N * c.ldT);
+    dim3 grid(nblk(c.N, 64), (c.n_r + 63) / 64);
+    k_transpose<<<grid, TB, 0, c.stream>>>(c.N, c.n_r, c.ldT, c.lab.as<int32_t>(), labT);
+    c.labT_valid = true;
+}
+
+__global__ void k_first_init(int64_t total, int32_t* first) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) first[i] = 0x7fffffff;
+}
+__global__ void k_first_min(int64_t N, const int32_t* lab, int32_t* first) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (v < N) atomicMin(&first[(int64_t)r * N + lab[(int64_t)r * N + v]], (int32_t)v);
+}
+__global__ void k_first_flag(int64_t N, int64_t total, const int32_t* lab, const int32_t* first, int32_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > total) return;
+    if (i == total) { flag[i] = 0; return; }
+    const int64_t r = i / N, v = i % N;
+    flag[i] = first[r * N + lab[i]] == (int32_t)v ? 1 : 0;
+}
+__global__ void k_relabel(int64_t N, int32_t* lab, const int32_t* first, const int32_t* rank) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    if (v >= N) return;
+    const int64_t base = (int64_t)r * N;
+    lab[base + v] = rank[base + first[base + lab[base + v]]] - rank[base];
+}
+// Community ids -> 0..k-1 in order of each community's first node (node order).
+void labels_renumber(Ctx& c) {
+    const int64_t N = c.N, total = (int64_t)c.n_r * N;
+    FC_REQUIRE(total < (int64_t(1) << 31), FC_ELIMIT, "n_p * n too large for renumbering");
+    int32_t* first = ensure<int32_t>(c.dec, total + 1);     // CD scratch is free now
+    int32_t* flag = ensure<int32_t>(c.wnew, total + 1);
+    int32_t* rank = ensure<int32_t>(c.hit, total + 1);
+    k_first_init<<<nblk(total), TB, 0, c.stream>>>(total, first);
+    dim3 g(nblk(N), c.n_r);
+    k_first_min<<<g, TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), first);
+    k_first_flag<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), first, flag);
+    exclusive_scan(c, flag, rank, total + 1);
+    k_relabel<<<g, TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), first, rank);
+    c.labT_valid = false;
+}
+
+}  // namespace fc

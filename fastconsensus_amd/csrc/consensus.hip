@@ -1,0 +1,470 @@
+// consensus.hip -- the consensus-graph update of fast_consensus():
+//   per-edge co-membership rule + tau threshold + delta check  (fast_consensus.py:150-173,
+//   :273-288, check_consensus_graph :17-37), triadic closure (:175-190, :292-304) and
+//   isolate repair (:193-195).  Integer/byte work, HBM/gather bound: no MFMA.
+#include <hipcub/hipcub.hpp>
+
+#include "fc_ctx.h"
+#include "fc_device.h"
+
+namespace fc {
+
+template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
+template <class K, class V>
+void sort_pairs_public(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit);
+
+static constexpr int TB = 256;
+static inline unsigned nblk(int64_t n, int tb = TB) {
+    int64_t b = (n + tb - 1) / tb;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+// ------------------------------------------------------------------ consensus partial
+// One edge per group of G lanes; each lane compares 4 replicas per 16-byte load of the
+// node-major label rows labT[node][ldT] (a 64-replica row is 256 B = one coalesced load
+// by 16 lanes).  LOUVAIN: highest global replica index whose labels split (u,v), or -1.
+// COUNT: number of replicas co-clustering (u,v).
+template <int G, bool LOUVAIN>
+__global__ __launch_bounds__(256) void k_pair_partial(int64_t m, const int32_t* __restrict__ eu,
+                                                      const int32_t* __restrict__ ev,
+                                                      const int32_t* __restrict__ labT, int ldT, int n_r,
+                                                      int rbase, int32_t* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t e = gid / G;
+    const int l = (int)(gid % G);
+    if (e >= m) return;  // whole groups exit together (G divides 64)
+    const int4* ru = reinterpret_cast<const int4*>(labT + (int64_t)eu[e] * ldT);
+    const int4* rv = reinterpret_cast<const int4*>(labT + (int64_t)ev[e] * ldT);
+    int res = LOUVAIN ? -1 : 0;
+    for (int q = l; 4 * q < n_r; q += G) {
+        const int4 a = ru[q], b = rv[q];
+        const int base = 4 * q;
+        if (LOUVAIN) {
+            if (base + 3 < n_r && a.w != b.w) res = max(res, base + 3);
+            else if (base + 2 < n_r && a.z != b.z) res = max(res, base + 2);
+            else if (base + 1 < n_r && a.y != b.y) res = max(res, base + 1);
+            else if (a.x != b.x) res = max(res, base);
+        } else {
+            res += (a.x == b.x);
+            if (base + 1 < n_r) res += (a.y == b.y);
+            if (base + 2 < n_r) res += (a.z == b.z);
+            if (base + 3 < n_r) res += (a.w == b.w);
+        }
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) {
+        int o = __shfl_xor(res, off, G);
+        res = LOUVAIN ? max(res, o) : res + o;
+    }
+    if (l == 0) out[e] = LOUVAIN ? (res < 0 ? -1 : res + rbase) : res;
+}
+
+template <bool LOUVAIN>
+static void launch_pair_partial(Ctx& c, int64_t m, const int32_t* eu, const int32_t* ev, int32_t* out) {
+    if (m <= 0) return;
+    const int chunks = (c.n_r + 3) / 4;
+    int G = 1;
+    while (G < chunks && G < 16) G <<= 1;
+    const int64_t threads = m * G;
+    const unsigned grid = nblk(threads);
+    const int32_t* labT = c.labT.as<int32_t>();
+    switch (G) {
+        case 1: k_pair_partial<1, LOUVAIN><<<grid, TB, 0, c.stream>>>(m, eu, ev, labT, c.ldT, c.n_r, c.rbase, out); break;
+        case 2: k_pair_partial<2, LOUVAIN><<<grid, TB, 0, c.stream>>>(m, eu, ev, labT, c.ldT, c.n_r, c.rbase, out); break;
+        case 4: k_pair_partial<4, LOUVAIN><<<grid, TB, 0, c.stream>>>(m, eu, ev, labT, c.ldT, c.n_r, c.rbase, out); break;
+        case 8: k_pair_partial<8, LOUVAIN><<<grid, TB, 0, c.stream>>>(m, eu, ev, labT, c.ldT, c.n_r, c.rbase, out); break;
+        default: k_pair_partial<16, LOUVAIN><<<grid, TB, 0, c.stream>>>(m, eu, ev, labT, c.ldT, c.n_r, c.rbase, out); break;
+    }
+}
+
+void consensus_partial(Ctx& c, int algo, int32_t* out) {
+    FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings: run fc_cd or fc_set_labels first");
+    if (!c.labT_valid) labels_transpose(c);
+    const int sl = timer_begin(c);
+    if (algo == FC_ALGO_LOUVAIN)
+        launch_pair_partial<true>(c, c.g.m, c.g.eu.as<int32_t>(), c.g.ev.as<int32_t>(), out);
+    else
+        launch_pair_partial<false>(c, c.g.m, c.g.eu.as<int32_t>(), c.g.ev.as<int32_t>(), out);
+    timer_end(c, 1, sl);
+}
+
+// ------------------------------------------------------------------ consensus apply
+// Closed form of the Louvain rule (fast_consensus.py:150-159), proven equal to the
+// literal loop in tests/test_oracle_golden.py: w in {0,n_p} -> 0; no split -> n_p;
+// else w + (n_p - 1 - k_last).  LPM (:273-280): the co-membership count.
+// keep iff !(w' < tau*n_p) in float64 (:165, :286).  Counts kept and "unconverged"
+// (w' not in {0, n_p}, check_consensus_graph :30-32) per block -> one atomic per block.
+__global__ __launch_bounds__(256) void k_consensus_apply(int louvain, int64_t m, int n_p, double cut,
+                                                         const int32_t* __restrict__ ew,
+                                                         const int32_t* __restrict__ part,
+                                                         int32_t* __restrict__ wnew, int64_t* __restrict__ flag,
+                                                         unsigned long long* counters) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int keep = 0, unc = 0;
+    if (e < m) {
+        int nw;
+        if (louvain) {
+            const int w = ew[e];
+            const int k = part[e];
+            nw = (w == 0 || w == n_p) ? 0 : (k < 0 ? n_p : w + (n_p - 1 - k));
+        } else {
+            nw = part[e];
+        }
+        keep = !((double)nw < cut);
+        unc = keep && nw != 0 && nw != n_p;
+        wnew[e] = nw;
+        flag[e] = keep;
+    }
+    // wave64 ballot counts, then one atomic per wave
+    const unsigned long long bk = __ballot(keep), bu = __ballot(unc);
+    if ((threadIdx.x & 63) == 0) {
+        if (bk) atomicAdd(&counters[0], (unsigned long long)__popcll(bk));
+        if (bu) atomicAdd(&counters[1], (unsigned long long)__popcll(bu));
+    }
+}
+
+__global__ void k_scatter_kept(int64_t m, const int64_t* flag, const int64_t* pos, const int32_t* eu,
+                               const int32_t* ev, const int32_t* wnew, const int64_t* eage, int32_t* ku,
+                               int32_t* kv, int32_t* kw, int64_t* kage) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m || !flag[e]) return;
+    const int64_t p = pos[e];
+    ku[p] = eu[e]; kv[p] = ev[e]; kw[p] = wnew[e]; kage[p] = eage[e];
+}
+// Kept CSR = the current CSR filtered by the edge keep flags (rows stay sorted).
+__global__ void k_csr_flags(int64_t m2, const int32_t* ceid, const int64_t* eflag, int64_t* f2) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m2) f2[j] = eflag[ceid[j]];
+    else if (j == m2) f2[j] = 0;
+}
+__global__ void k_csr_compact(int64_t m2, const int64_t* f2, const int64_t* p2, const int32_t* col,
+                              int32_t* kcol) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m2 && f2[j]) kcol[p2[j]] = col[j];
+}
+__global__ void k_krowptr(int64_t n, const int64_t* rowptr, const int64_t* p2, int64_t* krowptr) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x <= n) krowptr[x] = p2[rowptr[x]];
+}
+
+void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept_out,
+                     int64_t* unconv_out) {
+    const int sl = timer_begin(c);
+    Graph& g = c.g;
+    const int64_t m = g.m, cap = m + 1;
+    int32_t* wnew = ensure<int32_t>(c.wnew, cap);
+    int64_t* flag = ensure<int64_t>(c.flag, 2 * cap + 1);
+    int64_t* pos = ensure<int64_t>(c.pos, 2 * cap + 1);
+    unsigned long long* ctr = (unsigned long long*)ensure<int64_t>(c.counters, 16);
+    FC_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(int64_t), c.stream));
+    const double cut = tau * (double)n_p;  // Python float64 product (fast_consensus.py:165)
+    if (m > 0)
+        k_consensus_apply<<<nblk(m), TB, 0, c.stream>>>(algo == FC_ALGO_LOUVAIN, m, n_p, cut, g.ew.as<int32_t>(),
+                                                         partial, wnew, flag, ctr);
+    FC_HIP(hipMemsetAsync(flag + m, 0, sizeof(int64_t), c.stream));
+    exclusive_scan(c, flag, pos, m + 1);
+    FC_HIP(hipMemcpyAsync(c.hpin, ctr, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    const int64_t kept = c.hpin[0], unconv = c.hpin[1];
+    c.kept_m = kept;
+    const int64_t kc = kept > 0 ? kept : 1;
+    int32_t* ku = ensure<int32_t>(c.ku, kc);
+    int32_t* kv = ensure<int32_t>(c.kv, kc);
+    int32_t* kw = ensure<int32_t>(c.kw, kc);
+    int64_t* kage = ensure<int64_t>(c.kage, kc);
+    if (m > 0)
+        k_scatter_kept<<<nblk(m), TB, 0, c.stream>>>(m, flag, pos, g.eu.as<int32_t>(), g.ev.as<int32_t>(), wnew,
+                                                      g.eage.as<int64_t>(), ku, kv, kw, kage);
+    // kept CSR (for closure sampling and has_edge); flag[] holds edge flags, reuse wnew-free scratch
+    const int64_t m2 = 2 * m;
+    int64_t* f2 = ensure<int64_t>(c.nodetmp3, m2 + 1 > 2 * (c.N + 1) ? m2 + 1 : 2 * (c.N + 1));
+    int64_t* p2 = ensure<int64_t>(c.ckey2, m2 + 1);
+    k_csr_flags<<<nblk(m2 + 1), TB, 0, c.stream>>>(m2, g.ceid.as<int32_t>(), flag, f2);
+    exclusive_scan(c, f2, p2, m2 + 1);
+    int32_t* kcol = ensure<int32_t>(c.kcol, 2 * kc);
+    int64_t* krowptr = ensure<int64_t>(c.krowptr, c.N + 1);
+    k_csr_compact<<<nblk(m2), TB, 0, c.stream>>>(m2, f2, p2, g.col.as<int32_t>(), kcol);
+    k_krowptr<<<nblk(c.N + 1), TB, 0, c.stream>>>(c.N, g.rowptr.as<int64_t>(), p2, krowptr);
+    if (kept_out) *kept_out = kept;
+    if (unconv_out) *unconv_out = unconv;
+    timer_end(c, 1, sl);
+}
+
+// ------------------------------------------------------------------ closure
+__device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int32_t* col, int32_t a,
+                                                int32_t b) {
+    int64_t lo = rowptr[a], hi = rowptr[a + 1];
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t x = col[mid];
+        if (x < b) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < rowptr[a + 1] && col[lo] == b;
+}
+
+// Attempt t (fast_consensus.py:175-184): node uniform over all N (np.random.choice over
+// nextgraph.nodes(), :177); if it has >= 2 neighbours in the post-threshold graph, two
+// distinct neighbours uniformly (random.sample, :181); candidate iff not an edge (:183).
+// Samples are drawn from the post-threshold graph, not the growing one: statistical
+// parity.  Invalid attempts get the sentinel key (sorted to the end).
+__global__ __launch_bounds__(256) void k_closure_sample(int64_t attempts, int64_t n, uint32_t k0, uint32_t k1,
+                                                        uint32_t iter, const int64_t* __restrict__ krowptr,
+                                                        const int32_t* __restrict__ kcol, int bits,
+                                                        uint64_t* key, int64_t* val) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= attempts) return;
+    const uint64_t sent = (1ull << (2 * bits)) - 1ull;
+    U4 ctr = {(uint32_t)t, (uint32_t)(t >> 32), iter, 0x5eedu};
+    const U4 r = philox(ctr, k0, k1);
+    const int32_t x = (int32_t)below(r.x, (uint32_t)n);
+    const int64_t rb = krowptr[x];
+    const int64_t d = krowptr[x + 1] - rb;
+    uint64_t k = sent;
+    if (d >= 2) {
+        const uint32_t i1 = below(r.y, (uint32_t)d);
+        uint32_t i2 = below(r.z, (uint32_t)(d - 1));
+        if (i2 >= i1) ++i2;
+        const int32_t a = kcol[rb + i1], b = kcol[rb + i2];
+        const int32_t u = a < b ? a : b, v = a < b ? b : a;
+        if (!has_edge_sorted(krowptr, kcol, u, v)) k = ((uint64_t)u << bits) | (uint64_t)v;
+    }
+    key[t] = k;
+    val[t] = t;
+}
+__global__ void k_pairs_keys(int64_t np_, const int32_t* pairs, const int64_t* krowptr, const int32_t* kcol,
+                             int bits, uint64_t* key, int64_t* val) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= np_) return;
+    const uint64_t sent = (1ull << (2 * bits)) - 1ull;
+    const int32_t a = pairs[2 * t], b = pairs[2 * t + 1];
+    uint64_t k = sent;
+    if (a != b) {
+        const int32_t u = a < b ? a : b, v = a < b ? b : a;
+        if (!has_edge_sorted(krowptr, kcol, u, v)) k = ((uint64_t)u << bits) | (uint64_t)v;
+    }
+    key[t] = k;
+    val[t] = t;
+}
+// first occurrence of each candidate (stable radix sort keeps sample order in a key run)
+__global__ void k_first_flags(int64_t n, const uint64_t* key, int bits, int64_t* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) { flag[i] = 0; return; }
+    const uint64_t sent = (1ull << (2 * bits)) - 1ull;
+    flag[i] = (key[i] != sent && (i == 0 || key[i - 1] != key[i])) ? 1 : 0;
+}
+__global__ void k_scatter_cand(int64_t n, const int64_t* flag, const int64_t* pos, const uint64_t* key,
+                               const int64_t* val, int bits, int64_t age_base, int32_t* cu, int32_t* cv,
+                               int64_t* cage) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    const int64_t p = pos[i];
+    cu[p] = (int32_t)(key[i] >> bits);
+    cv[p] = (int32_t)(key[i] & ((1ull << bits) - 1ull));
+    cage[p] = age_base + val[i];  // creation order = first sample index
+}
+
+static void finish_candidates(Ctx& c, int64_t n, uint64_t* k1, int64_t* v1, int iteration) {
+    const int64_t cap = n > 0 ? n : 1;
+    uint64_t* k2 = ensure<uint64_t>(c.mkey2, cap);
+    int64_t* v2 = ensure<int64_t>(c.midx2, cap);
+    sort_pairs_public(c, (const uint64_t*)k1, k2, (const int64_t*)v1, v2, n, 2 * c.key_bits);
+    int64_t* fl = ensure<int64_t>(c.flag, n + 1 > 2 * (c.g.m + 1) + 1 ? n + 1 : 2 * (c.g.m + 1) + 1);
+    int64_t* ps = ensure<int64_t>(c.pos, n + 1 > 2 * (c.g.m + 1) + 1 ? n + 1 : 2 * (c.g.m + 1) + 1);
+    k_first_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, k2, c.key_bits, fl);
+    exclusive_scan(c, fl, ps, n + 1);
+    c.n_cand = read_i64(c, ps + n);
+    // closure + (up to N) repair edges share the "added" arrays
+    const int64_t acap = c.n_cand + c.N + 1;
+    int32_t* cu = ensure<int32_t>(c.cu, acap);
+    int32_t* cv = ensure<int32_t>(c.cv, acap);
+    ensure<int32_t>(c.cw2, acap);
+    int64_t* cage = ensure<int64_t>(c.cage, acap);
+    const int64_t base = (int64_t)(iteration + 1) << AGE_ITER_SHIFT;
+    k_scatter_cand<<<nblk(n), TB, 0, c.stream>>>(n, fl, ps, k2, v2, c.key_bits, base, cu, cv, cage);
+}
+
+void closure_sample(Ctx& c, int64_t attempts, int iteration) {
+    const int sl = timer_begin(c);
+    const int64_t cap = attempts > 0 ? attempts : 1;
+    uint64_t* k1 = ensure<uint64_t>(c.mkey, cap);
+    int64_t* v1 = ensure<int64_t>(c.midx, cap);
+    const uint64_t s = mix64(c.seed ^ 0xC105u);
+    if (attempts > 0)
+        k_closure_sample<<<nblk(attempts), TB, 0, c.stream>>>(attempts, c.N, (uint32_t)s, (uint32_t)(s >> 32),
+                                                             (uint32_t)iteration, c.krowptr.as<int64_t>(),
+                                                             c.kcol.as<int32_t>(), c.key_bits, k1, v1);
+    finish_candidates(c, attempts, k1, v1, iteration);
+    timer_end(c, 2, sl);
+}
+
+void closure_from_pairs(Ctx& c, int64_t npairs, const int32_t* pairs, int iteration) {
+    const int64_t cap = npairs > 0 ? npairs : 1;
+    int32_t* dp = ensure<int32_t>(c.ckey, 2 * cap);
+    if (npairs > 0) FC_HIP(hipMemcpyAsync(dp, pairs, sizeof(int32_t) * 2 * npairs, hipMemcpyHostToDevice, c.stream));
+    uint64_t* k1 = ensure<uint64_t>(c.mkey, cap);
+    int64_t* v1 = ensure<int64_t>(c.midx, cap);
+    if (npairs > 0)
+        k_pairs_keys<<<nblk(npairs), TB, 0, c.stream>>>(npairs, dp, c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
+                                                         c.key_bits, k1, v1);
+    finish_candidates(c, npairs, k1, v1, iteration);
+}
+
+void closure_partial(Ctx& c, int32_t* out) {
+    if (!c.labT_valid) labels_transpose(c);
+    launch_pair_partial<false>(c, c.n_cand, c.cu.as<int32_t>(), c.cv.as<int32_t>(), out);
+}
+
+// ------------------------------------------------------------------ repair
+__global__ void k_closure_weights(int64_t n, int louvain, const int32_t* counts, int32_t* cw) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) cw[i] = louvain ? counts[i] : 0;  // lpm closure weight is always 0 (:302-304)
+}
+__global__ void k_deg_next(int64_t n, const int64_t* krowptr, int64_t* deg) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < n) deg[x] = krowptr[x + 1] - krowptr[x];
+}
+__global__ void k_deg_add(int64_t k, const int32_t* cu, const int32_t* cv, int64_t* deg) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    atomicAdd((unsigned long long*)&deg[cu[i]], 1ull);
+    atomicAdd((unsigned long long*)&deg[cv[i]], 1ull);
+}
+__global__ void k_iso_flags(int64_t n, const int64_t* deg, const int64_t* rowptr, int64_t* flag) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x > n) return;
+    // isolated in nextgraph and has a neighbour in graph (else the reference raises)
+    flag[x] = (x < n && deg[x] == 0 && rowptr[x + 1] > rowptr[x]) ? 1 : 0;
+}
+// Target of isolated node x: its neighbour in the OLD graph with the minimum old weight;
+// ties -> first in networkx adjacency order = earlier neighbours ascending, then later
+// neighbours by creation age (proof: DESIGN.md; pinned by tests/golden adj snapshots).
+__global__ void k_iso_target(int64_t n, const int64_t* flag, const int64_t* pos, const int64_t* rowptr,
+                             const int32_t* col, const int32_t* cw, const int32_t* ceid, const int64_t* eage,
+                             int32_t* iso, int64_t* isoidx, int32_t* target, int32_t* tw) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    if (!flag[x]) { isoidx[x] = -1; return; }
+    const int64_t i = pos[x];
+    isoidx[x] = i;
+    iso[i] = (int32_t)x;
+    int32_t bw = 0x7fffffff, by = -1;
+    int64_t bs = 0x7fffffffffffffffll;
+    for (int64_t j = rowptr[x]; j < rowptr[x + 1]; ++j) {
+        const int32_t y = col[j], w = cw[j];
+        const int64_t sec = (y < x) ? (int64_t)y : ((int64_t)1 << 62) + eage[ceid[j]];
+        if (w < bw || (w == bw && sec < bs)) { bw = w; bs = sec; by = y; }
+    }
+    target[i] = by;
+    tw[i] = bw;
+}
+// Sequential live-isolates semantics (nx.isolates is a lazy generator): x is skipped iff
+// an earlier repaired node chose x.  Resolved by Jacobi sweeps over the DAG x' -> T(x').
+__global__ void k_iso_hit(int64_t k, const int32_t* iso, const int64_t* isoidx, const int32_t* target,
+                          const int32_t* active, int32_t* hit) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k || !active[i]) return;
+    const int32_t y = target[i];
+    const int64_t j = isoidx[y];
+    if (j >= 0 && y > iso[i]) hit[j] = 1;
+}
+__global__ void k_iso_update(int64_t k, const int32_t* hit, int32_t* active, int32_t* changed) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const int32_t a = hit[i] ? 0 : 1;
+    if (a != active[i]) { active[i] = a; *changed = 1; }
+}
+__global__ void k_iso_flag64(int64_t k, const int32_t* active, int64_t* f) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) f[i] = active[i];
+    else if (i == k) f[i] = 0;
+}
+__global__ void k_repair_edges(int64_t k, const int64_t* f, const int64_t* p, const int32_t* iso,
+                               const int32_t* target, const int32_t* tw, int64_t base, int64_t off, int32_t* cu,
+                               int32_t* cv, int32_t* cw, int64_t* cage) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k || !f[i]) return;
+    const int32_t x = iso[i], y = target[i];
+    const int64_t q = off + p[i];
+    cu[q] = x < y ? x : y;
+    cv[q] = x < y ? y : x;
+    cw[q] = tw[i];                 // carries the old weight (:195)
+    cage[q] = base + AGE_REPAIR_OFFSET + x;
+}
+
+static int64_t repair(Ctx& c, int iteration) {
+    const int64_t n = c.N;
+    Graph& g = c.g;  // still the OLD graph here
+    int64_t* deg = ensure<int64_t>(c.deg_next, n + 1);
+    k_deg_next<<<nblk(n), TB, 0, c.stream>>>(n, c.krowptr.as<int64_t>(), deg);
+    if (c.n_cand > 0) k_deg_add<<<nblk(c.n_cand), TB, 0, c.stream>>>(c.n_cand, c.cu.as<int32_t>(), c.cv.as<int32_t>(), deg);
+    int64_t* fl = ensure<int64_t>(c.nodetmp, n + 1);
+    int64_t* ps = ensure<int64_t>(c.nodetmp2, n + 1);
+    k_iso_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, deg, g.rowptr.as<int64_t>(), fl);
+    exclusive_scan(c, fl, ps, n + 1);
+    const int64_t k = read_i64(c, ps + n);
+    c.n_iso = k;
+    if (k == 0) return 0;
+    int32_t* iso = ensure<int32_t>(c.iso, k);
+    int64_t* isoidx = ensure<int64_t>(c.isoflag, n);
+    int32_t* target = ensure<int32_t>(c.target, k);
+    int32_t* tw = ensure<int32_t>(c.tw, k);
+    k_iso_target<<<nblk(n), TB, 0, c.stream>>>(n, fl, ps, g.rowptr.as<int64_t>(), g.col.as<int32_t>(),
+                                                g.cw.as<int32_t>(), g.ceid.as<int32_t>(), g.eage.as<int64_t>(), iso,
+                                                isoidx, target, tw);
+    int32_t* active = ensure<int32_t>(c.active, k);
+    int32_t* hit = ensure<int32_t>(c.hit, k + 1);
+    int32_t* changed = hit + k;
+    FC_HIP(hipMemsetAsync(active, 0, sizeof(int32_t) * k, c.stream));  // all-zero start: first pass flips all
+    for (int64_t it = 0; it <= k + 1; ++it) {
+        FC_HIP(hipMemsetAsync(hit, 0, sizeof(int32_t) * (k + 1), c.stream));
+        if (it > 0) k_iso_hit<<<nblk(k), TB, 0, c.stream>>>(k, iso, isoidx, target, active, hit);
+        k_iso_update<<<nblk(k), TB, 0, c.stream>>>(k, hit, active, changed);
+        int32_t ch = 0;
+        FC_HIP(hipMemcpyAsync(&ch, changed, sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        if (!ch && it > 0) break;
+    }
+    int64_t* f = ensure<int64_t>(c.nodetmp, k + 1);   // fl no longer needed
+    int64_t* p = ensure<int64_t>(c.nodetmp2, k + 1);
+    k_iso_flag64<<<nblk(k + 1), TB, 0, c.stream>>>(k, active, f);
+    exclusive_scan(c, f, p, k + 1);
+    const int64_t nrep = read_i64(c, p + k);
+    const int64_t base = (int64_t)(iteration + 1) << AGE_ITER_SHIFT;
+    k_repair_edges<<<nblk(k), TB, 0, c.stream>>>(k, f, p, iso, target, tw, base, c.n_cand, c.cu.as<int32_t>(),
+                                                  c.cv.as<int32_t>(), c.cw2.as<int32_t>(), c.cage.as<int64_t>());
+    return nrep;
+}
+
+// ------------------------------------------------------------------ convergence check
+__global__ __launch_bounds__(256) void k_count_unconv(int64_t m, int n_p, const int32_t* w,
+                                                      unsigned long long* out) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int u = (e < m) && w[e] != 0 && w[e] != n_p;
+    const unsigned long long b = __ballot(u);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+}
+int64_t count_unconverged(Ctx& c, const int32_t* w, int64_t m, int n_p) {
+    unsigned long long* ctr = (unsigned long long*)ensure<int64_t>(c.counters, 16) + 4;
+    FC_HIP(hipMemsetAsync(ctr, 0, sizeof(int64_t), c.stream));
+    if (m > 0) k_count_unconv<<<nblk(m), TB, 0, c.stream>>>(m, n_p, w, ctr);
+    return read_i64(c, (const int64_t*)ctr);
+}
+
+void closure_apply(Ctx& c, int algo, int n_p, const int32_t* counts, int iteration) {
+    int sl = timer_begin(c);
+    if (c.n_cand > 0)
+        k_closure_weights<<<nblk(c.n_cand), TB, 0, c.stream>>>(c.n_cand, algo == FC_ALGO_LOUVAIN, counts,
+                                                               c.cw2.as<int32_t>());
+    int64_t nrep = 0;
+    if (algo == FC_ALGO_LOUVAIN) nrep = repair(c, iteration);  // lpm has no repair (:260-310)
+    timer_end(c, 2, sl);
+    sl = timer_begin(c);
+    graph_merge_next(c, c.n_cand + nrep);
+    timer_end(c, 3, sl);
+    (void)n_p;
+}
+
+}  // namespace fc

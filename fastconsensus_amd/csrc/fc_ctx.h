@@ -1,0 +1,149 @@
+// fc_ctx.h -- engine context: device-resident graph, replica state and scratch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+#include "../../include/fastconsensus_amd.h"
+
+namespace fc {
+
+void set_error(const std::string& msg);
+
+struct FcError {
+    int code;
+    std::string msg;
+};
+
+#define FC_HIP(call)                                                                       \
+    do {                                                                                   \
+        hipError_t _e = (call);                                                            \
+        if (_e != hipSuccess)                                                              \
+            throw ::fc::FcError{FC_EHIP, std::string(#call) + ": " + hipGetErrorString(_e)}; \
+    } while (0)
+#define FC_REQUIRE(cond, code, msg)                      \
+    do {                                                 \
+        if (!(cond)) throw ::fc::FcError{(code), (msg)}; \
+    } while (0)
+
+// Growable device buffer (never shrinks; grows by 1.5x).
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    void ensure(size_t need) {
+        if (need <= bytes) return;
+        size_t nb = bytes ? bytes + bytes / 2 : 0;
+        if (nb < need) nb = need;
+        nb = (nb + 255) & ~size_t(255);
+        if (p) FC_HIP(hipFree(p));
+        p = nullptr;
+        FC_HIP(hipMalloc(&p, nb));
+        bytes = nb;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+// Canonical edge list (u < v in node order, sorted by (u,v)) + symmetric CSR with
+// every row sorted ascending.
+struct Graph {
+    int64_t m = 0;
+    DevBuf eu, ev, ew, eage;        // int32, int32, int32, int64  [m]
+    DevBuf rowptr, col, cw, ceid;   // int64 [N+1], int32 [2m] x3
+    DevBuf kdeg;                    // int64 [N] weighted degree
+    int64_t M2 = 0;                 // sum of kdeg = 2 * total weight
+    int32_t max_deg = 0;
+    int64_t max_kdeg = 0;
+    void release() {
+        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &kdeg};
+        for (auto* x : b) x->release();
+    }
+};
+
+struct Timer {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    std::vector<std::pair<int, int>> spans[5];  // cd, consensus, closure, rebuild, decide
+    size_t next = 0;
+};
+
+struct Ctx {
+    int device = 0;
+    uint64_t seed = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    int64_t N = 0, m_original = 0;
+    int key_bits = 1;               // bits to hold a node id (N <= 2^key_bits)
+    Graph g;                        // `graph` (fast_consensus.py:131)
+    Graph g0;                       // pristine G as loaded (never modified, like the caller's G)
+    // replica state (replica-major [n_r][N])
+    int n_r = 0, rbase = 0, n_p_total = 0;
+    DevBuf lab, tot, dec, labT;     // int32 [n_r][N], int64 [n_r][N], int32 [n_r][S], int32 [N][ldT]
+    int ldT = 0;
+    bool labT_valid = false;
+    DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable
+    DevBuf heavy_list, heavy_cnt, heavy_scratch;
+    // consensus / kept graph
+    DevBuf wnew, flag, pos;         // int32 [m] (flag/pos also reused for 2m CSR compaction)
+    int64_t kept_m = 0;
+    DevBuf ku, kv, kw, kage;        // kept canonical list
+    DevBuf krowptr, kcol;           // kept CSR (sorted rows)
+    DevBuf counters;                // int64 scratch counters
+    DevBuf hcounters;               // (pinned host) mirror
+    // closure / repair / merge
+    int64_t n_cand = 0;
+    DevBuf ckey, cval, ckey2, cval2;  // uint64 keys + int64 sample index
+    DevBuf cu, cv, cw2, cage;       // closure edges
+    DevBuf deg_next, iso, isoflag, target, tw, active, active2, hit;
+    int64_t n_iso = 0;
+    DevBuf mkey, mkey2, midx, midx2;  // merge sort
+    DevBuf sort_tmp;                // hipcub temporary storage
+    DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
+    DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)
+    // params
+    int buckets = 32, max_sweeps = 200, max_iters = 1000;
+    Timer timer;
+    fc_stats acc{};                 // accumulated during a run (fc_run)
+    fc_stats prof{};                // accumulated since the last fc_collect_timing
+    int64_t* hpin = nullptr;        // pinned host scratch (64 int64)
+};
+
+// graph.cpp
+void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v);
+void graph_build_csr(Ctx& c, Graph& g);
+void graph_merge_next(Ctx& c, int64_t n_added);
+void graph_copy(Ctx& c, Graph& dst, const Graph& src);
+// cd.cpp
+void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
+void labels_transpose(Ctx& c);
+void labels_renumber(Ctx& c);
+// consensus.cpp
+void consensus_partial(Ctx& c, int algo, int32_t* out);
+void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept,
+                     int64_t* unconv);
+void closure_sample(Ctx& c, int64_t attempts, int iteration);
+void closure_from_pairs(Ctx& c, int64_t npairs, const int32_t* pairs, int iteration);
+void closure_partial(Ctx& c, int32_t* out);
+void closure_apply(Ctx& c, int algo, int n_p, const int32_t* counts, int iteration);
+int64_t count_unconverged(Ctx& c, const int32_t* w, int64_t m, int n_p);
+// timing helpers
+int timer_begin(Ctx& c);
+void timer_end(Ctx& c, int slot, int begin_ev);
+void timer_collect(Ctx& c, fc_stats* st);
+// scratch helpers
+template <class T> inline T* ensure(DevBuf& b, size_t count) {
+    b.ensure(count * sizeof(T) + 16);
+    return b.as<T>();
+}
+void sync(Ctx& c);
+int64_t read_i64(Ctx& c, const int64_t* dev);
+
+constexpr int64_t AGE_ITER_SHIFT = 40;
+constexpr int64_t AGE_REPAIR_OFFSET = int64_t(1) << 39;
+
+}  // namespace fc

@@ -1,0 +1,303 @@
+// graph.hip -- device-resident graph: ingest (replaces nx.read_edgelist + G.copy() +
+// weight reset, fast_consensus.py:131-136, :434), deterministic CSR build, and the
+// merge that turns nextgraph into graph (fast_consensus.py:198, :307).
+#include <hipcub/hipcub.hpp>
+
+#include "fc_ctx.h"
+#include "fc_device.h"
+
+namespace fc {
+
+static constexpr int TB = 256;
+static inline unsigned nblk(int64_t n, int tb = TB) {
+    int64_t b = (n + tb - 1) / tb;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+// ------------------------------------------------------------------ hipcub wrappers
+template <class K, class V>
+static void sort_pairs(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit) {
+    if (n <= 0) return;
+    size_t tmp = 0;
+    FC_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)n, 0, end_bit, c.stream));
+    c.sort_tmp.ensure(tmp);
+    FC_HIP(hipcub::DeviceRadixSort::SortPairs(c.sort_tmp.p, tmp, kin, kout, vin, vout, (int)n, 0, end_bit,
+                                              c.stream));
+}
+template <class T>
+void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n) {
+    if (n <= 0) return;
+    size_t tmp = 0;
+    FC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)n, c.stream));
+    c.sort_tmp.ensure(tmp);
+    FC_HIP(hipcub::DeviceScan::ExclusiveSum(c.sort_tmp.p, tmp, in, out, (int)n, c.stream));
+}
+template void exclusive_scan<int64_t>(Ctx&, const int64_t*, int64_t*, int64_t);
+template void exclusive_scan<int32_t>(Ctx&, const int32_t*, int32_t*, int64_t);
+template <class K, class V>
+void sort_pairs_public(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit) {
+    sort_pairs(c, kin, kout, vin, vout, n, end_bit);
+}
+template void sort_pairs_public<uint64_t, int64_t>(Ctx&, const uint64_t*, uint64_t*, const int64_t*, int64_t*,
+                                                   int64_t, int);
+template void sort_pairs_public<uint64_t, int32_t>(Ctx&, const uint64_t*, uint64_t*, const int32_t*, int32_t*,
+                                                   int64_t, int);
+
+void sync(Ctx& c) { FC_HIP(hipStreamSynchronize(c.stream)); }
+int64_t read_i64(Ctx& c, const int64_t* dev) {
+    FC_HIP(hipMemcpyAsync(c.hpin, dev, sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    return c.hpin[0];
+}
+
+// ------------------------------------------------------------------ ingest kernels
+__global__ void k_make_keys(int64_t m, const int32_t* u, const int32_t* v, int bits, uint64_t* key,
+                            int64_t* idx) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t a = u[i], b = v[i];
+    uint64_t sent = (bits >= 32) ? ~0ull : ((1ull << (2 * bits)) - 1ull);
+    uint64_t k = sent;
+    if (a != b) {
+        uint64_t lo = (uint64_t)(a < b ? a : b), hi = (uint64_t)(a < b ? b : a);
+        k = (lo << bits) | hi;
+    }
+    key[i] = k;
+    idx[i] = i;
+}
+
+__global__ void k_unique_flags(int64_t m, const uint64_t* key, int bits, int64_t* flag) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    uint64_t sent = (bits >= 32) ? ~0ull : ((1ull << (2 * bits)) - 1ull);
+    uint64_t k = key[i];
+    flag[i] = (k != sent && (i == 0 || key[i - 1] != k)) ? 1 : 0;
+}
+
+__global__ void k_scatter_unique(int64_t m, const uint64_t* key, const int64_t* idx, const int64_t* flag,
+                                 const int64_t* pos, int bits, int32_t* eu, int32_t* ev, int32_t* ew,
+                                 int64_t* eage) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || !flag[i]) return;
+    int64_t p = pos[i];
+    uint64_t k = key[i];
+    eu[p] = (int32_t)(k >> bits);
+    ev[p] = (int32_t)(k & ((1ull << bits) - 1ull));
+    ew[p] = 1;          // fast_consensus.py:135-136: every weight reset to 1.0
+    eage[p] = idx[i];   // first occurrence (stable sort) = networkx adjacency age
+}
+
+void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v) {
+    FC_REQUIRE(n >= 1 && n < (int64_t(1) << 31), FC_EINVAL, "node count out of range");
+    FC_REQUIRE(m >= 0 && m < (int64_t(1) << 31), FC_EINVAL, "edge count out of range");
+    for (int64_t i = 0; i < m; ++i)
+        FC_REQUIRE(u[i] >= 0 && u[i] < n && v[i] >= 0 && v[i] < n, FC_EINVAL, "edge endpoint out of range");
+    c.N = n;
+    int bits = 1;
+    while ((int64_t(1) << bits) < n) ++bits;
+    c.key_bits = bits;
+    int64_t mm = m > 0 ? m : 1;
+    int32_t* du = ensure<int32_t>(c.cu, mm);
+    int32_t* dv = ensure<int32_t>(c.cv, mm);
+    FC_HIP(hipMemcpyAsync(du, u, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+    FC_HIP(hipMemcpyAsync(dv, v, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+    uint64_t* k1 = ensure<uint64_t>(c.mkey, mm);
+    uint64_t* k2 = ensure<uint64_t>(c.mkey2, mm);
+    int64_t* i1 = ensure<int64_t>(c.midx, mm);
+    int64_t* i2 = ensure<int64_t>(c.midx2, mm);
+    int64_t* fl = ensure<int64_t>(c.ckey, mm + 1);
+    int64_t* ps = ensure<int64_t>(c.ckey2, mm + 1);
+    k_make_keys<<<nblk(m), TB, 0, c.stream>>>(m, du, dv, bits, k1, i1);
+    sort_pairs(c, k1, k2, i1, i2, m, 2 * bits);
+    k_unique_flags<<<nblk(m), TB, 0, c.stream>>>(m, k2, bits, fl);
+    exclusive_scan(c, fl, ps, m);
+    int64_t last_pos = 0, last_flag = 0;
+    if (m > 0) {
+        FC_HIP(hipMemcpyAsync(&c.hpin[0], ps + m - 1, 8, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(&c.hpin[1], fl + m - 1, 8, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        last_pos = c.hpin[0];
+        last_flag = c.hpin[1];
+    }
+    int64_t mu = last_pos + last_flag;
+    Graph& g = c.g;
+    g.m = mu;
+    int64_t cap = mu > 0 ? mu : 1;
+    ensure<int32_t>(g.eu, cap); ensure<int32_t>(g.ev, cap); ensure<int32_t>(g.ew, cap); ensure<int64_t>(g.eage, cap);
+    k_scatter_unique<<<nblk(m), TB, 0, c.stream>>>(m, k2, i2, fl, ps, bits, g.eu.as<int32_t>(), g.ev.as<int32_t>(),
+                                                    g.ew.as<int32_t>(), g.eage.as<int64_t>());
+    c.m_original = mu;   // L = G.number_of_edges() (fast_consensus.py:132, :144)
+    graph_build_csr(c, g);
+    graph_copy(c, c.g0, g);
+    c.labT_valid = false;
+}
+
+// graph = G.copy() (fast_consensus.py:131): device-to-device, the input stays resident.
+void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
+    const int64_t m = src.m > 0 ? src.m : 1, n = c.N;
+    auto cp = [&](DevBuf& d, const DevBuf& s, size_t bytes) {
+        d.ensure(bytes + 16);
+        FC_HIP(hipMemcpyAsync(d.p, s.p, bytes, hipMemcpyDeviceToDevice, c.stream));
+    };
+    cp(dst.eu, src.eu, 4 * m); cp(dst.ev, src.ev, 4 * m); cp(dst.ew, src.ew, 4 * m); cp(dst.eage, src.eage, 8 * m);
+    cp(dst.rowptr, src.rowptr, 8 * (n + 1));
+    cp(dst.col, src.col, 8 * m); cp(dst.cw, src.cw, 8 * m); cp(dst.ceid, src.ceid, 8 * m);
+    cp(dst.kdeg, src.kdeg, 8 * n);
+    dst.m = src.m; dst.M2 = src.M2; dst.max_deg = src.max_deg; dst.max_kdeg = src.max_kdeg;
+    c.labT_valid = false;
+}
+
+// ------------------------------------------------------------------ CSR build
+__global__ void k_count_uv(int64_t m, const int32_t* eu, const int32_t* ev, int64_t* cu, int64_t* cv) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    atomicAdd((unsigned long long*)&cu[eu[e]], 1ull);
+    atomicAdd((unsigned long long*)&cv[ev[e]], 1ull);
+}
+__global__ void k_rowptr(int64_t n, int64_t m, const int64_t* us, const int64_t* vs, int64_t* rowptr) {
+    int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < n) rowptr[x] = us[x] + vs[x];
+    if (x == n) rowptr[n] = 2 * m;
+}
+__global__ void k_iota_ev(int64_t m, const int32_t* ev, uint32_t* key, int32_t* idx) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    key[e] = (uint32_t)ev[e];
+    idx[e] = (int32_t)e;
+}
+// Row x = [neighbours u < x, ascending] ++ [neighbours v > x, ascending]: fully sorted rows.
+__global__ void k_fill_upper(int64_t m, const int32_t* eu, const int32_t* ev, const int32_t* ew,
+                             const int64_t* rowptr, const int64_t* ustart, const int64_t* vstart,
+                             int32_t* col, int32_t* cw, int32_t* ceid) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    int32_t u = eu[e];
+    int64_t nlow = vstart[u + 1] - vstart[u];
+    int64_t p = rowptr[u] + nlow + (e - ustart[u]);
+    col[p] = ev[e]; cw[p] = ew[e]; ceid[p] = (int32_t)e;
+}
+__global__ void k_fill_lower(int64_t m, const int32_t* perm, const int32_t* eu, const int32_t* ev,
+                             const int32_t* ew, const int64_t* rowptr, const int64_t* vstart, int32_t* col,
+                             int32_t* cw, int32_t* ceid) {
+    int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= m) return;
+    int32_t e = perm[f];
+    int32_t v = ev[e];
+    int64_t p = rowptr[v] + (f - vstart[v]);
+    col[p] = eu[e]; cw[p] = ew[e]; ceid[p] = e;
+}
+__global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int64_t* kdeg, int64_t* red) {
+    int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t s = 0, d = 0;
+    if (x < n) {
+        for (int64_t j = rowptr[x]; j < rowptr[x + 1]; ++j) s += cw[j];
+        kdeg[x] = s;
+        d = rowptr[x + 1] - rowptr[x];
+    }
+    // block reduce: sum(kdeg), max(deg), max(kdeg)
+    __shared__ long long ss[TB], sd[TB], sk[TB];
+    ss[threadIdx.x] = s; sd[threadIdx.x] = d; sk[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = TB / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            ss[threadIdx.x] += ss[threadIdx.x + o];
+            sd[threadIdx.x] = max(sd[threadIdx.x], sd[threadIdx.x + o]);
+            sk[threadIdx.x] = max(sk[threadIdx.x], sk[threadIdx.x + o]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd((unsigned long long*)&red[0], (unsigned long long)ss[0]);
+        atomicMax((long long*)&red[1], sd[0]);
+        atomicMax((long long*)&red[2], sk[0]);
+    }
+}
+
+void graph_build_csr(Ctx& c, Graph& g) {
+    const int64_t n = c.N, m = g.m;
+    int64_t* cu = ensure<int64_t>(c.nodetmp, n + 1);
+    int64_t* cv = ensure<int64_t>(c.nodetmp2, n + 1);
+    int64_t* us = ensure<int64_t>(c.nodetmp3, 2 * (n + 1));
+    int64_t* vs = us + (n + 1);
+    FC_HIP(hipMemsetAsync(cu, 0, sizeof(int64_t) * (n + 1), c.stream));
+    FC_HIP(hipMemsetAsync(cv, 0, sizeof(int64_t) * (n + 1), c.stream));
+    if (m > 0) k_count_uv<<<nblk(m), TB, 0, c.stream>>>(m, g.eu.as<int32_t>(), g.ev.as<int32_t>(), cu, cv);
+    exclusive_scan(c, cu, us, n + 1);
+    exclusive_scan(c, cv, vs, n + 1);
+    int64_t* rowptr = ensure<int64_t>(g.rowptr, n + 1);
+    k_rowptr<<<nblk(n + 1), TB, 0, c.stream>>>(n, m, us, vs, rowptr);
+    int64_t m2 = 2 * m > 0 ? 2 * m : 1;
+    int32_t* col = ensure<int32_t>(g.col, m2);
+    int32_t* cw = ensure<int32_t>(g.cw, m2);
+    int32_t* ceid = ensure<int32_t>(g.ceid, m2);
+    if (m > 0) {
+        uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, m);
+        uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, m);
+        int32_t* i1 = (int32_t*)ensure<int64_t>(c.midx, m);
+        int32_t* i2 = (int32_t*)ensure<int64_t>(c.midx2, m);
+        k_iota_ev<<<nblk(m), TB, 0, c.stream>>>(m, g.ev.as<int32_t>(), k1, i1);
+        sort_pairs(c, (const uint32_t*)k1, k2, (const int32_t*)i1, i2, m, c.key_bits);
+        k_fill_upper<<<nblk(m), TB, 0, c.stream>>>(m, g.eu.as<int32_t>(), g.ev.as<int32_t>(), g.ew.as<int32_t>(),
+                                                    rowptr, us, vs, col, cw, ceid);
+        k_fill_lower<<<nblk(m), TB, 0, c.stream>>>(m, i2, g.eu.as<int32_t>(), g.ev.as<int32_t>(),
+                                                    g.ew.as<int32_t>(), rowptr, vs, col, cw, ceid);
+    }
+    int64_t* kdeg = ensure<int64_t>(g.kdeg, n);
+    int64_t* red = ensure<int64_t>(c.counters, 16);
+    FC_HIP(hipMemsetAsync(red, 0, 3 * sizeof(int64_t), c.stream));
+    k_kdeg<<<nblk(n), TB, 0, c.stream>>>(n, rowptr, cw, kdeg, red);
+    FC_HIP(hipMemcpyAsync(c.hpin, red, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    g.M2 = c.hpin[0];
+    g.max_deg = (int32_t)c.hpin[1];
+    g.max_kdeg = c.hpin[2];
+}
+
+// ------------------------------------------------------------------ merge
+// graph <- kept ++ closure ++ repair, re-sorted canonically (fast_consensus.py:198, :307).
+__global__ void k_merge_keys(int64_t n0, int64_t n1, const int32_t* au, const int32_t* av, const int32_t* bu,
+                             const int32_t* bv, int bits, uint64_t* key, int64_t* idx) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n0 + n1) return;
+    int32_t u, v;
+    if (i < n0) { u = au[i]; v = av[i]; } else { u = bu[i - n0]; v = bv[i - n0]; }
+    key[i] = ((uint64_t)u << bits) | (uint64_t)v;
+    idx[i] = i;
+}
+__global__ void k_merge_gather(int64_t n, int64_t n0, const int64_t* idx, const int32_t* au, const int32_t* av,
+                               const int32_t* aw, const int64_t* aage, const int32_t* bu, const int32_t* bv,
+                               const int32_t* bw, const int64_t* bage, int32_t* eu, int32_t* ev, int32_t* ew,
+                               int64_t* eage) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t s = idx[i];
+    if (s < n0) { eu[i] = au[s]; ev[i] = av[s]; ew[i] = aw[s]; eage[i] = aage[s]; }
+    else { s -= n0; eu[i] = bu[s]; ev[i] = bv[s]; ew[i] = bw[s]; eage[i] = bage[s]; }
+}
+
+// kept (c.ku..) ++ added (c.cu.., n_cand closure + n_rep repair) -> c.g, then CSR.
+void graph_merge_next(Ctx& c, int64_t n_added) {
+    const int64_t n0 = c.kept_m, total = c.kept_m + n_added;
+    int64_t cap = total > 0 ? total : 1;
+    uint64_t* k1 = ensure<uint64_t>(c.mkey, cap);
+    uint64_t* k2 = ensure<uint64_t>(c.mkey2, cap);
+    int64_t* i1 = ensure<int64_t>(c.midx, cap);
+    int64_t* i2 = ensure<int64_t>(c.midx2, cap);
+    Graph& g = c.g;
+    ensure<int32_t>(g.eu, cap); ensure<int32_t>(g.ev, cap); ensure<int32_t>(g.ew, cap); ensure<int64_t>(g.eage, cap);
+    if (total > 0) {
+        k_merge_keys<<<nblk(total), TB, 0, c.stream>>>(n0, n_added, c.ku.as<int32_t>(), c.kv.as<int32_t>(),
+                                                        c.cu.as<int32_t>(), c.cv.as<int32_t>(), c.key_bits, k1, i1);
+        sort_pairs(c, k1, k2, i1, i2, total, 2 * c.key_bits);
+        k_merge_gather<<<nblk(total), TB, 0, c.stream>>>(
+            total, n0, i2, c.ku.as<int32_t>(), c.kv.as<int32_t>(), c.kw.as<int32_t>(), c.kage.as<int64_t>(),
+            c.cu.as<int32_t>(), c.cv.as<int32_t>(), c.cw2.as<int32_t>(), c.cage.as<int64_t>(), g.eu.as<int32_t>(),
+            g.ev.as<int32_t>(), g.ew.as<int32_t>(), g.eage.as<int64_t>());
+    }
+    g.m = total;
+    graph_build_csr(c, g);
+    c.labT_valid = false;
+}
+
+}  // namespace fc

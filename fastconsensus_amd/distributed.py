@@ -1,0 +1,108 @@
+"""Replica-sharded fast_consensus over several GPUs (one process per GPU, RCCL over xGMI).
+
+The n_p community-detection runs of every iteration are independent given the graph, so
+rank g owns the CONTIGUOUS replica range [g*n_p/W, (g+1)*n_p/W) (the Louvain consensus
+rule depends on replica order, fast_consensus.py:154-159).  Every rank keeps an identical
+copy of the graph; the only data-path exchanges are
+  * per-edge partials: Louvain k_last (all-reduce MAX) / LPM co-membership counts (SUM);
+  * per-candidate closure co-membership counts (SUM, louvain only);
+after which threshold, check, closure (same counter-based RNG on every rank), repair and
+the graph rebuild run replicated and deterministically -- no graph broadcast.  The final
+partitions are all-gathered to rank 0.  The loop mirrors fc_run (capi.cpp) step for step,
+so W ranks produce bit-identical results to one GPU.
+
+The driver only needs an "engine" with the step API of fastconsensus_amd.Engine; buffers
+are torch tensors on the engine's device (RCCL) or on the CPU (gloo, used by the tests).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .core import FINAL_PASS_ITER
+
+LOUVAIN = 0
+
+
+def shard(n_p, rank, world):
+    return n_p * rank // world, n_p * (rank + 1) // world
+
+
+def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True):
+    """Returns (labels [n_p][N] on rank 0 (None elsewhere), stats dict)."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    r0, r1 = shard(n_p, rank, world)
+    louv = algo == LOUVAIN
+    on_gpu = str(device).startswith("cuda")
+    if on_gpu:  # engine kernels and torch/RCCL ops on ONE stream: no cross-stream races
+        engine.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv)
+    finally:
+        if on_gpu:
+            engine.set_stream(None)
+
+
+def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv):
+    mine = r1 - r0
+    engine.reset_graph()
+    n, _, L = engine.graph_info()
+    st = {"iterations": 0, "exit_check": 0, "hit_iter_cap": 0, "partition_edges": 0, "n_p": n_p}
+    it = 0
+    while True:
+        if it >= max_iters:
+            st["hit_iter_cap"] = 1
+            break
+        m = engine.m
+        part = torch.empty(max(m, 1), dtype=torch.int32, device=device)
+        if mine > 0:
+            engine.cd(algo, r0, mine, n_p, it)                       # :148 / :270
+            engine.consensus_partial(algo, part)                     # :150-159 / :273-280
+        else:
+            part.fill_(-1 if louv else 0)
+        if world > 1:
+            dist.all_reduce(part, op=dist.ReduceOp.MAX if louv else dist.ReduceOp.SUM)
+        st["partition_edges"] += n_p * m
+        conv1, kept, unc = engine.consensus_apply(algo, n_p, tau, delta, part)   # :163-173
+        if louv and conv1:
+            st["exit_check"] = 1
+            break
+        nc = engine.closure_sample(L, it)                            # :175-184 / :292-300
+        cnt = None
+        if louv and nc > 0:
+            cnt = torch.zeros(nc, dtype=torch.int32, device=device)
+            if mine > 0:
+                engine.closure_partial(cnt)                          # :186-190
+            if world > 1:
+                dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        conv2, _ = engine.closure_apply(algo, n_p, delta, cnt, it)   # :193-202 / :307-310
+        it += 1
+        if conv2:
+            st["exit_check"] = 2
+            break
+    st["iterations"] = it + (1 if st["exit_check"] == 1 else 0)
+    m = engine.m
+    st["partition_edges"] += n_p * m
+    st["m_final"] = m
+    local = None
+    if mine > 0:
+        engine.cd(algo, r0, mine, n_p, FINAL_PASS_ITER + it)         # final pass :383-392
+        local = engine.get_labels(mine, renumber=True)
+    if not gather:
+        return local, st
+    if world == 1:
+        return local, st
+    cap = max(shard(n_p, g, world)[1] - shard(n_p, g, world)[0] for g in range(world))
+    buf = torch.full((cap, n), -1, dtype=torch.int32, device=device)
+    if mine > 0:
+        buf[:mine].copy_(torch.from_numpy(local))
+    bufs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    if rank != 0:
+        return None, st
+    out = np.empty((n_p, n), np.int32)
+    for g in range(world):
+        a, b = shard(n_p, g, world)
+        if b > a:
+            out[a:b] = bufs[g][:b - a].cpu().numpy()
+    return out, st

@@ -1,0 +1,153 @@
+/*
+ * fastconsensus_amd.h -- C-ABI of the MI355X-native fast-consensus engine.
+ *
+ * The reference (ytabatabaee/fastconsensus, fast_consensus.py) is a Python script with
+ * no FFI; its hot path is the while-loop of fast_consensus() (fast_consensus.py:129-411)
+ * plus the community-detection calls it makes.  Each entry point below replaces a span
+ * of that loop; the replaced reference lines are cited per function.  A host binds this
+ * with ctypes (see fastconsensus_amd/_lib.py and INTEGRATION.md).
+ *
+ * Conventions
+ *   - Plain pointers + sizes; no torch or HIP types in signatures (streams are void*).
+ *   - Node ids are 0..n-1 in NODE ORDER (first appearance, as networkx read_edgelist
+ *     orders nodes); the host keeps the label<->id map.
+ *   - Every function returns 0 on success, a negative FC_E* code on error; the message
+ *     is in fc_last_error() (thread-local).  There is no CPU fallback: without a usable
+ *     gfx950 device fc_create fails with FC_ENODEV.
+ *   - One context per host thread; a context is bound to one GPU and is not thread-safe.
+ *   - Host arrays are caller-owned and copied; device buffers are context-owned, except
+ *     buffers passed as `void* dev_*` which the caller owns (e.g. torch tensors used as
+ *     RCCL all-reduce buffers).
+ */
+#ifndef FASTCONSENSUS_AMD_H
+#define FASTCONSENSUS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FC_OK 0
+#define FC_EINVAL -1      /* bad argument */
+#define FC_ENODEV -2      /* no HIP device / not gfx950 */
+#define FC_EHIP -3        /* HIP runtime error */
+#define FC_ESTATE -4      /* call out of order (e.g. no graph loaded) */
+#define FC_ELIMIT -5      /* a size limit was exceeded */
+
+#define FC_ALGO_LOUVAIN 0 /* fast_consensus.py:141-202 (+ final pass :383-384) */
+#define FC_ALGO_LPM 1     /* fast_consensus.py:260-310 (+ final pass :391-392) */
+
+typedef struct fc_ctx fc_ctx;
+
+typedef struct fc_stats {
+    int32_t iterations;       /* consensus iterations executed (while-loop trips)          */
+    int32_t exit_check;       /* 1: louvain check #1 (:172-173); 2: check after closure     */
+    int32_t hit_iter_cap;     /* 1 if max_iters stopped the loop (the reference never stops) */
+    int32_t n_p;
+    int64_t m_final;          /* edges of the graph the final pass ran on                  */
+    int64_t partition_edges;  /* sum_iter n_p*m_iter + n_p*m_final                           */
+    int64_t cd_sweeps;        /* local-moving / LPA sweeps, summed over replicas            */
+    int64_t cd_vertex_visits; /* vertices processed by CD kernels, summed over replicas     */
+    int64_t cd_edge_visits;   /* adjacency entries scanned by CD kernels                    */
+    double cd_ms;             /* device time per phase (filled when timing is enabled)      */
+    double consensus_ms;
+    double closure_ms;
+    double rebuild_ms;
+    double decide_ms;         /* light local-moving kernel (the dominant kernel)            */
+    int64_t decide_launches;
+    int64_t decide_bytes;     /* algorithmic bytes of those launches */
+} fc_stats;
+
+/* ---- lifecycle ---------------------------------------------------------------- */
+const char* fc_last_error(void);
+const char* fc_version(void);
+/* device: HIP ordinal; seed: drives every random choice (CD order/ties, closure). */
+int fc_create(int device, uint64_t seed, fc_ctx** out);
+void fc_destroy(fc_ctx* ctx);
+/* Run all work on an external stream (e.g. torch.cuda.current_stream().cuda_stream).
+ * NULL restores the context's own stream. */
+int fc_set_stream(fc_ctx* ctx, void* hip_stream);
+/* 0/1: record HIP events around kernels and fill the *_ms fields of fc_stats. */
+int fc_set_timing(fc_ctx* ctx, int enable);
+/* Fill *stats with everything accumulated since the last call: the *_ms fields and
+ * decide_launches from the recorded HIP events (synchronises the stream) and the CD
+ * counters (sweeps, visits, decide_bytes) of every fc_run / fc_cd; then reset both. */
+int fc_collect_timing(fc_ctx* ctx, fc_stats* stats);
+/* Tunables (0 = default): buckets per sweep, max sweeps per CD run, max iterations. */
+int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
+
+/* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */
+/* Edge list in input order (ids 0..n-1).  Self loops are dropped, duplicates keep their
+ * first occurrence (its position defines the edge's networkx adjacency age); all weights
+ * are set to 1 (fast_consensus.py:135-136). */
+int fc_load_graph(fc_ctx* ctx, int64_t n, int64_t m, const int32_t* u, const int32_t* v);
+int fc_graph_info(fc_ctx* ctx, int64_t* n, int64_t* m, int64_t* m_original);
+/* graph <- the loaded G (device-to-device; fc_run does this itself, like graph = G.copy()
+ * at fast_consensus.py:131).  The step API calls it before a new run. */
+int fc_reset_graph(fc_ctx* ctx);
+/* Copy the working graph `graph` out: canonical (u<v) sorted by (u,v); any pointer may
+ * be NULL. */
+int fc_get_graph(fc_ctx* ctx, int32_t* u, int32_t* v, int32_t* w, int64_t* age);
+
+/* Copy out the post-threshold `nextgraph` left by fc_consensus_apply (what the reference
+ * passes to check #1, fast_consensus.py:172): canonical, sorted, consensus weights. */
+int fc_get_nextgraph(fc_ctx* ctx, int64_t* m, int32_t* u, int32_t* v, int32_t* w, int64_t* age);
+
+/* ---- one-shot driver: fast_consensus(G, algorithm, n_p, thresh, delta) (:129-411) --- */
+/* Starts from the loaded G every call (G itself is never modified).  labels_out: [n_p][n] final partitions (community ids renumbered 0..k-1 in node
+ * order), may be NULL (then fc_get_labels can fetch them). */
+int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* labels_out,
+           fc_stats* stats);
+
+/* ---- fine-grained steps (distributed driver; parity tests) ------------------------ */
+/* Community detection on the working graph for replicas [replica_begin,
+ * replica_begin+replica_count) of n_p_total (:148 / :384 louvain level 0, :270 / :392 LPA).
+ * Randomness depends on (seed, global replica index, iteration), not on the sharding. */
+int fc_cd(fc_ctx* ctx, int algo, int replica_begin, int replica_count, int n_p_total,
+          int iteration);
+/* Replay: install host labelings [count][n] as the local replicas (begin = 0). */
+int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels);
+/* Download local labelings [count][n]; renumber != 0 -> ids 0..k-1 by first node. */
+int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber);
+/* Per-edge partial over the local replicas into caller device buffer dev_out (int32[m]):
+ * louvain -> largest global replica index whose labels split the edge, or -1
+ * (reduce with MAX); lpm -> number of local replicas co-clustering it (reduce with SUM). */
+int fc_consensus_partial(fc_ctx* ctx, int algo, void* dev_out);
+/* Apply the reduced partial: consensus weight rule (:150-159 / :273-280), threshold
+ * (:163-168 / :284-288) and, for louvain, check #1 (:172).  kept_out/unconv_out: counts. */
+int fc_consensus_apply(fc_ctx* ctx, int algo, int n_p, double tau, double delta,
+                       const void* dev_partial, int* converged, int64_t* kept_out,
+                       int64_t* unconverged_out);
+/* Closure candidates: L attempts drawn on the device (:175-184 / :292-300), or recorded
+ * pairs (replay, int32[npairs][2]).  n_cand: new distinct absent edges. */
+int fc_closure_sample(fc_ctx* ctx, int64_t attempts, int iteration, int64_t* n_cand);
+int fc_closure_set_pairs(fc_ctx* ctx, int64_t npairs, const int32_t* pairs, int iteration,
+                         int64_t* n_cand);
+/* Per-candidate count of local replicas co-clustering it into dev_out (int32[n_cand]). */
+int fc_closure_partial(fc_ctx* ctx, void* dev_out);
+/* Add closure edges (louvain weight = reduced count (:186-190); lpm weight 0 (:302-304)),
+ * isolate repair for louvain (:193-195), swap graph <- nextgraph (:198 / :307) and run
+ * the check (:201 / :309). dev_counts may be NULL for lpm. */
+int fc_closure_apply(fc_ctx* ctx, int algo, int n_p, double delta, const void* dev_counts,
+                     int iteration, int* converged, int64_t* m_out);
+
+/* ---- synthetic inputs for benchmarks (host C++, not on the hot path) ---------------- */
+/* LFR-like benchmark graph (power-law degrees tau1, community sizes tau2, mixing mu).
+ * Writes at most m_cap edges into u/v and the planted community of every node. */
+int fc_generate_lfr(int64_t n, double tau1, double tau2, double mu, double avg_deg,
+                    int32_t max_deg, int32_t min_comm, int32_t max_comm, uint64_t seed,
+                    int64_t m_cap, int32_t* u, int32_t* v, int64_t* m_out, int32_t* planted);
+/* Planted-partition SBM: n/block_size blocks, expected internal/external degree. */
+int fc_generate_sbm(int64_t n, int32_t block_size, double deg_in, double deg_out,
+                    uint64_t seed, int64_t m_cap, int32_t* u, int32_t* v, int64_t* m_out);
+/* Edge-list text parser (2+ whitespace-separated int columns; extra columns ignored).
+ * Returns labels in node order (first appearance) and edges as ids. Two-phase: call with
+ * NULL outputs to get sizes. */
+int fc_read_edgelist(const char* path, int64_t* n_out, int64_t* m_out, int64_t* labels,
+                     int32_t* u, int32_t* v);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FASTCONSENSUS_AMD_H */

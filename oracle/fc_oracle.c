@@ -421,3 +421,150 @@ void orc_build_csr(i64 N, i64 m, const i32* eu, const i32* ev, const i32* w, i64
     for (i64 e = 0; e < m; ++e) { i64 p = fill[eu[e]]++; col[p] = ev[e]; if (cw) cw[p] = w ? w[e] : 1; }
     free(fill);
 }
+
+/* ==================================================================================
+ * CPU twin of the engine's bucketed community detection (fastconsensus_amd/csrc/cd.hip).
+ * This is NOT the reference algorithm: it restates, sequentially, the device algorithm
+ * (random bucketed order, synchronous decisions inside a bucket, integer gains, hashed
+ * tie-breaks) so that the HIP kernels can be checked bit-exactly on the same seed.
+ * Statistical closeness to the reference's sequential algorithms is tested separately
+ * against orc_louvain_level0 / orc_lpa above.
+ * ================================================================================== */
+static inline uint32_t tw_hash32(uint32_t x) {
+    x ^= x >> 16; x *= 0x85ebca6bu; x ^= x >> 13; x *= 0xc2b2ae35u; x ^= x >> 16; return x;
+}
+static inline uint32_t tw_hash2(uint32_t a, uint32_t b) { return tw_hash32(a ^ tw_hash32(b + 0x9e3779b9u)); }
+static inline u64 tw_mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static inline uint32_t tw_stream_key(u64 seed, uint32_t rg, uint32_t iter, uint32_t sweep, uint32_t salt) {
+    u64 z = tw_mix64(seed ^ (0x9E3779B97F4A7C15ull * (1 + (u64)rg)));
+    z = tw_mix64(z ^ ((u64)iter << 32 | sweep) ^ ((u64)salt << 56));
+    return (uint32_t)(z ^ (z >> 32));
+}
+typedef struct { uint32_t n, hb, mask, k0, k1, k2, k3; } tw_perm;
+static tw_perm tw_make_perm(uint32_t n, uint32_t key) {
+    tw_perm p;
+    uint32_t bits = 1;
+    while (bits < 32 && (1u << bits) < n) ++bits;
+    uint32_t hb = (bits + 1) / 2;
+    if (hb < 1) hb = 1;
+    p.n = n; p.hb = hb; p.mask = (1u << hb) - 1u;
+    p.k0 = tw_hash2(key, 0x1234567u); p.k1 = tw_hash2(key, 0x89abcdefu);
+    p.k2 = tw_hash2(key, 0x2468aceu); p.k3 = tw_hash2(key, 0x13579bdu);
+    return p;
+}
+static uint32_t tw_perm_apply(const tw_perm* p, uint32_t x) {
+    do {
+        uint32_t L = x >> p->hb, R = x & p->mask, t;
+        t = R; R = L ^ (tw_hash32(R ^ p->k0) & p->mask); L = t;
+        t = R; R = L ^ (tw_hash32(R ^ p->k1) & p->mask); L = t;
+        t = R; R = L ^ (tw_hash32(R ^ p->k2) & p->mask); L = t;
+        t = R; R = L ^ (tw_hash32(R ^ p->k3) & p->mask); L = t;
+        x = (L << p->hb) | R;
+    } while (x >= p->n);
+    return x;
+}
+static inline uint32_t tw_tie(uint32_t tbk, i32 v, i32 c) { return tw_hash32(tw_hash32(tbk ^ (uint32_t)v) ^ (uint32_t)c); }
+static inline int tw_better(long long s1, uint32_t h1, i32 c1, long long s2, uint32_t h2, i32 c2) {
+    if (s1 != s2) return s1 > s2;
+    if (h1 != h2) return h1 > h2;
+    return c1 < c2;
+}
+
+/* One replica.  algo 0 = louvain local moving, 1 = lpa.  Returns sweeps executed. */
+static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
+                      u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, i32* lab) {
+    const int louv = algo == 0;
+    i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
+    i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
+    i64* acc = (i64*)calloc((size_t)N, sizeof(i64));
+    u8* seen = (u8*)calloc((size_t)N, 1);
+    i32* keys = (i32*)malloc(sizeof(i32) * (size_t)(N + 1));
+    const int B = (int)(buckets < N ? buckets : N);
+    const i64 S = (N + B - 1) / B;
+    i32* dec = (i32*)malloc(sizeof(i32) * (size_t)(S + 1));
+    for (i64 v = 0; v < N; ++v) { lab[v] = (i32)v; tot[v] = kdeg[v]; csz[v] = 1; }
+    int active = M2 > 0, sweep = 0;
+    for (; sweep < max_sweeps && active; ++sweep) {
+        const tw_perm P = tw_make_perm((uint32_t)N, tw_stream_key(seed, rg, iter, (uint32_t)sweep, 1));
+        const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
+        unsigned long long dq = 0, moves = 0, unstable = 0;
+        for (int k = 0; k < B; ++k) {
+            i64 blen = N - (i64)k * S;
+            if (blen > S) blen = S;
+            if (blen <= 0) continue;
+            for (i64 i = 0; i < blen; ++i) {
+                const i32 v = (i32)tw_perm_apply(&P, (uint32_t)((i64)k * S + i));
+                dec[i] = -1;
+                const i64 rb = rowptr[v], re = rowptr[v + 1];
+                if (re == rb) continue;
+                i64 nk = 0;
+                for (i64 j = rb; j < re; ++j) {
+                    const i32 c = lab[col[j]];
+                    if (!seen[c]) { seen[c] = 1; acc[c] = 0; keys[nk++] = c; }
+                    acc[c] += louv ? cw[j] : 1;
+                }
+                const i32 own = lab[v];
+                const i64 kown = seen[own] ? acc[own] : 0;
+                const i64 kv = kdeg[v];
+                long long best_s = 0; uint32_t best_h = 0; i32 best_c = 0x7fffffff; int have = 0;
+                for (i64 q = 0; q < nk; ++q) {
+                    const i32 c = keys[q];
+                    long long sc;
+                    if (louv) { if (c == own) continue; sc = (long long)acc[c] * M2 - kv * tot[c]; }
+                    else sc = acc[c];
+                    const uint32_t h = tw_tie(tbk, v, c);
+                    if (!have || tw_better(sc, h, c, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = c; have = 1; }
+                }
+                for (i64 q = 0; q < nk; ++q) seen[keys[q]] = 0;
+                if (!have) continue;
+                if (louv) {
+                    const long long G = best_s - kown * M2 + kv * (tot[own] - kv);
+                    if (G <= 0) continue;
+                    const double d = (double)G * 2.0 / ((double)M2 * (double)M2);
+                    dq += (unsigned long long)llrint(d * 1099511627776.0);
+                    dec[i] = best_c;
+                } else {
+                    unstable += (kown != best_s);
+                    if (best_c != own) dec[i] = best_c;
+                }
+            }
+            for (i64 i = 0; i < blen; ++i) {
+                if (dec[i] < 0) continue;
+                const i32 v = (i32)tw_perm_apply(&P, (uint32_t)((i64)k * S + i));
+                const i32 old = lab[v], nw = dec[i];
+                lab[v] = nw;
+                if (louv) { tot[old] -= kdeg[v]; tot[nw] += kdeg[v]; csz[old]--; csz[nw]++; }
+                ++moves;
+            }
+        }
+        if (louv) { if (moves == 0 || ((double)dq / 1099511627776.0) < 1e-7) active = 0; }
+        else if (unstable == 0) active = 0;
+    }
+    free(tot); free(csz); free(acc); free(seen); free(keys); free(dec);
+    return sweep;
+}
+
+/* Replicas [rbase, rbase+n_r) of the engine's bucketed CD on a symmetric CSR.
+ * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
+void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
+                   int iteration, u64 seed, int buckets, int max_sweeps, i32* lab, int* sweeps) {
+    i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
+    i64 M2 = 0;
+    for (i64 v = 0; v < N; ++v) {
+        i64 s = 0;
+        for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) s += cw[j];
+        kdeg[v] = s;
+        M2 += s;
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < n_r; ++r) {
+        int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
+                            buckets, max_sweeps, lab + (i64)r * N);
+        if (sweeps) sweeps[r] = sw;
+    }
+    free(kdeg);
+}

@@ -62,6 +62,8 @@ def lib():
                                    ctypes.c_int]
         L.orc_modularity.argtypes = [i64, _i64p, _i32p, ctypes.c_void_p, _i32p]
         L.orc_modularity.restype = dbl
+        L.orc_engine_cd.argtypes = [ctypes.c_int, i64, _i64p, _i32p, _i32p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
         _lib = L
     return _lib
@@ -184,6 +186,28 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     sw = np.empty(n_r, np.int32)
     lib().orc_cd_batch(algo, n_r, g.N, rowptr, col, cw, int(seed) & (2**64 - 1), lab, sw, int(nthreads))
     return lab, sw
+
+
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200):
+    """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels)."""
+    rowptr, col, cw = g.csr()
+    lab = np.empty((n_r, g.N), np.int32)
+    sw = np.empty(n_r, np.int32)
+    lib().orc_engine_cd(algo, g.N, rowptr, col, cw, n_r, rbase, iteration, int(seed) & (2**64 - 1), buckets,
+                        max_sweeps, lab, sw)
+    return lab, sw
+
+
+def renumber(labels):
+    """Community ids -> 0..k-1 by first node (engine's output convention)."""
+    out = np.empty_like(labels)
+    for r, lab in enumerate(labels):
+        _, first, inv = np.unique(lab, return_index=True, return_inverse=True)
+        order = np.argsort(first)
+        rank = np.empty_like(order)
+        rank[order] = np.arange(len(order))
+        out[r] = rank[inv]
+    return out
 
 
 def modularity(g, labels, weighted=True):

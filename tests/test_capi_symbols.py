@@ -1,0 +1,58 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares (no GPU needed),
+and the product path fails loudly without a GPU (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for fn in os.listdir(os.path.join(ROOT, "include")):
+        if fn.endswith(".h"):
+            src = open(os.path.join(ROOT, "include", fn)).read()
+            src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+            names |= set(re.findall(r"\b(fc_[a-z_]+)\s*\(", src))
+    return names
+
+
+def test_header_declares_expected_surface():
+    names = declared_symbols()
+    for must in ("fc_create", "fc_run", "fc_consensus_partial", "fc_consensus_apply", "fc_closure_apply",
+                 "fc_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from fastconsensus_amd import _lib
+    from fastconsensus_amd.build import build
+    build(verbose=False)
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in sorted(declared_symbols()) if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(_lib.SYMBOLS) == declared_symbols()
+    _lib.load()
+    assert b"gfx950" in _lib.load().fc_version()
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import fastconsensus_amd as fc
+    with pytest.raises(fc.FastConsensusError) as ei:
+        fc.Engine(seed=1)
+    assert ei.value.code == -2
+
+
+def test_product_package_never_imports_oracle():
+    pkg = os.path.join(ROOT, "fastconsensus_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".cpp", ".hip", ".h")):
+                src = open(os.path.join(dirpath, fn)).read()
+                for pat in (r"^\s*(from|import)\s+oracle", r"fcoracle", r"\borc_[a-z]", r"oracle\.oracle"):
+                    assert not re.search(pat, src, flags=re.M), (fn, pat)
