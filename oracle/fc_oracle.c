@@ -201,9 +201,9 @@ void orc_adjacency_order(i64 N, i64 m, const i32* eu, const i32* ev, const i32* 
  * ties go to the first neighbour in networkx adjacency order -- carrying that weight.
  * old graph: (m_old, ou, ov, ow, oage); nextgraph degrees: deg[N] (updated in place).
  * Returns the number of repair edges written to out_u/out_v/out_w (canonical u<v) in
- * the order they are added. */
+ * the order they are added; out_x (may be NULL) receives the repaired node x. */
 i64 orc_repair(i64 N, i64 m_old, const i32* ou, const i32* ov, const i32* ow, const i64* oage,
-               i64* deg, i32* out_u, i32* out_v, i32* out_w) {
+               i64* deg, i32* out_u, i32* out_v, i32* out_w, i64* out_x) {
     i64* ptr = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
     i32* nbr = (i32*)malloc(sizeof(i32) * (size_t)(2 * m_old + 1));
     i32* nw = (i32*)malloc(sizeof(i32) * (size_t)(2 * m_old + 1));
@@ -217,6 +217,7 @@ i64 orc_repair(i64 N, i64 m_old, const i32* ou, const i32* ov, const i32* ow, co
             if (nw[j] < nw[best]) best = j;          /* strict: first minimum wins */
         i32 y = nbr[best];
         out_u[k] = (i32)(x < y ? x : y); out_v[k] = (i32)(x < y ? y : x); out_w[k] = nw[best];
+        if (out_x) out_x[k] = x;   /* creation order of repair edges = node order of x */
         ++k;
         deg[x]++; deg[y]++;
     }

@@ -51,7 +51,7 @@ def lib():
                                         _i32p, _i32p, _i32p, _i64p]
         L.orc_closure_pairs.restype = i64
         L.orc_adjacency_order.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, _i64p, _i32p, _i32p]
-        L.orc_repair.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, _i64p, _i32p, _i32p, _i32p]
+        L.orc_repair.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, _i64p, _i32p, _i32p, _i32p, _i64p]
         L.orc_repair.restype = i64
         L.orc_sort_edges.argtypes = [i64, _i32p, _i32p, _i64p]
         L.orc_louvain_level0.argtypes = [i64, _i64p, _i32p, _i32p, u64, _i32p]
@@ -176,8 +176,9 @@ def repair(old, deg):
     """deg: int64 degrees of nextgraph after closure (updated in place)."""
     k_max = old.N
     ou, ov, ow = (np.empty(max(k_max, 1), np.int32) for _ in range(3))
-    k = lib().orc_repair(old.N, old.m, old.u, old.v, old.w, old.age, deg, ou, ov, ow)
-    return ou[:k].copy(), ov[:k].copy(), ow[:k].copy()
+    ox = np.empty(max(k_max, 1), np.int64)
+    k = lib().orc_repair(old.N, old.m, old.u, old.v, old.w, old.age, deg, ou, ov, ow, ox)
+    return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), ox[:k].copy()
 
 
 def cd_batch(algo, n_r, g, seed, nthreads=0):
@@ -240,8 +241,8 @@ def iterate(algo, graph, labels, pairs, n_p, tau, delta, it):
     parts = [kept, closure]
     if algo == LOUVAIN:
         deg = kept.degrees() + closure.degrees()
-        ru, rv, rw = repair(graph, deg)
-        rep = EdgeGraph(graph.N, ru, rv, rw, base + AGE_REPAIR_OFFSET + np.arange(len(ru), dtype=np.int64))
+        ru, rv, rw, rx = repair(graph, deg)
+        rep = EdgeGraph(graph.N, ru, rv, rw, base + AGE_REPAIR_OFFSET + rx)
         trace["repair"] = rep
         parts.append(rep)
     new = concat(parts)
