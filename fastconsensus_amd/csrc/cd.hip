@@ -36,6 +36,9 @@ static constexpr int LIGHT_MAX_DEG = 64;
 static constexpr int HEAVY_LDS_SLOTS = 4096;
 static constexpr int HEAVY_GRID = 256;
 static constexpr double DQ_SCALE = 1099511627776.0;  // 2^40 fixed point for predicted dQ
+static constexpr int NSH = 16;          // counter shards per replica
+static constexpr int RF = 8;            // fields: 0 dq, 1 unstable, 2 moves, 3 verts, 4 entries, 5 cands
+
 
 static inline unsigned nblk(int64_t n, int tb = TB) {
     int64_t b = (n + tb - 1) / tb;
@@ -55,18 +58,25 @@ struct CDArgs {
     const int64_t* kdeg;
     int64_t M2;
     int32_t* lab;
-    int64_t* tot;
+    int32_t* nlab;               // [n_r][m2]: label of the neighbour behind adjacency entry j
+    const int32_t* rev;          // reverse adjacency entry of j
+    int64_t m2;                  // 2m (adjacency entries)
+    void* tot;                   // int32 [n_r][N] when 2M < 2^31, else int64
     int32_t* dec;
     int32_t* active;
-    unsigned long long* dq;      // per replica fixed-point predicted gain (louvain)
-    unsigned long long* moves;   // per replica moves this sweep
-    unsigned long long* unstable;// per replica (lpa)
+    // Sharded per-replica counters [n_r][NSH][RF]: one hot address per replica would
+    // serialise every block's atomic (~12 ns each, MI355X_MICROARCH.md "fanin").
+    unsigned long long* red;
     int32_t* heavy;              // (r, p) pairs
     int32_t* heavy_cnt;
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
     int64_t heavy_slots;         // slots per global table (power of 2)
-    unsigned long long* stats;   // [0] vertices, [1] entries, [2] distinct candidates (light kernel)
+    unsigned long long* sacc;    // [n_r][4] light-kernel vertices / entries / candidates, summed by k_sweep_end
 };
+
+__device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
+    return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
+}
 
 // Block -> (replica, chunk) with all chunks of a replica on as few XCDs as possible
 // (blocks b and b+8 share an XCD under round-robin dispatch; speed only).
@@ -85,6 +95,16 @@ __device__ __forceinline__ void tbl_insert(int32_t* keys, int32_t* vals, uint32_
         h = (h + 1) & mask;
     }
 }
+// Same, but returns the slot when THIS lane created it (the slot's owner evaluates it).
+__device__ __forceinline__ int tbl_insert_owner(int32_t* keys, int32_t* vals, uint32_t mask, int32_t c, int32_t w) {
+    uint32_t h = hash32((uint32_t)c) & mask;
+    while (true) {
+        const int32_t prev = atomicCAS(&keys[h], -1, c);
+        if (prev == -1) { atomicAdd(&vals[h], w); return (int)h; }
+        if (prev == c) { atomicAdd(&vals[h], w); return -1; }
+        h = (h + 1) & mask;
+    }
+}
 
 // Lexicographic best: larger score, then larger random tie key, then smaller id.
 __device__ __forceinline__ bool better(long long s1, uint32_t h1, int32_t c1, long long s2, uint32_t h2, int32_t c2) {
@@ -98,7 +118,7 @@ __device__ __forceinline__ uint32_t tie_hash(uint32_t tbk, int32_t v, int32_t c)
 
 // Final decision shared by the light and heavy kernels (runs on one lane).
 // Returns the target community or -1; writes predicted dQ (fixed point) / unstable flag.
-template <bool LOUV>
+template <bool LOUV, typename TT>
 __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t v, int32_t own, long long best_s,
                                                 int32_t best_c, long long kown, int have_best,
                                                 unsigned long long* dq_out, int* unstable_out) {
@@ -107,7 +127,7 @@ __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t 
     if (LOUV) {
         if (!have_best) return -1;
         const int64_t kv = a.kdeg[v];
-        const int64_t tot_own = a.tot[(int64_t)r * a.N + own];
+        const int64_t tot_own = ((const TT*)a.tot)[(int64_t)r * a.N + own];
         const long long G = best_s - kown * a.M2 + kv * (tot_own - kv);
         if (G <= 0) return -1;
         const double dq = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
@@ -120,12 +140,17 @@ __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t 
     }
 }
 
-template <bool LOUV>
+// One 16-lane tile per vertex.  Every lane first issues ALL of its (<= 4) neighbour
+// gathers (col, weight, neighbour label) so up to 4 misses per lane are in flight, then
+// inserts them into the tile's LDS hash table; the lane that creates a slot owns it and
+// evaluates that candidate community (its tot gather batched likewise).
+template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep, int64_t blen,
                                                       int64_t chunks) {
-    __shared__ int32_t s_key[TILES * HCAP];
-    __shared__ int32_t s_val[TILES * HCAP];
+    __shared__ __attribute__((aligned(16))) int32_t s_key[TILES * HCAP];
+    __shared__ __attribute__((aligned(16))) int32_t s_val[TILES * HCAP];
     __shared__ unsigned long long s_red[TILES][5];
+    constexpr int PER = LIGHT_MAX_DEG / TILE;   // neighbours per lane
     const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
     int r;
     int64_t chunk;
@@ -134,54 +159,67 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     const int rg = a.rbase + r;
     const bool rep_on = r < a.n_r && a.active[r];
     const bool valid = rep_on && i < blen;
-    const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, rg, a.iter, sweep, 1));
-    const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
     int32_t v = 0;
     int64_t rb = 0, d = 0;
     if (valid) {
+        const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, rg, a.iter, sweep, 1));
         v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
         rb = a.rowptr[v];
         d = a.rowptr[v + 1] - rb;
     }
     const bool heavy = valid && d > LIGHT_MAX_DEG;
     const bool work = valid && !heavy && d > 0;
+    const int32_t* labr = a.lab + (int64_t)r * a.N;
+    const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+    const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
+    // ---- the row's neighbour labels are STREAMED from nlab (no gather), weights alongside
+    int32_t cq[PER], wq[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int64_t j = rb + lane + TILE * q;
+        const bool ok = work && j < rb + d;
+        cq[q] = ok ? nlr[j] : -1;
+        wq[q] = ok ? (LOUV ? a.cw[j] : 1) : 0;
+    }
+    const int32_t own = work ? labr[v] : 0;
+    const int64_t kv = (LOUV && work) ? a.kdeg[v] : 0;
+    // ---- tile table: clear (16-byte stores), insert, owners evaluate
     int32_t* keys = s_key + tile * HCAP;
     int32_t* vals = s_val + tile * HCAP;
-    for (int s = lane; s < HCAP; s += TILE) { keys[s] = -1; vals[s] = 0; }
-    __syncthreads();
-    const int32_t* labr = a.lab + (int64_t)r * a.N;
-    if (work) {
-        for (int64_t j = rb + lane; j < rb + d; j += TILE) {
-            const int32_t cj = labr[a.col[j]];
-            tbl_insert(keys, vals, HCAP - 1, cj, LOUV ? a.cw[j] : 1);
-        }
+    {
+        int4* k4 = reinterpret_cast<int4*>(keys);
+        int4* v4 = reinterpret_cast<int4*>(vals);
+        for (int s = lane; s < HCAP / 4; s += TILE) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
     }
     __syncthreads();
-    int32_t own = 0;
+    int slot[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) slot[q] = cq[q] >= 0 ? tbl_insert_owner(keys, vals, HCAP - 1, cq[q], wq[q]) : -1;
+    __syncthreads();
+    TT tq[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) tq[q] = (LOUV && slot[q] >= 0 && cq[q] != own) ? totr[cq[q]] : (TT)0;
     long long best_s = LLONG_MIN, kown = 0;
     uint32_t best_h = 0;
     int32_t best_c = 0x7fffffff;
     int have = 0, ncand = 0;
-    if (work) {
-        own = labr[v];
-        const int64_t kv = a.kdeg[v];
-        const int64_t* totr = a.tot + (int64_t)r * a.N;
-        for (int s = lane; s < HCAP; s += TILE) {
-            const int32_t key = keys[s];
-            if (key < 0) continue;
-            const int32_t val = vals[s];
-            ++ncand;
-            if (key == own) kown = val;
-            long long sc;
-            if (LOUV) {
-                if (key == own) continue;
-                sc = (long long)val * a.M2 - kv * totr[key];
-            } else {
-                sc = val;
-            }
-            const uint32_t h = tie_hash(tbk, v, key);
-            if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
+    const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        if (slot[q] < 0) continue;
+        const int32_t key = cq[q];
+        const int32_t val = vals[slot[q]];
+        ++ncand;
+        if (key == own) kown = val;
+        long long sc;
+        if (LOUV) {
+            if (key == own) continue;
+            sc = (long long)val * a.M2 - kv * (long long)tq[q];
+        } else {
+            sc = val;
         }
+        const uint32_t h = tie_hash(tbk, v, key);
+        if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
     }
 #pragma unroll
     for (int off = TILE / 2; off > 0; off >>= 1) {
@@ -197,7 +235,7 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     int unst = 0;
     if (lane == 0) {
         int32_t dcs = -1;
-        if (work) dcs = decide_final<LOUV>(a, r, v, own, best_s, best_c, kown, have, &dq, &unst);
+        if (work) dcs = decide_final<LOUV, TT>(a, r, v, own, best_s, best_c, kown, have, &dq, &unst);
         if (valid) a.dec[(int64_t)r * a.S + i] = dcs;   // heavy rows: overwritten by k_decide_heavy
         if (heavy) {
             const int q = atomicAdd(a.heavy_cnt, 1);
@@ -214,16 +252,13 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     if (threadIdx.x < 5 && rep_on) {
         unsigned long long s = 0;
         for (int t = 0; t < TILES; ++t) s += s_red[t][threadIdx.x];
-        if (s) {
-            if (threadIdx.x == 0) atomicAdd(&a.dq[r], s);
-            else if (threadIdx.x == 1) atomicAdd(&a.unstable[r], s);
-            else atomicAdd(&a.stats[threadIdx.x - 2], s);
-        }
+        // fields: s_red 0 dq -> 0, 1 unstable -> 1, 2 verts -> 3, 3 entries -> 4, 4 cands -> 5
+        if (s) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), s);
     }
 }
 
 // Workgroup per high-degree vertex.  Table in LDS when it fits, else a global slice.
-template <bool LOUV>
+template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int sweep) {
     __shared__ int32_t s_key[HEAVY_LDS_SLOTS];
     __shared__ int32_t s_val[HEAVY_LDS_SLOTS];
@@ -254,12 +289,13 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         for (uint32_t s = threadIdx.x; s < slots; s += TB) { keys[s] = -1; vals[s] = 0; }
         __syncthreads();
         const int32_t* labr = a.lab + (int64_t)r * a.N;
+        const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
         for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB)
-            tbl_insert(keys, vals, slots - 1, labr[a.col[j]], LOUV ? a.cw[j] : 1);
+            tbl_insert(keys, vals, slots - 1, nlr[j], LOUV ? a.cw[j] : 1);
         __syncthreads();
         const int32_t own = labr[v];
         const int64_t kv = a.kdeg[v];
-        const int64_t* totr = a.tot + (int64_t)r * a.N;
+        const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
         long long best_s = LLONG_MIN, kown = 0;
         uint32_t best_h = 0;
         int32_t best_c = 0x7fffffff;
@@ -272,7 +308,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
             long long sc;
             if (LOUV) {
                 if (key == own) continue;
-                sc = (long long)val * a.M2 - kv * totr[key];
+                sc = (long long)val * a.M2 - kv * (long long)totr[key];
             } else {
                 sc = val;
             }
@@ -297,16 +333,16 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         if (threadIdx.x == 0) {
             unsigned long long dq = 0;
             int unst = 0;
-            const int32_t dcs = decide_final<LOUV>(a, r, v, own, r_s[0], r_c[0], r_kown[0], r_have[0], &dq, &unst);
+            const int32_t dcs = decide_final<LOUV, TT>(a, r, v, own, r_s[0], r_c[0], r_kown[0], r_have[0], &dq, &unst);
             a.dec[(int64_t)r * a.S + i] = dcs;
-            if (dq) atomicAdd(&a.dq[r], dq);
-            if (unst) atomicAdd(&a.unstable[r], 1ull);
+            if (dq) atomicAdd(red_slot(a, r, 0), dq);
+            if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
         }
         __syncthreads();
     }
 }
 
-template <bool LOUV>
+template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, int64_t blen) {
     const int r = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -319,16 +355,29 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, 
             int32_t* l = a.lab + (int64_t)r * a.N + v;
             const int32_t old = *l;
             *l = d;
+            int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+            for (int64_t j = a.rowptr[v]; j < a.rowptr[v + 1]; ++j) nlr[a.rev[j]] = d;
             if (LOUV) {
-                const long long kv = a.kdeg[v];
-                atomicAdd((unsigned long long*)&a.tot[(int64_t)r * a.N + old], (unsigned long long)(-kv));
-                atomicAdd((unsigned long long*)&a.tot[(int64_t)r * a.N + d], (unsigned long long)kv);
+                TT* tot = (TT*)a.tot + (int64_t)r * a.N;
+                const TT kv = (TT)a.kdeg[v];
+                if constexpr (sizeof(TT) == 8) {
+                    atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
+                    atomicAdd((unsigned long long*)&tot[d], (unsigned long long)kv);
+                } else {
+                    atomicAdd((int*)&tot[old], -(int)kv);
+                    atomicAdd((int*)&tot[d], (int)kv);
+                }
             }
             moved = 1;
         }
     }
     const unsigned long long b = __ballot(moved);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&a.moves[r], (unsigned long long)__popcll(b));
+    __shared__ unsigned long long s_mv;
+    if (threadIdx.x == 0) s_mv = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&s_mv, (unsigned long long)__popcll(b));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_mv) atomicAdd(red_slot(a, r, 2), s_mv);
 }
 
 // End of sweep: python-louvain stops a level when the pass gained < 1e-7 modularity or
@@ -339,25 +388,48 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
+        unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long* base = a.red + (size_t)r * NSH * RF;
+        for (int sh = 0; sh < NSH; ++sh)
+            for (int k = 0; k < RF; ++k) { f[k] += base[sh * RF + k]; base[sh * RF + k] = 0; }
+        a.sacc[4 * r + 0] += f[3]; a.sacc[4 * r + 1] += f[4]; a.sacc[4 * r + 2] += f[5];
         if (a.active[r]) {
             bool stop;
-            if (LOUV) stop = a.moves[r] == 0 || ((double)a.dq[r] / DQ_SCALE) < 1e-7;
-            else stop = a.unstable[r] == 0;
+            if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < 1e-7;
+            else stop = f[1] == 0;
             if (stop) a.active[r] = 0;
             else atomicAdd(&cnt, 1);
         }
-        a.dq[r] = 0; a.moves[r] = 0; a.unstable[r] = 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) *n_active_out = cnt;
 }
 
-__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab, int64_t* tot, int louv) {
+__global__ void k_nlab_init(int64_t m2, const int32_t* col, int32_t* nlab) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m2) nlab[(int64_t)blockIdx.y * m2 + j] = col[j];
+}
+
+template <typename TT>
+__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab, TT* tot, int louv) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
     if (v >= n) return;
     lab[(int64_t)r * n + v] = (int32_t)v;
-    if (louv) tot[(int64_t)r * n + v] = kdeg[v];
+    if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
+}
+
+// One bucket: decide (light + heavy rows) against the state left by earlier buckets, apply.
+template <bool LOUV, typename TT>
+static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, int64_t blen, bool any_heavy) {
+    const int64_t chunks = (blen + TILES - 1) / TILES;
+    FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
+    const int ev = timer_begin(c);
+    k_decide_light<LOUV, TT><<<(unsigned)(chunks * a.n_r), TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
+    timer_end(c, 4, ev);
+    if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
+    dim3 ag(nblk(blen), a.n_r);
+    k_apply<LOUV, TT><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
 }
 
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
@@ -372,17 +444,19 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int B = (int)std::min<int64_t>(c.buckets, N);
     const int64_t S = (N + B - 1) / B;
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
-    int64_t* tot = louv ? ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
+    // tot in int32 whenever every community total fits (all <= 2M < 2^31): half the gathers
+    const bool tot32 = g.M2 <= 0x7fffffffll;
+    void* tot = louv ? (void*)ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
     int32_t* dec = ensure<int32_t>(c.dec, (size_t)rcount * S);
-    // per-replica: active i32 | dq u64 | moves u64 | unstable u64 | stats u64[4] | n_active i32
-    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * 32 + 128);
+    const int64_t m2 = 2 * g.m;
+    int32_t* nlab = ensure<int32_t>(c.nlab, (size_t)rcount * (m2 > 0 ? m2 : 1));
+    // per-replica state: active i32 [n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active
+    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * (4 + 8 * NSH * RF + 32) + 256);
     int32_t* active = (int32_t*)rs;
-    unsigned long long* dq = (unsigned long long*)(rs + (((size_t)rcount * 4 + 15) & ~size_t(15)));
-    unsigned long long* moves = dq + rcount;
-    unsigned long long* unstable = moves + rcount;
-    unsigned long long* stats = unstable + rcount;
-    int32_t* n_active = (int32_t*)(stats + 4);
-    const size_t zero_bytes = (char*)(n_active + 1) - (char*)dq;
+    unsigned long long* red = (unsigned long long*)(rs + (((size_t)rcount * 4 + 255) & ~size_t(255)));
+    unsigned long long* sacc = red + (size_t)rcount * NSH * RF;
+    int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);
+    const size_t zero_bytes = (char*)(n_active + 1) - (char*)red;
     int32_t* heavy = ensure<int32_t>(c.heavy_list, 2 * (size_t)rcount * S + 2);
     int32_t* heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
     int64_t heavy_slots = 1;
@@ -395,9 +469,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         FC_HIP(hipMemcpyAsync(active, ones.data(), sizeof(int32_t) * rcount, hipMemcpyHostToDevice, c.stream));
         sync(c);  // `ones` is pageable host memory
     }
-    FC_HIP(hipMemsetAsync(dq, 0, zero_bytes, c.stream));
+    FC_HIP(hipMemsetAsync(red, 0, zero_bytes, c.stream));
     dim3 ig(nblk(N), rcount);
-    k_cd_init<<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, tot, louv ? 1 : 0);
+    if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, (int32_t*)tot, louv ? 1 : 0);
+    else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, (int64_t*)tot, louv ? 1 : 0);
+    if (m2 > 0) k_nlab_init<<<dim3(nblk(m2), rcount), TB, 0, c.stream>>>(m2, g.col.as<int32_t>(), nlab);
     FC_REQUIRE(!louv || (double)g.max_kdeg * (double)g.M2 < 4.0e18, FC_ELIMIT,
                "edge weights too large for exact int64 modularity gains");
 
@@ -406,9 +482,9 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
-    a.dq = dq; a.moves = moves; a.unstable = unstable;
+    a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
+    a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
-    a.stats = stats;
 
     int n_act = (g.M2 > 0) ? rcount : 0;
     int sweep = 0;
@@ -418,19 +494,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         for (int k = 0; k < B; ++k) {
             const int64_t blen = std::min<int64_t>(S, N - (int64_t)k * S);
             if (blen <= 0) continue;
-            const int64_t chunks = (blen + TILES - 1) / TILES;
-            FC_HIP(hipMemsetAsync(heavy_cnt, 0, sizeof(int32_t), c.stream));
-            const int ev = timer_begin(c);
-            if (louv) k_decide_light<true><<<(unsigned)(chunks * rcount), TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
-            else k_decide_light<false><<<(unsigned)(chunks * rcount), TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
-            timer_end(c, 4, ev);
-            if (g.max_deg > LIGHT_MAX_DEG) {
-                if (louv) k_decide_heavy<true><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
-                else k_decide_heavy<false><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
-            }
-            dim3 ag(nblk(blen), rcount);
-            if (louv) k_apply<true><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
-            else k_apply<false><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
+            const bool hv = g.max_deg > LIGHT_MAX_DEG;
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, blen, hv);
+            else sub_round<true, int64_t>(c, a, k, sweep, blen, hv);
         }
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
@@ -439,12 +506,18 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         n_act = ((int32_t*)c.hpin)[0];
     }
     // light-kernel traffic counters for the roofline model
-    FC_HIP(hipMemcpyAsync(c.hpin, stats, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
+    std::vector<unsigned long long> sa(4 * (size_t)rcount);
+    FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
     sync(c);
+    c.hpin[0] = c.hpin[1] = c.hpin[2] = 0;
+    for (int r = 0; r < rcount; ++r) { c.hpin[0] += sa[4 * r]; c.hpin[1] += sa[4 * r + 1]; c.hpin[2] += sa[4 * r + 2]; }
     // algorithmic bytes of the light decide kernel: per vertex rowptr 16 + kdeg 8 + own
-    // label 4 + own tot 8 + decision 4; per adjacency entry col 4 + weight 4 + label 4;
-    // per distinct candidate community its tot 8 (louvain).
-    const int64_t db = c.hpin[0] * (louv ? 40 : 24) + c.hpin[1] * (louv ? 12 : 8) + (louv ? c.hpin[2] * 8 : 0);
+    // label 4 + own tot (4|8) + decision 4; per adjacency entry neighbour label 4 +
+    // weight 4; per distinct candidate community its tot (4|8) (louvain).  LPA: no
+    // kdeg/tot/weights.
+    const int64_t tsz = tot32 ? 4 : 8;
+    const int64_t db = louv ? c.hpin[0] * (32 + tsz) + c.hpin[1] * 8 + c.hpin[2] * tsz
+                            : c.hpin[0] * 24 + c.hpin[1] * 4;
     for (fc_stats* s : {&c.acc, &c.prof}) {
         s->cd_vertex_visits += c.hpin[0];
         s->cd_edge_visits += c.hpin[1];

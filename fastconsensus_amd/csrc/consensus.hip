@@ -116,11 +116,19 @@ __global__ __launch_bounds__(256) void k_consensus_apply(int louvain, int64_t m,
         wnew[e] = nw;
         flag[e] = keep;
     }
-    // wave64 ballot counts, then one atomic per wave
+    // wave64 ballot counts -> LDS -> one sharded atomic per block and field
+    __shared__ unsigned long long s_k, s_u;
+    if (threadIdx.x == 0) { s_k = 0; s_u = 0; }
+    __syncthreads();
     const unsigned long long bk = __ballot(keep), bu = __ballot(unc);
     if ((threadIdx.x & 63) == 0) {
-        if (bk) atomicAdd(&counters[0], (unsigned long long)__popcll(bk));
-        if (bu) atomicAdd(&counters[1], (unsigned long long)__popcll(bu));
+        if (bk) atomicAdd(&s_k, (unsigned long long)__popcll(bk));
+        if (bu) atomicAdd(&s_u, (unsigned long long)__popcll(bu));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_k) atomicAdd(shard(counters, 2, 0), s_k);
+        if (s_u) atomicAdd(shard(counters, 2, 1), s_u);
     }
 }
 
@@ -156,17 +164,16 @@ void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* parti
     int32_t* wnew = ensure<int32_t>(c.wnew, cap);
     int64_t* flag = ensure<int64_t>(c.flag, 2 * cap + 1);
     int64_t* pos = ensure<int64_t>(c.pos, 2 * cap + 1);
-    unsigned long long* ctr = (unsigned long long*)ensure<int64_t>(c.counters, 16);
-    FC_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(int64_t), c.stream));
+    unsigned long long* ctr = shards_begin(c, 2);
     const double cut = tau * (double)n_p;  // Python float64 product (fast_consensus.py:165)
     if (m > 0)
         k_consensus_apply<<<nblk(m), TB, 0, c.stream>>>(algo == FC_ALGO_LOUVAIN, m, n_p, cut, g.ew.as<int32_t>(),
                                                          partial, wnew, flag, ctr);
     FC_HIP(hipMemsetAsync(flag + m, 0, sizeof(int64_t), c.stream));
     exclusive_scan(c, flag, pos, m + 1);
-    FC_HIP(hipMemcpyAsync(c.hpin, ctr, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
-    sync(c);
-    const int64_t kept = c.hpin[0], unconv = c.hpin[1];
+    int64_t h[2];
+    shards_fold(c, 2, 0u, h);
+    const int64_t kept = h[0], unconv = h[1];
     c.kept_m = kept;
     const int64_t kc = kept > 0 ? kept : 1;
     int32_t* ku = ensure<int32_t>(c.ku, kc);
@@ -443,14 +450,20 @@ __global__ __launch_bounds__(256) void k_count_unconv(int64_t m, int n_p, const 
                                                       unsigned long long* out) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int u = (e < m) && w[e] != 0 && w[e] != n_p;
+    __shared__ unsigned long long s_u;
+    if (threadIdx.x == 0) s_u = 0;
+    __syncthreads();
     const unsigned long long b = __ballot(u);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&s_u, (unsigned long long)__popcll(b));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_u) atomicAdd(shard(out, 1, 0), s_u);
 }
 int64_t count_unconverged(Ctx& c, const int32_t* w, int64_t m, int n_p) {
-    unsigned long long* ctr = (unsigned long long*)ensure<int64_t>(c.counters, 16) + 4;
-    FC_HIP(hipMemsetAsync(ctr, 0, sizeof(int64_t), c.stream));
+    unsigned long long* ctr = shards_begin(c, 1);
     if (m > 0) k_count_unconv<<<nblk(m), TB, 0, c.stream>>>(m, n_p, w, ctr);
-    return read_i64(c, (const int64_t*)ctr);
+    int64_t h[1];
+    shards_fold(c, 1, 0u, h);
+    return h[0];
 }
 
 void closure_apply(Ctx& c, int algo, int n_p, const int32_t* counts, int iteration) {

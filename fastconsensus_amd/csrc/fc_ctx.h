@@ -37,7 +37,10 @@ struct DevBuf {
         size_t nb = bytes ? bytes + bytes / 2 : 0;
         if (nb < need) nb = need;
         nb = (nb + 255) & ~size_t(255);
-        if (p) FC_HIP(hipFree(p));
+        if (p) {
+            FC_HIP(hipDeviceSynchronize());  // queued kernels may still use the old buffer
+            FC_HIP(hipFree(p));
+        }
         p = nullptr;
         FC_HIP(hipMalloc(&p, nb));
         bytes = nb;
@@ -55,12 +58,13 @@ struct Graph {
     int64_t m = 0;
     DevBuf eu, ev, ew, eage;        // int32, int32, int32, int64  [m]
     DevBuf rowptr, col, cw, ceid;   // int64 [N+1], int32 [2m] x3
+    DevBuf crev;                    // int32 [2m]: index of the reverse entry (v->u for u->v)
     DevBuf kdeg;                    // int64 [N] weighted degree
     int64_t M2 = 0;                 // sum of kdeg = 2 * total weight
     int32_t max_deg = 0;
     int64_t max_kdeg = 0;
     void release() {
-        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &kdeg};
+        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &crev, &kdeg};
         for (auto* x : b) x->release();
     }
 };
@@ -84,6 +88,7 @@ struct Ctx {
     // replica state (replica-major [n_r][N])
     int n_r = 0, rbase = 0, n_p_total = 0;
     DevBuf lab, tot, dec, labT;     // int32 [n_r][N], int64 [n_r][N], int32 [n_r][S], int32 [N][ldT]
+    DevBuf nlab;                    // int32 [n_r][2m]: label of each adjacency entry's neighbour
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable
@@ -141,6 +146,9 @@ template <class T> inline T* ensure(DevBuf& b, size_t count) {
     return b.as<T>();
 }
 void sync(Ctx& c);
+// zero / fold sharded counters (CSH x F u64 in c.counters); max_mask bit f: max instead of sum
+unsigned long long* shards_begin(Ctx& c, int F);
+void shards_fold(Ctx& c, int F, unsigned max_mask, int64_t* host_out);
 int64_t read_i64(Ctx& c, const int64_t* dev);
 
 constexpr int64_t AGE_ITER_SHIFT = 40;

@@ -45,6 +45,36 @@ template void sort_pairs_public<uint64_t, int32_t>(Ctx&, const uint64_t*, uint64
                                                    int64_t, int);
 
 void sync(Ctx& c) { FC_HIP(hipStreamSynchronize(c.stream)); }
+
+__global__ void k_reduce_shards(unsigned long long* base, int F, unsigned max_mask) {
+    __shared__ unsigned long long s[CSH];
+    for (int f = 0; f < F; ++f) {
+        const bool mx = (max_mask >> f) & 1u;
+        s[threadIdx.x] = base[(size_t)threadIdx.x * F + f];
+        __syncthreads();
+        for (int o = CSH / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) {
+                const unsigned long long a = s[threadIdx.x], b = s[threadIdx.x + o];
+                s[threadIdx.x] = mx ? (a > b ? a : b) : a + b;
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) base[(size_t)CSH * F + f] = s[0];
+        __syncthreads();
+    }
+}
+unsigned long long* shards_begin(Ctx& c, int F) {
+    unsigned long long* base = (unsigned long long*)ensure<int64_t>(c.counters, (size_t)(CSH + 1) * F);
+    FC_HIP(hipMemsetAsync(base, 0, sizeof(unsigned long long) * CSH * F, c.stream));
+    return base;
+}
+void shards_fold(Ctx& c, int F, unsigned max_mask, int64_t* host_out) {
+    unsigned long long* base = (unsigned long long*)c.counters.p;
+    k_reduce_shards<<<1, CSH, 0, c.stream>>>(base, F, max_mask);
+    FC_HIP(hipMemcpyAsync(c.hpin, base + (size_t)CSH * F, sizeof(int64_t) * F, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    for (int f = 0; f < F; ++f) host_out[f] = c.hpin[f];
+}
 int64_t read_i64(Ctx& c, const int64_t* dev) {
     FC_HIP(hipMemcpyAsync(c.hpin, dev, sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
     sync(c);
@@ -143,6 +173,7 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
     cp(dst.eu, src.eu, 4 * m); cp(dst.ev, src.ev, 4 * m); cp(dst.ew, src.ew, 4 * m); cp(dst.eage, src.eage, 8 * m);
     cp(dst.rowptr, src.rowptr, 8 * (n + 1));
     cp(dst.col, src.col, 8 * m); cp(dst.cw, src.cw, 8 * m); cp(dst.ceid, src.ceid, 8 * m);
+    cp(dst.crev, src.crev, 8 * m);
     cp(dst.kdeg, src.kdeg, 8 * n);
     dst.m = src.m; dst.M2 = src.M2; dst.max_deg = src.max_deg; dst.max_kdeg = src.max_kdeg;
     c.labT_valid = false;
@@ -169,25 +200,36 @@ __global__ void k_iota_ev(int64_t m, const int32_t* ev, uint32_t* key, int32_t* 
 // Row x = [neighbours u < x, ascending] ++ [neighbours v > x, ascending]: fully sorted rows.
 __global__ void k_fill_upper(int64_t m, const int32_t* eu, const int32_t* ev, const int32_t* ew,
                              const int64_t* rowptr, const int64_t* ustart, const int64_t* vstart,
-                             int32_t* col, int32_t* cw, int32_t* ceid) {
+                             int32_t* col, int32_t* cw, int32_t* ceid, int32_t* posu) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
     int32_t u = eu[e];
     int64_t nlow = vstart[u + 1] - vstart[u];
     int64_t p = rowptr[u] + nlow + (e - ustart[u]);
     col[p] = ev[e]; cw[p] = ew[e]; ceid[p] = (int32_t)e;
+    posu[e] = (int32_t)p;
 }
 __global__ void k_fill_lower(int64_t m, const int32_t* perm, const int32_t* eu, const int32_t* ev,
                              const int32_t* ew, const int64_t* rowptr, const int64_t* vstart, int32_t* col,
-                             int32_t* cw, int32_t* ceid) {
+                             int32_t* cw, int32_t* ceid, int32_t* posv) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= m) return;
     int32_t e = perm[f];
     int32_t v = ev[e];
     int64_t p = rowptr[v] + (f - vstart[v]);
     col[p] = eu[e]; cw[p] = ew[e]; ceid[p] = e;
+    posv[e] = (int32_t)p;
 }
-__global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int64_t* kdeg, int64_t* red) {
+// rev[j] = position of the reverse adjacency entry (the same undirected edge seen from
+// the other endpoint): moving vertex v updates nlab at rev[j] for each j in row(v).
+__global__ void k_fill_rev(int64_t m, const int32_t* posu, const int32_t* posv, int32_t* rev) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const int32_t a = posu[e], b = posv[e];
+    rev[a] = b;
+    rev[b] = a;
+}
+__global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int64_t* kdeg, unsigned long long* red) {
     int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int64_t s = 0, d = 0;
     if (x < n) {
@@ -208,9 +250,9 @@ __global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int6
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        atomicAdd((unsigned long long*)&red[0], (unsigned long long)ss[0]);
-        atomicMax((long long*)&red[1], sd[0]);
-        atomicMax((long long*)&red[2], sk[0]);
+        atomicAdd(shard(red, 3, 0), (unsigned long long)ss[0]);
+        atomicMax(shard(red, 3, 1), (unsigned long long)sd[0]);
+        atomicMax(shard(red, 3, 2), (unsigned long long)sk[0]);
     }
 }
 
@@ -238,20 +280,23 @@ void graph_build_csr(Ctx& c, Graph& g) {
         int32_t* i2 = (int32_t*)ensure<int64_t>(c.midx2, m);
         k_iota_ev<<<nblk(m), TB, 0, c.stream>>>(m, g.ev.as<int32_t>(), k1, i1);
         sort_pairs(c, (const uint32_t*)k1, k2, (const int32_t*)i1, i2, m, c.key_bits);
+        int32_t* posu = (int32_t*)k1;   // sort inputs are dead once the sort is enqueued
+        int32_t* posv = i1;
+        int32_t* rev = ensure<int32_t>(g.crev, m2);
         k_fill_upper<<<nblk(m), TB, 0, c.stream>>>(m, g.eu.as<int32_t>(), g.ev.as<int32_t>(), g.ew.as<int32_t>(),
-                                                    rowptr, us, vs, col, cw, ceid);
+                                                    rowptr, us, vs, col, cw, ceid, posu);
         k_fill_lower<<<nblk(m), TB, 0, c.stream>>>(m, i2, g.eu.as<int32_t>(), g.ev.as<int32_t>(),
-                                                    g.ew.as<int32_t>(), rowptr, vs, col, cw, ceid);
+                                                    g.ew.as<int32_t>(), rowptr, vs, col, cw, ceid, posv);
+        k_fill_rev<<<nblk(m), TB, 0, c.stream>>>(m, posu, posv, rev);
     }
     int64_t* kdeg = ensure<int64_t>(g.kdeg, n);
-    int64_t* red = ensure<int64_t>(c.counters, 16);
-    FC_HIP(hipMemsetAsync(red, 0, 3 * sizeof(int64_t), c.stream));
+    unsigned long long* red = shards_begin(c, 3);
     k_kdeg<<<nblk(n), TB, 0, c.stream>>>(n, rowptr, cw, kdeg, red);
-    FC_HIP(hipMemcpyAsync(c.hpin, red, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c.stream));
-    sync(c);
-    g.M2 = c.hpin[0];
-    g.max_deg = (int32_t)c.hpin[1];
-    g.max_kdeg = c.hpin[2];
+    int64_t h[3];
+    shards_fold(c, 3, 0x6u, h);
+    g.M2 = h[0];
+    g.max_deg = (int32_t)h[1];
+    g.max_kdeg = h[2];
 }
 
 // ------------------------------------------------------------------ merge

@@ -18,6 +18,7 @@ for s in "$@"; do
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench100k) step bench_100k 600 python bench.py --config lfr100k --steps 2 --warmup 1 --no-cpu-baseline ;;
         bench1m) step bench_1m 900 python bench.py --steps 2 --warmup 1 ;;
+        bench1m_fast) step bench_1m 900 python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
