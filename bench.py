@@ -101,6 +101,9 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--buckets", type=int, default=0)
+    ap.add_argument("--chunk", type=int, default=-1, help="CD visit-order chunk (engine option; -1 = default)")
+    ap.add_argument("--ids", default="generator", choices=["generator", "planted"],
+                    help="experiment: renumber node ids by planted community before loading")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -121,10 +124,17 @@ def main():
 
     t0 = time.time()
     n, u, v, planted = make_graph(cfg, args.seed)
+    if args.ids == "planted" and planted is not None:
+        order = np.argsort(planted, kind="stable")
+        newid = np.empty(n, np.int32)
+        newid[order] = np.arange(n, dtype=np.int32)
+        u, v = newid[u], newid[v]
     log("[rank %d] graph n=%d m=%d generated in %.1fs" % (rank, n, len(u), time.time() - t0))
     eng = fc.Engine(device=local, seed=args.seed)
     if args.buckets:
         eng.set_params(buckets=args.buckets)
+    if args.chunk >= 0:
+        eng.set_option("chunk", args.chunk)
     t0 = time.time()
     eng.load_graph(n, u, v)
     torch.cuda.synchronize()

@@ -69,6 +69,9 @@ class Engine:
     def set_params(self, buckets=0, max_sweeps=0, max_iters=0):
         check(self._L.fc_set_params(self._ctx, int(buckets), int(max_sweeps), int(max_iters)))
 
+    def set_option(self, name, value):
+        check(self._L.fc_set_option(self._ctx, _lib.OPTIONS[name], int(value)))
+
     # -- graph -----------------------------------------------------------------------
     def load_graph(self, n, u, v):
         u = np.ascontiguousarray(u, dtype=np.int32)

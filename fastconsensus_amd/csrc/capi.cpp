@@ -163,6 +163,22 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters) {
     FC_API_END
 }
 
+int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    switch (option) {
+        case FC_OPT_BUCKETS: FC_REQUIRE(value >= 1, FC_EINVAL, "buckets >= 1"); c.buckets = (int)value; break;
+        case FC_OPT_MAX_SWEEPS: FC_REQUIRE(value >= 1, FC_EINVAL, "max_sweeps >= 1"); c.max_sweeps = (int)value; break;
+        case FC_OPT_MAX_ITERS: FC_REQUIRE(value >= 1, FC_EINVAL, "max_iters >= 1"); c.max_iters = (int)value; break;
+        case FC_OPT_CHUNK:
+            FC_REQUIRE(value == 0 || value == 16, FC_EINVAL, "chunk must be 0 or 16 (one block of tiles)");
+            c.chunk = (int)value;
+            break;
+        default: throw FcError{FC_EINVAL, "unknown option"};
+    }
+    FC_API_END
+}
+
 int fc_load_graph(fc_ctx* ctx, int64_t n, int64_t m, const int32_t* u, const int32_t* v) {
     FC_CTX(ctx)
     FC_API_BEGIN

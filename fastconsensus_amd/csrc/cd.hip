@@ -49,6 +49,8 @@ static inline unsigned nblk(int64_t n, int tb = TB) {
 struct CDArgs {
     int64_t N;
     int64_t S;          // bucket size (positions per bucket)
+    int chunk;          // 0: vertex-level random order; else order over chunks of `chunk` vertices
+    uint32_t perm_n;    // permutation domain: N, or the number of chunks
     int n_r, rbase;
     uint32_t iter;
     uint64_t seed;
@@ -76,6 +78,13 @@ struct CDArgs {
 
 __device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
     return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
+}
+
+// Vertex visited at sweep position p, or -1 for a padding slot of the last chunk.
+__device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, int64_t p) {
+    if (!a.chunk) return (int32_t)perm_apply(P, (uint32_t)p);
+    const int64_t v = (int64_t)perm_apply(P, (uint32_t)(p / a.chunk)) * a.chunk + (p % a.chunk);
+    return v < a.N ? (int32_t)v : -1;
 }
 
 // Block -> (replica, chunk) with all chunks of a replica on as few XCDs as possible
@@ -158,12 +167,15 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     const int64_t i = chunk * TILES + tile;                // position inside the bucket
     const int rg = a.rbase + r;
     const bool rep_on = r < a.n_r && a.active[r];
-    const bool valid = rep_on && i < blen;
+    bool valid = rep_on && i < blen;
     int32_t v = 0;
     int64_t rb = 0, d = 0;
     if (valid) {
-        const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, rg, a.iter, sweep, 1));
-        v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
+        const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
+        v = pos_vertex(a, P, bucket * a.S + i);
+        valid = v >= 0;
+    }
+    if (valid) {
         rb = a.rowptr[v];
         d = a.rowptr[v + 1] - rb;
     }
@@ -236,7 +248,7 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     if (lane == 0) {
         int32_t dcs = -1;
         if (work) dcs = decide_final<LOUV, TT>(a, r, v, own, best_s, best_c, kown, have, &dq, &unst);
-        if (valid) a.dec[(int64_t)r * a.S + i] = dcs;   // heavy rows: overwritten by k_decide_heavy
+        if (rep_on && i < blen) a.dec[(int64_t)r * a.S + i] = dcs;   // heavy rows: overwritten by k_decide_heavy
         if (heavy) {
             const int q = atomicAdd(a.heavy_cnt, 1);
             a.heavy[2 * q] = r;
@@ -272,9 +284,9 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         const int r = a.heavy[2 * item];
         const int64_t i = a.heavy[2 * item + 1];
         const int rg = a.rbase + r;
-        const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, rg, a.iter, sweep, 1));
+        const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
         const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
-        const int32_t v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
+        const int32_t v = pos_vertex(a, P, bucket * a.S + i);
         const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
         uint32_t slots = 1;
         while (slots < 2 * (uint32_t)d) slots <<= 1;
@@ -350,8 +362,8 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, 
     if (i < blen && a.active[r]) {
         const int32_t d = a.dec[(int64_t)r * a.S + i];
         if (d >= 0) {
-            const Perm P = make_perm((uint32_t)a.N, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
-            const int32_t v = (int32_t)perm_apply(P, (uint32_t)(bucket * a.S + i));
+            const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
+            const int32_t v = pos_vertex(a, P, bucket * a.S + i);
             int32_t* l = a.lab + (int64_t)r * a.N + v;
             const int32_t old = *l;
             *l = d;
@@ -441,8 +453,13 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     Graph& g = c.g;
     c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
     c.labT_valid = false;
-    const int B = (int)std::min<int64_t>(c.buckets, N);
-    const int64_t S = (N + B - 1) / B;
+    // sweep positions: vertices in a random order, or whole chunks of `chunk` consecutive
+    // vertices in a random chunk order (coalesced per-vertex accesses inside a block)
+    const int CH = c.chunk;
+    const int64_t NC = CH ? (N + CH - 1) / CH : N;
+    const int64_t PN = CH ? NC * CH : N;
+    const int B = (int)std::min<int64_t>(c.buckets, NC);
+    const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
     // tot in int32 whenever every community total fits (all <= 2M < 2^31): half the gathers
     const bool tot32 = g.M2 <= 0x7fffffffll;
@@ -478,7 +495,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                "edge weights too large for exact int64 modularity gains");
 
     CDArgs a;
-    a.N = N; a.S = S; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
+    a.N = N; a.S = S; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
@@ -492,7 +509,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         c.acc.cd_sweeps += n_act;
         c.prof.cd_sweeps += n_act;
         for (int k = 0; k < B; ++k) {
-            const int64_t blen = std::min<int64_t>(S, N - (int64_t)k * S);
+            const int64_t blen = std::min<int64_t>(S, PN - (int64_t)k * S);
             if (blen <= 0) continue;
             const bool hv = g.max_deg > LIGHT_MAX_DEG;
             if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv);

@@ -112,6 +112,7 @@ struct Ctx {
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)
     // params
     int buckets = 32, max_sweeps = 200, max_iters = 1000;
+    int chunk = 0;                  // CD order granularity (0 = per vertex), FC_OPT_CHUNK
     Timer timer;
     fc_stats acc{};                 // accumulated during a run (fc_run)
     fc_stats prof{};                // accumulated since the last fc_collect_timing

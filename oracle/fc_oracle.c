@@ -477,29 +477,36 @@ static inline int tw_better(long long s1, uint32_t h1, i32 c1, long long s2, uin
 
 /* One replica.  algo 0 = louvain local moving, 1 = lpa.  Returns sweeps executed. */
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
-                      u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, i32* lab) {
+                      u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, i32* lab) {
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
     i64* acc = (i64*)calloc((size_t)N, sizeof(i64));
     u8* seen = (u8*)calloc((size_t)N, 1);
     i32* keys = (i32*)malloc(sizeof(i32) * (size_t)(N + 1));
-    const int B = (int)(buckets < N ? buckets : N);
-    const i64 S = (N + B - 1) / B;
+    /* visit order: vertices, or chunks of `chunk` consecutive vertices, in random order */
+    const i64 NC = chunk ? (N + chunk - 1) / chunk : N;
+    const i64 PN = chunk ? NC * chunk : N;
+    const int B = (int)(buckets < NC ? buckets : NC);
+    const i64 S = chunk ? ((NC + B - 1) / B) * chunk : (N + B - 1) / B;
     i32* dec = (i32*)malloc(sizeof(i32) * (size_t)(S + 1));
     for (i64 v = 0; v < N; ++v) { lab[v] = (i32)v; tot[v] = kdeg[v]; csz[v] = 1; }
     int active = M2 > 0, sweep = 0;
     for (; sweep < max_sweeps && active; ++sweep) {
-        const tw_perm P = tw_make_perm((uint32_t)N, tw_stream_key(seed, rg, iter, (uint32_t)sweep, 1));
+        const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, rg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
         unsigned long long dq = 0, moves = 0, unstable = 0;
         for (int k = 0; k < B; ++k) {
-            i64 blen = N - (i64)k * S;
+            i64 blen = PN - (i64)k * S;
             if (blen > S) blen = S;
             if (blen <= 0) continue;
             for (i64 i = 0; i < blen; ++i) {
-                const i32 v = (i32)tw_perm_apply(&P, (uint32_t)((i64)k * S + i));
+                const i64 p = (i64)k * S + i;
+                const i64 vv = chunk ? (i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk
+                                     : (i64)tw_perm_apply(&P, (uint32_t)p);
                 dec[i] = -1;
+                if (vv >= N) continue;
+                const i32 v = (i32)vv;
                 const i64 rb = rowptr[v], re = rowptr[v + 1];
                 if (re == rb) continue;
                 i64 nk = 0;
@@ -535,7 +542,9 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
             }
             for (i64 i = 0; i < blen; ++i) {
                 if (dec[i] < 0) continue;
-                const i32 v = (i32)tw_perm_apply(&P, (uint32_t)((i64)k * S + i));
+                const i64 p = (i64)k * S + i;
+                const i32 v = chunk ? (i32)((i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk)
+                                    : (i32)tw_perm_apply(&P, (uint32_t)p);
                 const i32 old = lab[v], nw = dec[i];
                 lab[v] = nw;
                 if (louv) { tot[old] -= kdeg[v]; tot[nw] += kdeg[v]; csz[old]--; csz[nw]++; }
@@ -552,7 +561,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
 /* Replicas [rbase, rbase+n_r) of the engine's bucketed CD on a symmetric CSR.
  * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
 void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
-                   int iteration, u64 seed, int buckets, int max_sweeps, i32* lab, int* sweeps) {
+                   int iteration, u64 seed, int buckets, int max_sweeps, int chunk, i32* lab, int* sweeps) {
     i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
     i64 M2 = 0;
     for (i64 v = 0; v < N; ++v) {
@@ -564,8 +573,47 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
-                            buckets, max_sweeps, lab + (i64)r * N);
+                            buckets, max_sweeps, chunk, lab + (i64)r * N);
         if (sweeps) sweeps[r] = sw;
     }
     free(kdeg);
+}
+
+/* CPU twin of the engine's counter-based closure sampler (consensus.hip k_closure_sample):
+ * attempt t draws Philox4x32-10(counter = {t_lo, t_hi, iteration, 0x5eed}); node
+ * x = uniform over N; if x has >= 2 neighbours in the post-threshold CSR (sorted rows),
+ * two distinct positions i1 != i2 uniformly.  Writes the pair (a, b) or (-1, -1).
+ * Feeding these pairs to orc_closure_pairs reproduces the device's candidates. */
+typedef struct { uint32_t x, y, z, w; } tw_u4;
+static tw_u4 tw_philox(tw_u4 c, uint32_t k0, uint32_t k1) {
+    for (int i = 0; i < 10; ++i) {
+        u64 p0 = (u64)0xD2511F53u * c.x, p1 = (u64)0xCD9E8D57u * c.z;
+        tw_u4 n;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
+        c = n;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+static inline uint32_t tw_below(uint32_t r, uint32_t n) { return (uint32_t)(((u64)r * n) >> 32); }
+void orc_closure_sample(i64 N, const i64* krowptr, const i32* kcol, i64 attempts, u64 seed, int iteration,
+                        i32* pairs) {
+    const u64 s = tw_mix64(seed ^ 0xC105u);
+    const uint32_t k0 = (uint32_t)s, k1 = (uint32_t)(s >> 32);
+    for (i64 t = 0; t < attempts; ++t) {
+        tw_u4 ctr = {(uint32_t)t, (uint32_t)((u64)t >> 32), (uint32_t)iteration, 0x5eedu};
+        const tw_u4 r = tw_philox(ctr, k0, k1);
+        const i32 x = (i32)tw_below(r.x, (uint32_t)N);
+        const i64 rb = krowptr[x], d = krowptr[x + 1] - rb;
+        pairs[2 * t] = pairs[2 * t + 1] = -1;
+        if (d < 2) continue;
+        const uint32_t i1 = tw_below(r.y, (uint32_t)d);
+        uint32_t i2 = tw_below(r.z, (uint32_t)(d - 1));
+        if (i2 >= i1) ++i2;
+        pairs[2 * t] = kcol[rb + i1];
+        pairs[2 * t + 1] = kcol[rb + i2];
+    }
 }

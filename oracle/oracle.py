@@ -63,7 +63,8 @@ def lib():
         L.orc_modularity.argtypes = [i64, _i64p, _i32p, ctypes.c_void_p, _i32p]
         L.orc_modularity.restype = dbl
         L.orc_engine_cd.argtypes = [ctypes.c_int, i64, _i64p, _i32p, _i32p, ctypes.c_int, ctypes.c_int,
-                                    ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
+                                    ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
+        L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
         _lib = L
     return _lib
@@ -172,6 +173,14 @@ def closure_from_pairs(algo, g, pairs, labels, n_p):
     return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), of[:k].copy()
 
 
+def closure_sample_pairs(kept, attempts, seed, iteration):
+    """Engine's device sampler, restated: the (a, b) pair of every attempt (or (-1, -1))."""
+    rowptr, col, _ = kept.csr()
+    pairs = np.empty((max(int(attempts), 1), 2), np.int32)
+    lib().orc_closure_sample(kept.N, rowptr, col, int(attempts), int(seed) & (2**64 - 1), int(iteration), pairs)
+    return pairs[:attempts]
+
+
 def repair(old, deg):
     """deg: int64 degrees of nextgraph after closure (updated in place)."""
     k_max = old.N
@@ -189,13 +198,13 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     return lab, sw
 
 
-def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200):
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=0):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels)."""
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)
     lib().orc_engine_cd(algo, g.N, rowptr, col, cw, n_r, rbase, iteration, int(seed) & (2**64 - 1), buckets,
-                        max_sweeps, lab, sw)
+                        max_sweeps, chunk, lab, sw)
     return lab, sw
 
 

@@ -1,0 +1,101 @@
+"""CPU model of the engine's step API, built on the oracle (TEST INFRASTRUCTURE ONLY).
+
+Drives fastconsensus_amd.distributed.run_sharded over gloo on CPU (the multi-rank logic:
+replica ranges, k_last MAX / count SUM all-reduces, identical replicated updates), and is
+compared bit-for-bit with the HIP engine on the GPU.  It restates the engine's semantics:
+bucketed CD (oracle twin), closed-form consensus rule, counter-based closure sampler,
+isolate repair and the age model.
+"""
+import numpy as np
+
+from oracle import oracle as orc
+
+
+class OracleEngine:
+    def __init__(self, seed, buckets=32, chunk=0):
+        self.seed = int(seed)
+        self.buckets = buckets
+        self.chunk = chunk
+        self.lab = None
+
+    # graph -----------------------------------------------------------------------------
+    def load_graph(self, n, u, v):
+        self.g0 = orc.EdgeGraph.from_lines(n, np.stack([np.asarray(u), np.asarray(v)], 1))
+        self.m0 = self.g0.m
+        self.reset_graph()
+
+    def set_stream(self, s):
+        pass
+
+    def reset_graph(self):
+        g = self.g0
+        self.g = orc.EdgeGraph(g.N, g.u.copy(), g.v.copy(), g.w.copy(), g.age.copy())
+
+    def graph_info(self):
+        return self.g.N, self.g.m, self.m0
+
+    @property
+    def m(self):
+        return self.g.m
+
+    # steps -----------------------------------------------------------------------------
+    def cd(self, algo, r0, count, n_p, iteration):
+        self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
+                                    chunk=self.chunk)
+        self.r0 = r0
+
+    def consensus_partial(self, algo, out):
+        g, lab = self.g, self.lab
+        diff = lab[:, g.u] != lab[:, g.v]
+        if algo == 0:
+            idx = lab.shape[0] - 1 - np.argmax(diff[::-1], axis=0)
+            res = np.where(diff.any(0), self.r0 + idx, -1)
+        else:
+            res = (~diff).sum(0)
+        out.numpy()[:g.m] = res
+
+    def consensus_apply(self, algo, n_p, tau, delta, part):
+        g = self.g
+        p = part.numpy()[:g.m].astype(np.int64)
+        if algo == 0:
+            nw = np.where((g.w == 0) | (g.w == n_p), 0, np.where(p < 0, n_p, g.w + n_p - 1 - p))
+        else:
+            nw = p
+        nw = nw.astype(np.int32)
+        keep = orc.threshold(nw, tau, n_p)
+        self.kept = orc.EdgeGraph(g.N, g.u[keep], g.v[keep], nw[keep], g.age[keep])
+        conv, cnt = orc.check(self.kept.w, n_p, delta)
+        return (conv if algo == 0 else False), self.kept.m, cnt
+
+    def closure_sample(self, attempts, iteration):
+        pairs = orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration)
+        dummy = np.zeros((1, self.g.N), np.int32)
+        cu, cv, _, cf = orc.closure_from_pairs(1, self.kept, pairs, dummy, 1)
+        order = np.lexsort((cv, cu))                  # the device keeps candidates key-sorted
+        self.cand = (cu[order], cv[order], cf[order])
+        return len(cu)
+
+    def closure_partial(self, out):
+        cu, cv, _ = self.cand
+        out.numpy()[:len(cu)] = (self.lab[:, cu] == self.lab[:, cv]).sum(0)
+
+    def closure_apply(self, algo, n_p, delta, counts, iteration):
+        cu, cv, cf = self.cand
+        base = np.int64(iteration + 1) << orc.AGE_ITER_SHIFT
+        w = counts.numpy()[:len(cu)].astype(np.int32) if (algo == 0 and counts is not None) else \
+            np.zeros(len(cu), np.int32)
+        closure = orc.EdgeGraph(self.g.N, cu, cv, w, base + cf)
+        parts = [self.kept, closure]
+        if algo == 0:
+            deg = self.kept.degrees() + closure.degrees()
+            ru, rv, rw, rx = orc.repair(self.g, deg)
+            parts.append(orc.EdgeGraph(self.g.N, ru, rv, rw, base + orc.AGE_REPAIR_OFFSET + rx))
+        self.g = orc.concat(parts)
+        conv, _ = orc.check(self.g.w, n_p, delta)
+        return conv, self.g.m
+
+    def get_labels(self, count, renumber=False):
+        return orc.renumber(self.lab) if renumber else self.lab.copy()
+
+    def get_graph(self):
+        return self.g.u, self.g.v, self.g.w, self.g.age

@@ -146,16 +146,17 @@ def _lfr1k_graph():
 
 
 @pytest.mark.parametrize("algo", [0, 1])
-@pytest.mark.parametrize("buckets", [32, 5])
-def test_cd_bit_exact_vs_twin(fcmod, algo, buckets):
+@pytest.mark.parametrize("buckets,chunk", [(32, 0), (5, 0), (32, 16), (7, 16)])
+def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk):
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=99)
     eng.set_params(buckets=buckets)
+    eng.set_option("chunk", chunk)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 4)
     got = eng.get_labels(n_r)
-    exp, sw = orc.engine_cd(algo, g, n_r, 0, 4, 99, buckets=buckets)
+    exp, sw = orc.engine_cd(algo, g, n_r, 0, 4, 99, buckets=buckets, chunk=chunk)
     np.testing.assert_array_equal(got, exp)
     # sharding invariance: replicas 2..4 alone give the same labelings
     eng.cd(algo, 2, 3, n_r, 4)
@@ -184,15 +185,16 @@ def _heavy_graph(seed, hub_deg):
 
 
 @pytest.mark.parametrize("algo", [0, 1])
-@pytest.mark.parametrize("hub_deg", [300, 3000])
-def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg):
+@pytest.mark.parametrize("hub_deg,chunk", [(300, 0), (3000, 0), (3000, 16)])
+def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk):
     N, e = _heavy_graph(5, hub_deg)
     g = orc.EdgeGraph.from_lines(N, e)
     eng = fcmod.Engine(seed=7)
+    eng.set_option("chunk", chunk)
     eng.load_graph(N, e[:, 0], e[:, 1])
     eng.cd(algo, 0, 4, 4, 1)
     got = eng.get_labels(4)
-    exp, _ = orc.engine_cd(algo, g, 4, 0, 1, 7)
+    exp, _ = orc.engine_cd(algo, g, 4, 0, 1, 7, chunk=chunk)
     np.testing.assert_array_equal(got, exp)
     eng.close()
 
@@ -298,4 +300,34 @@ def test_closure_sampler_properties(fcmod):
     for a, b, c, _ in closure[:2000]:
         assert nbrs[a] & nbrs[b], "closure edge must close a 2-path"
         assert c == int((lab[:, a] == lab[:, b]).sum())
+    eng.close()
+
+
+# ------------------------------------------------------------------------- whole runs, bit-exact
+@pytest.mark.parametrize("algo,n_p,tau,chunk", [(0, 10, 0.2, 0), (0, 12, 0.2, 16), (1, 4, 0.8, 0), (0, 20, 0.2, 0)])
+def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk):
+    """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
+    loop (bucketed CD twin, consensus rule, Philox closure sampler, repair, ages): final
+    partitions AND the final graph are identical (n_p=10 runs 9 iterations)."""
+    from fastconsensus_amd.distributed import run_sharded
+    from tests.cpu_engine import OracleEngine
+    case, _ = _lfr1k_graph()
+    e = case.edges_file
+    cpu = OracleEngine(seed=17, chunk=chunk)
+    cpu.load_graph(case.N, e[:, 0], e[:, 1])
+    exp_labels, exp_st = run_sharded(cpu, algo, n_p, tau, 0.02, device="cpu", max_iters=50)
+    eng = fcmod.Engine(seed=17)
+    eng.set_option("chunk", chunk)
+    eng.set_params(max_iters=50)
+    eng.load_graph(case.N, e[:, 0], e[:, 1])
+    labels, st = eng.run(algo, n_p, tau, 0.02)
+    assert st["iterations"] == exp_st["iterations"]
+    assert st["partition_edges"] == exp_st["partition_edges"]
+    np.testing.assert_array_equal(labels, exp_labels)
+    for a, b in zip(eng.get_graph(), cpu.get_graph()):
+        np.testing.assert_array_equal(a, b)
+    # the Python sharded driver (world = 1, torch stream) == the native driver
+    labels2, st2 = run_sharded(eng, algo, n_p, tau, 0.02, device="cuda")
+    np.testing.assert_array_equal(labels2, labels)
+    assert st2["partition_edges"] == st["partition_edges"]
     eng.close()
