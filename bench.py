@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--buckets", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=-1, help="CD visit-order chunk (engine option; -1 = default)")
+    ap.add_argument("--prune", type=int, default=-1, help="CD vertex pruning (engine option; -1 = default)")
     ap.add_argument("--ids", default="generator", choices=["generator", "planted"],
                     help="experiment: renumber node ids by planted community before loading")
     args = ap.parse_args()
@@ -135,6 +136,8 @@ def main():
         eng.set_params(buckets=args.buckets)
     if args.chunk >= 0:
         eng.set_option("chunk", args.chunk)
+    if args.prune >= 0:
+        eng.set_option("prune", args.prune)
     t0 = time.time()
     eng.load_graph(n, u, v)
     torch.cuda.synchronize()

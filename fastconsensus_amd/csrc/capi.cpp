@@ -126,7 +126,7 @@ void fc_destroy(fc_ctx* ctx) {
     (void)hipStreamSynchronize(c.stream);
     c.g.release();
     c.g0.release();
-    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
+    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
                       &c.heavy_scratch, &c.wnew, &c.flag, &c.pos, &c.ku, &c.kv, &c.kw, &c.kage, &c.krowptr,
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
@@ -174,6 +174,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
             FC_REQUIRE(value == 0 || value == 16, FC_EINVAL, "chunk must be 0 or 16 (one block of tiles)");
             c.chunk = (int)value;
             break;
+        case FC_OPT_PRUNE: c.prune = value != 0; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }
     FC_API_END

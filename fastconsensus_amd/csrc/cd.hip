@@ -69,7 +69,14 @@ struct CDArgs {
     // Sharded per-replica counters [n_r][NSH][RF]: one hot address per replica would
     // serialise every block's atomic (~12 ns each, MI355X_MICROARCH.md "fanin").
     unsigned long long* red;
-    int32_t* heavy;              // (r, p) pairs
+    // pruning (list mode): per sweep >= 1 only vertices whose neighbour moved are visited
+    uint8_t* aff;                // [n_r][N] affected flags (set by moves, read+cleared by list build)
+    int32_t* track;              // [n_r] moves mark neighbours affected this sweep; [n_r..2n_r) list filters
+    int prune;
+    const int32_t* list;         // [B][n_r][S] bucket positions to visit, or nullptr = every position
+    const int32_t* lcnt;         // [B][n_r] list lengths
+    const int32_t* blk_off;      // [B][n_r+1] light-kernel block offsets per replica
+    int32_t* heavy;              // (r, dec index, position) triples
     int32_t* heavy_cnt;
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
     int64_t heavy_slots;         // slots per global table (power of 2)
@@ -163,11 +170,28 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
     int r;
     int64_t chunk;
-    xcd_remap(blockIdx.x, (int64_t)gridDim.x, chunks, &r, &chunk);
-    const int64_t i = chunk * TILES + tile;                // position inside the bucket
+    int64_t di, i;             // decision slot (dec index) and position inside the bucket
+    bool in_range;
+    if (!a.list) {
+        xcd_remap(blockIdx.x, (int64_t)gridDim.x, chunks, &r, &chunk);
+        di = i = chunk * TILES + tile;
+        in_range = i < blen;
+    } else {
+        int rr;
+        int64_t w;
+        xcd_remap(blockIdx.x, (int64_t)gridDim.x, (int64_t)gridDim.x, &rr, &w);
+        const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
+        int lo = 0, hi = a.n_r;            // last replica with bo[r] <= w (uniform search)
+        while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (bo[mid] <= w) lo = mid; else hi = mid; }
+        r = lo;
+        di = (w - bo[r]) * TILES + tile;
+        const int64_t seg = ((int64_t)bucket * a.n_r + r);
+        in_range = di < a.lcnt[seg];
+        i = in_range ? a.list[seg * a.S + di] : 0;
+    }
     const int rg = a.rbase + r;
     const bool rep_on = r < a.n_r && a.active[r];
-    bool valid = rep_on && i < blen;
+    bool valid = rep_on && in_range;
     int32_t v = 0;
     int64_t rb = 0, d = 0;
     if (valid) {
@@ -248,11 +272,12 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     if (lane == 0) {
         int32_t dcs = -1;
         if (work) dcs = decide_final<LOUV, TT>(a, r, v, own, best_s, best_c, kown, have, &dq, &unst);
-        if (rep_on && i < blen) a.dec[(int64_t)r * a.S + i] = dcs;   // heavy rows: overwritten by k_decide_heavy
+        if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = dcs;   // heavy rows: overwritten by k_decide_heavy
         if (heavy) {
             const int q = atomicAdd(a.heavy_cnt, 1);
-            a.heavy[2 * q] = r;
-            a.heavy[2 * q + 1] = (int32_t)i;
+            a.heavy[3 * q] = r;
+            a.heavy[3 * q + 1] = (int32_t)di;
+            a.heavy[3 * q + 2] = (int32_t)i;
         }
         s_red[tile][0] = dq;
         s_red[tile][1] = (unsigned long long)unst;
@@ -281,8 +306,9 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     __shared__ long long r_kown[TB];
     const int cnt = *a.heavy_cnt;
     for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
-        const int r = a.heavy[2 * item];
-        const int64_t i = a.heavy[2 * item + 1];
+        const int r = a.heavy[3 * item];
+        const int64_t di = a.heavy[3 * item + 1];
+        const int64_t i = a.heavy[3 * item + 2];
         const int rg = a.rbase + r;
         const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
         const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
@@ -346,7 +372,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
             unsigned long long dq = 0;
             int unst = 0;
             const int32_t dcs = decide_final<LOUV, TT>(a, r, v, own, r_s[0], r_c[0], r_kown[0], r_have[0], &dq, &unst);
-            a.dec[(int64_t)r * a.S + i] = dcs;
+            a.dec[(int64_t)r * a.S + di] = dcs;
             if (dq) atomicAdd(red_slot(a, r, 0), dq);
             if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
         }
@@ -354,33 +380,51 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     }
 }
 
+// Apply a bucket's decisions: one 16-lane tile per decision slot; lane 0 updates the
+// label and the community totals, the tile scatters the new label into the reverse
+// adjacency entries (nlab) and, while tracking, flags the neighbours for the next sweep.
 template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, int64_t blen) {
     const int r = blockIdx.y;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
+    const int64_t di = (int64_t)blockIdx.x * TILES + tile;
     int moved = 0;
-    if (i < blen && a.active[r]) {
-        const int32_t d = a.dec[(int64_t)r * a.S + i];
+    const int64_t seg = (int64_t)bucket * a.n_r + r;
+    const bool in_range = a.list ? di < a.lcnt[seg] : di < blen;
+    if (in_range && a.active[r]) {
+        const int32_t d = a.dec[(int64_t)r * a.S + di];
         if (d >= 0) {
+            const int64_t i = a.list ? a.list[seg * a.S + di] : di;
             const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
             const int32_t v = pos_vertex(a, P, bucket * a.S + i);
-            int32_t* l = a.lab + (int64_t)r * a.N + v;
-            const int32_t old = *l;
-            *l = d;
-            int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-            for (int64_t j = a.rowptr[v]; j < a.rowptr[v + 1]; ++j) nlr[a.rev[j]] = d;
-            if (LOUV) {
-                TT* tot = (TT*)a.tot + (int64_t)r * a.N;
-                const TT kv = (TT)a.kdeg[v];
-                if constexpr (sizeof(TT) == 8) {
-                    atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
-                    atomicAdd((unsigned long long*)&tot[d], (unsigned long long)kv);
-                } else {
-                    atomicAdd((int*)&tot[old], -(int)kv);
-                    atomicAdd((int*)&tot[d], (int)kv);
+            if (lane == 0) {
+                int32_t* l = a.lab + (int64_t)r * a.N + v;
+                const int32_t old = *l;
+                *l = d;
+                if (LOUV) {
+                    TT* tot = (TT*)a.tot + (int64_t)r * a.N;
+                    const TT kv = (TT)a.kdeg[v];
+                    if constexpr (sizeof(TT) == 8) {
+                        atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
+                        atomicAdd((unsigned long long*)&tot[d], (unsigned long long)kv);
+                    } else {
+                        atomicAdd((int*)&tot[old], -(int)kv);
+                        atomicAdd((int*)&tot[d], (int)kv);
+                    }
                 }
+                moved = 1;
             }
-            moved = 1;
+            int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+            const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
+            if (a.track[r]) {
+                uint8_t* aff = a.aff + (int64_t)r * a.N;
+                for (int64_t j = rb + lane; j < re; j += TILE) {
+                    nlr[a.rev[j]] = d;     // neighbours now see v's new community
+                    aff[a.col[j]] = 1;     // ... and are revisited next sweep (pruning)
+                }
+            } else {
+                for (int64_t j = rb + lane; j < re; j += TILE) nlr[a.rev[j]] = d;
+            }
         }
     }
     const unsigned long long b = __ballot(moved);
@@ -397,7 +441,8 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, 
 template <bool LOUV>
 __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
     __shared__ int cnt;
-    if (threadIdx.x == 0) cnt = 0;
+    __shared__ unsigned long long mv;
+    if (threadIdx.x == 0) { cnt = 0; mv = 0; }
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -405,6 +450,11 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         for (int sh = 0; sh < NSH; ++sh)
             for (int k = 0; k < RF; ++k) { f[k] += base[sh * RF + k]; base[sh * RF + k] = 0; }
         a.sacc[4 * r + 0] += f[3]; a.sacc[4 * r + 1] += f[4]; a.sacc[4 * r + 2] += f[5];
+        atomicAdd(&mv, f[2]);
+        if (a.prune) {   // lists filter next sweep iff moves were tracked this sweep
+            a.track[a.n_r + r] = a.track[r];
+            if (f[2] * 4 < (unsigned long long)a.N) a.track[r] = 1;
+        }
         if (a.active[r]) {
             bool stop;
             if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < 1e-7;
@@ -414,7 +464,7 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) *n_active_out = cnt;
+    if (threadIdx.x == 0) { n_active_out[0] = cnt; *(unsigned long long*)(n_active_out + 2) = mv; }
 }
 
 __global__ void k_nlab_init(int64_t m2, const int32_t* col, int32_t* nlab) {
@@ -431,16 +481,60 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
     if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
 }
 
+// Pruned sweep: per (bucket, replica) the positions whose vertex is flagged affected, in
+// position order (deterministic); flags are read and cleared here, moves of this sweep
+// set them again for the next one.  One block per (bucket, replica) segment.
+__global__ __launch_bounds__(256) void k_build_lists(CDArgs a, int sweep, int64_t PN, int32_t* list, int32_t* lcnt) {
+    const int k = blockIdx.x / a.n_r, r = blockIdx.x % a.n_r;
+    const int64_t seg = blockIdx.x;
+    __shared__ int s_w[TB / 64];
+    if (!a.active[r]) {
+        if (threadIdx.x == 0) lcnt[seg] = 0;
+        return;
+    }
+    const int64_t blen = min((int64_t)a.S, PN - (int64_t)k * a.S);
+    const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
+    uint8_t* aff = a.aff + (int64_t)r * a.N;
+    const bool filter = a.track[a.n_r + r] != 0;   // moves were tracked during the previous sweep
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int base = 0;
+    for (int64_t i0 = 0; i0 < blen; i0 += TB) {
+        const int64_t i = i0 + threadIdx.x;
+        bool f = false;
+        if (i < blen) {
+            const int32_t v = pos_vertex(a, P, (int64_t)k * a.S + i);
+            if (v >= 0) { f = filter ? aff[v] != 0 : true; aff[v] = 0; }
+        }
+        const unsigned long long b = __ballot(f);
+        if (lane == 0) s_w[wave] = __popcll(b);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wave; ++w) off += s_w[w];
+        int tot = 0;
+        for (int w = 0; w < TB / 64; ++w) tot += s_w[w];
+        if (f) list[seg * a.S + off + __popcll(b & ((1ull << lane) - 1ull))] = (int32_t)i;
+        base += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) lcnt[seg] = base;
+}
+
 // One bucket: decide (light + heavy rows) against the state left by earlier buckets, apply.
+// Full mode: grid = all bucket positions of every replica.  List mode: light blocks =
+// light_blocks (sum over replicas of ceil(list length / 16)), apply covers max_len.
 template <bool LOUV, typename TT>
-static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, int64_t blen, bool any_heavy) {
+static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, int64_t blen, bool any_heavy,
+                      int64_t light_blocks, int64_t max_len) {
     const int64_t chunks = (blen + TILES - 1) / TILES;
+    const int64_t nb = a.list ? light_blocks : chunks * a.n_r;
+    const int64_t alen = a.list ? max_len : blen;
+    if (nb <= 0) return;
     FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     const int ev = timer_begin(c);
-    k_decide_light<LOUV, TT><<<(unsigned)(chunks * a.n_r), TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
+    k_decide_light<LOUV, TT><<<(unsigned)nb, TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
-    dim3 ag(nblk(blen), a.n_r);
+    dim3 ag((unsigned)((alen + TILES - 1) / TILES), a.n_r);
     k_apply<LOUV, TT><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
 }
 
@@ -472,9 +566,18 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int32_t* active = (int32_t*)rs;
     unsigned long long* red = (unsigned long long*)(rs + (((size_t)rcount * 4 + 255) & ~size_t(255)));
     unsigned long long* sacc = red + (size_t)rcount * NSH * RF;
-    int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);
-    const size_t zero_bytes = (char*)(n_active + 1) - (char*)red;
-    int32_t* heavy = ensure<int32_t>(c.heavy_list, 2 * (size_t)rcount * S + 2);
+    int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);   // [0] active, [2..3] u64 moves
+    const size_t zero_bytes = (char*)(n_active + 4) - (char*)red;
+    int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * S + 3);
+    uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
+    FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));   // sweep 0 visits everyone
+    int32_t* track = ensure<int32_t>(c.track, 2 * (size_t)rcount);
+    FC_HIP(hipMemsetAsync(track, 0, 8 * (size_t)rcount, c.stream));
+    int32_t* list = c.prune ? ensure<int32_t>(c.vlist, (size_t)B * rcount * S) : nullptr;
+    int32_t* lcnt = c.prune ? ensure<int32_t>(c.vcnt, (size_t)B * rcount + (size_t)B * (rcount + 1)) : nullptr;
+    int32_t* blk_off = c.prune ? lcnt + (size_t)B * rcount : nullptr;
+    std::vector<int32_t> h_cnt(c.prune ? (size_t)B * rcount : 0), h_off(c.prune ? (size_t)B * (rcount + 1) : 0);
+    std::vector<int64_t> light_blocks(B, 0), max_len(B, 0);
     int32_t* heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
     int64_t heavy_slots = 1;
     while (heavy_slots < 2 * (int64_t)g.max_deg) heavy_slots <<= 1;
@@ -502,25 +605,57 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
+    a.aff = aff; a.list = nullptr; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
 
     int n_act = (g.M2 > 0) ? rcount : 0;
     int sweep = 0;
     for (; sweep < c.max_sweeps && n_act > 0; ++sweep) {
         c.acc.cd_sweeps += n_act;
         c.prof.cd_sweeps += n_act;
+        a.list = nullptr;
+        if (c.prune && sweep > 0) {
+            // visit lists of this sweep: vertices whose neighbour moved in the previous sweep
+            k_build_lists<<<(unsigned)(B * rcount), TB, 0, c.stream>>>(a, sweep, PN, list, lcnt);
+            FC_HIP(hipMemcpyAsync(h_cnt.data(), lcnt, 4 * h_cnt.size(), hipMemcpyDeviceToHost, c.stream));
+            sync(c);
+            for (int k = 0; k < B; ++k) {
+                int64_t acc = 0, mx = 0;
+                for (int r = 0; r < rcount; ++r) {
+                    const int64_t n = h_cnt[(size_t)k * rcount + r];
+                    h_off[(size_t)k * (rcount + 1) + r] = (int32_t)acc;
+                    acc += (n + TILES - 1) / TILES;
+                    mx = std::max(mx, n);
+                }
+                h_off[(size_t)k * (rcount + 1) + rcount] = (int32_t)acc;
+                light_blocks[k] = acc;
+                max_len[k] = mx;
+            }
+            FC_HIP(hipMemcpyAsync(blk_off, h_off.data(), 4 * h_off.size(), hipMemcpyHostToDevice, c.stream));
+            a.list = list;
+        }
         for (int k = 0; k < B; ++k) {
             const int64_t blen = std::min<int64_t>(S, PN - (int64_t)k * S);
             if (blen <= 0) continue;
             const bool hv = g.max_deg > LIGHT_MAX_DEG;
-            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv);
-            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, blen, hv);
-            else sub_round<true, int64_t>(c, a, k, sweep, blen, hv);
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k]);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k]);
+            else sub_round<true, int64_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k]);
         }
+        if (a.list) sync(c);   // h_off (pageable) must outlive its async upload
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
-        FC_HIP(hipMemcpyAsync(c.hpin, n_active, sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(c.hpin, n_active, 16, hipMemcpyDeviceToHost, c.stream));
         sync(c);
         n_act = ((int32_t*)c.hpin)[0];
+        if (c.trace) {
+            std::vector<unsigned long long> sa(4 * (size_t)rcount);
+            FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
+            sync(c);
+            unsigned long long vv = 0;
+            for (int r = 0; r < rcount; ++r) vv += sa[4 * r];
+            fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu moves=%llu\n", iteration,
+                    sweep, n_act, vv, (unsigned long long)c.hpin[1]);
+        }
     }
     // light-kernel traffic counters for the roofline model
     std::vector<unsigned long long> sa(4 * (size_t)rcount);

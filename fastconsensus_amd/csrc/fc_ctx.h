@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string>
 #include <vector>
 
@@ -89,6 +90,7 @@ struct Ctx {
     int n_r = 0, rbase = 0, n_p_total = 0;
     DevBuf lab, tot, dec, labT;     // int32 [n_r][N], int64 [n_r][N], int32 [n_r][S], int32 [N][ldT]
     DevBuf nlab;                    // int32 [n_r][2m]: label of each adjacency entry's neighbour
+    DevBuf aff, vlist, vcnt, track; // pruning: affected flags, per-sweep visit lists, list lengths, modes
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable
@@ -113,6 +115,8 @@ struct Ctx {
     // params
     int buckets = 32, max_sweeps = 200, max_iters = 1000;
     int chunk = 0;                  // CD order granularity (0 = per vertex), FC_OPT_CHUNK
+    int prune = 0;                  // FC_OPT_PRUNE: after sweep 0 visit only vertices whose neighbour moved
+    bool trace = getenv("FC_TRACE") != nullptr;  // per-sweep progress on stderr
     Timer timer;
     fc_stats acc{};                 // accumulated during a run (fc_run)
     fc_stats prof{};                // accumulated since the last fc_collect_timing

@@ -34,13 +34,19 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     r0, r1 = shard(n_p, rank, world)
     louv = algo == LOUVAIN
     on_gpu = str(device).startswith("cuda")
-    if on_gpu:  # engine kernels and torch/RCCL ops on ONE stream: no cross-stream races
-        engine.set_stream(torch.cuda.current_stream().cuda_stream)
-    try:
+    if not on_gpu:
         return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv)
+    # engine kernels and torch/RCCL ops on ONE explicit stream: no cross-stream races
+    # (torch's default stream is the legacy null stream, which the engine cannot adopt)
+    stream = torch.cuda.Stream(device=device)
+    stream.wait_stream(torch.cuda.current_stream(device))
+    engine.set_stream(stream.cuda_stream)
+    try:
+        with torch.cuda.stream(stream):
+            return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv)
     finally:
-        if on_gpu:
-            engine.set_stream(None)
+        stream.synchronize()
+        engine.set_stream(None)
 
 
 def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv):

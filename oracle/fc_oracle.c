@@ -477,7 +477,8 @@ static inline int tw_better(long long s1, uint32_t h1, i32 c1, long long s2, uin
 
 /* One replica.  algo 0 = louvain local moving, 1 = lpa.  Returns sweeps executed. */
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
-                      u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, i32* lab) {
+                      u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
+                      i32* lab) {
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
@@ -490,21 +491,47 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     const int B = (int)(buckets < NC ? buckets : NC);
     const i64 S = chunk ? ((NC + B - 1) / B) * chunk : (N + B - 1) / B;
     i32* dec = (i32*)malloc(sizeof(i32) * (size_t)(S + 1));
+    u8* aff = (u8*)calloc((size_t)N, 1);
+    i64* lists = (i64*)malloc(sizeof(i64) * (size_t)(PN + 1));   /* per-bucket visit lists */
+    i64* loff = (i64*)malloc(sizeof(i64) * (size_t)(B + 1));
     for (i64 v = 0; v < N; ++v) { lab[v] = (i32)v; tot[v] = kdeg[v]; csz[v] = 1; }
     int active = M2 > 0, sweep = 0;
+    int track_now = 0, prune_now = 0;   /* adaptive pruning state (engine: k_sweep_end) */
     for (; sweep < max_sweeps && active; ++sweep) {
         const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, rg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
         unsigned long long dq = 0, moves = 0, unstable = 0;
+        const int listed = prune && sweep > 0;
+        if (listed) {   /* all lists are built (and flags cleared) at the sweep start;
+                           unfiltered (every position) until moves have been tracked */
+            i64 n = 0;
+            for (int k = 0; k < B; ++k) {
+                loff[k] = n;
+                i64 blen = PN - (i64)k * S;
+                if (blen > S) blen = S;
+                for (i64 i = 0; i < blen; ++i) {
+                    const i64 p = (i64)k * S + i;
+                    const i64 vv = chunk ? (i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk
+                                         : (i64)tw_perm_apply(&P, (uint32_t)p);
+                    if (vv < N) {
+                        if (!prune_now || aff[vv]) lists[n++] = i;
+                        aff[vv] = 0;
+                    }
+                }
+            }
+            loff[B] = n;
+        }
         for (int k = 0; k < B; ++k) {
             i64 blen = PN - (i64)k * S;
             if (blen > S) blen = S;
             if (blen <= 0) continue;
-            for (i64 i = 0; i < blen; ++i) {
+            const i64 ne = listed ? loff[k + 1] - loff[k] : blen;
+            for (i64 e = 0; e < ne; ++e) {
+                const i64 i = listed ? lists[loff[k] + e] : e;
+                dec[e] = -1;
                 const i64 p = (i64)k * S + i;
                 const i64 vv = chunk ? (i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk
                                      : (i64)tw_perm_apply(&P, (uint32_t)p);
-                dec[i] = -1;
                 if (vv >= N) continue;
                 const i32 v = (i32)vv;
                 const i64 rb = rowptr[v], re = rowptr[v + 1];
@@ -534,34 +561,42 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
                     if (G <= 0) continue;
                     const double d = (double)G * 2.0 / ((double)M2 * (double)M2);
                     dq += (unsigned long long)llrint(d * 1099511627776.0);
-                    dec[i] = best_c;
+                    dec[e] = best_c;
                 } else {
                     unstable += (kown != best_s);
-                    if (best_c != own) dec[i] = best_c;
+                    if (best_c != own) dec[e] = best_c;
                 }
             }
-            for (i64 i = 0; i < blen; ++i) {
-                if (dec[i] < 0) continue;
+            for (i64 e = 0; e < ne; ++e) {
+                if (dec[e] < 0) continue;
+                const i64 i = listed ? lists[loff[k] + e] : e;
                 const i64 p = (i64)k * S + i;
                 const i32 v = chunk ? (i32)((i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk)
                                     : (i32)tw_perm_apply(&P, (uint32_t)p);
-                const i32 old = lab[v], nw = dec[i];
+                const i32 old = lab[v], nw = dec[e];
                 lab[v] = nw;
                 if (louv) { tot[old] -= kdeg[v]; tot[nw] += kdeg[v]; csz[old]--; csz[nw]++; }
+                if (track_now)
+                    for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) aff[col[j]] = 1;
                 ++moves;
             }
+        }
+        if (prune) {
+            prune_now = track_now;
+            if (moves * 4 < (unsigned long long)N) track_now = 1;
         }
         if (louv) { if (moves == 0 || ((double)dq / 1099511627776.0) < 1e-7) active = 0; }
         else if (unstable == 0) active = 0;
     }
-    free(tot); free(csz); free(acc); free(seen); free(keys); free(dec);
+    free(tot); free(csz); free(acc); free(seen); free(keys); free(dec); free(aff); free(lists); free(loff);
     return sweep;
 }
 
 /* Replicas [rbase, rbase+n_r) of the engine's bucketed CD on a symmetric CSR.
  * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
 void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
-                   int iteration, u64 seed, int buckets, int max_sweeps, int chunk, i32* lab, int* sweeps) {
+                   int iteration, u64 seed, int buckets, int max_sweeps, int chunk, int prune, i32* lab,
+                   int* sweeps) {
     i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
     i64 M2 = 0;
     for (i64 v = 0; v < N; ++v) {
@@ -573,7 +608,7 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
-                            buckets, max_sweeps, chunk, lab + (i64)r * N);
+                            buckets, max_sweeps, chunk, prune, lab + (i64)r * N);
         if (sweeps) sweeps[r] = sw;
     }
     free(kdeg);

@@ -12,10 +12,11 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=0):
+    def __init__(self, seed, buckets=32, chunk=0, prune=0):
         self.seed = int(seed)
         self.buckets = buckets
         self.chunk = chunk
+        self.prune = prune
         self.lab = None
 
     # graph -----------------------------------------------------------------------------
@@ -41,7 +42,7 @@ class OracleEngine:
     # steps -----------------------------------------------------------------------------
     def cd(self, algo, r0, count, n_p, iteration):
         self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
-                                    chunk=self.chunk)
+                                    chunk=self.chunk, prune=self.prune)
         self.r0 = r0
 
     def consensus_partial(self, algo, out):

@@ -146,17 +146,19 @@ def _lfr1k_graph():
 
 
 @pytest.mark.parametrize("algo", [0, 1])
-@pytest.mark.parametrize("buckets,chunk", [(32, 0), (5, 0), (32, 16), (7, 16)])
-def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk):
+@pytest.mark.parametrize("buckets,chunk,prune", [(32, 0, 0), (5, 0, 0), (32, 16, 0), (7, 16, 0), (32, 0, 1),
+                                                 (5, 16, 1)])
+def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune):
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=99)
     eng.set_params(buckets=buckets)
     eng.set_option("chunk", chunk)
+    eng.set_option("prune", prune)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 4)
     got = eng.get_labels(n_r)
-    exp, sw = orc.engine_cd(algo, g, n_r, 0, 4, 99, buckets=buckets, chunk=chunk)
+    exp, sw = orc.engine_cd(algo, g, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune)
     np.testing.assert_array_equal(got, exp)
     # sharding invariance: replicas 2..4 alone give the same labelings
     eng.cd(algo, 2, 3, n_r, 4)
@@ -185,16 +187,17 @@ def _heavy_graph(seed, hub_deg):
 
 
 @pytest.mark.parametrize("algo", [0, 1])
-@pytest.mark.parametrize("hub_deg,chunk", [(300, 0), (3000, 0), (3000, 16)])
-def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk):
+@pytest.mark.parametrize("hub_deg,chunk,prune", [(300, 0, 0), (3000, 0, 0), (3000, 16, 0), (3000, 0, 1)])
+def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune):
     N, e = _heavy_graph(5, hub_deg)
     g = orc.EdgeGraph.from_lines(N, e)
     eng = fcmod.Engine(seed=7)
     eng.set_option("chunk", chunk)
+    eng.set_option("prune", prune)
     eng.load_graph(N, e[:, 0], e[:, 1])
     eng.cd(algo, 0, 4, 4, 1)
     got = eng.get_labels(4)
-    exp, _ = orc.engine_cd(algo, g, 4, 0, 1, 7, chunk=chunk)
+    exp, _ = orc.engine_cd(algo, g, 4, 0, 1, 7, chunk=chunk, prune=prune)
     np.testing.assert_array_equal(got, exp)
     eng.close()
 
@@ -304,8 +307,9 @@ def test_closure_sampler_properties(fcmod):
 
 
 # ------------------------------------------------------------------------- whole runs, bit-exact
-@pytest.mark.parametrize("algo,n_p,tau,chunk", [(0, 10, 0.2, 0), (0, 12, 0.2, 16), (1, 4, 0.8, 0), (0, 20, 0.2, 0)])
-def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk):
+@pytest.mark.parametrize("algo,n_p,tau,chunk,prune", [(0, 10, 0.2, 0, 0), (0, 12, 0.2, 16, 0), (1, 4, 0.8, 0, 0),
+                                                       (0, 20, 0.2, 0, 0), (0, 10, 0.2, 0, 1), (1, 6, 0.8, 16, 1)])
+def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
     loop (bucketed CD twin, consensus rule, Philox closure sampler, repair, ages): final
     partitions AND the final graph are identical (n_p=10 runs 9 iterations)."""
@@ -313,11 +317,12 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk):
     from tests.cpu_engine import OracleEngine
     case, _ = _lfr1k_graph()
     e = case.edges_file
-    cpu = OracleEngine(seed=17, chunk=chunk)
+    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune)
     cpu.load_graph(case.N, e[:, 0], e[:, 1])
     exp_labels, exp_st = run_sharded(cpu, algo, n_p, tau, 0.02, device="cpu", max_iters=50)
     eng = fcmod.Engine(seed=17)
     eng.set_option("chunk", chunk)
+    eng.set_option("prune", prune)
     eng.set_params(max_iters=50)
     eng.load_graph(case.N, e[:, 0], e[:, 1])
     labels, st = eng.run(algo, n_p, tau, 0.02)
