@@ -71,7 +71,8 @@ struct CDArgs {
     unsigned long long* red;
     // pruning (list mode): per sweep >= 1 only vertices whose neighbour moved are visited
     uint8_t* aff;                // [n_r][N] affected flags (set by moves, read+cleared by list build)
-    int32_t* track;              // [n_r] moves mark neighbours affected this sweep; [n_r..2n_r) list filters
+    int32_t* track;              // [n_r] moves mark neighbours affected this sweep; [n_r..2n_r) list filters;
+                                 // [2n_r..3n_r) push mode: nlab is current (else decide gathers lab[col])
     int prune;
     const int32_t* list;         // [B][n_r][S] bucket positions to visit, or nullptr = every position
     const int32_t* lcnt;         // [B][n_r] list lengths
@@ -208,14 +209,20 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
     const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
-    // ---- the row's neighbour labels are STREAMED from nlab (no gather), weights alongside
+    // ---- push mode: the row's neighbour labels are STREAMED from nlab; pull mode (early,
+    // move-heavy sweeps): gathered from lab[col[j]] -- the same values either way
+    const bool push = a.track[2 * a.n_r + r] != 0;
     int32_t cq[PER], wq[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int64_t j = rb + lane + TILE * q;
         const bool ok = work && j < rb + d;
-        cq[q] = ok ? nlr[j] : -1;
+        cq[q] = ok ? (push ? nlr[j] : a.col[j]) : -1;
         wq[q] = ok ? (LOUV ? a.cw[j] : 1) : 0;
+    }
+    if (!push) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) cq[q] = cq[q] >= 0 ? labr[cq[q]] : -1;
     }
     const int32_t own = work ? labr[v] : 0;
     const int64_t kv = (LOUV && work) ? a.kdeg[v] : 0;
@@ -328,8 +335,9 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         __syncthreads();
         const int32_t* labr = a.lab + (int64_t)r * a.N;
         const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+        const bool push = a.track[2 * a.n_r + r] != 0;
         for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB)
-            tbl_insert(keys, vals, slots - 1, nlr[j], LOUV ? a.cw[j] : 1);
+            tbl_insert(keys, vals, slots - 1, push ? nlr[j] : labr[a.col[j]], LOUV ? a.cw[j] : 1);
         __syncthreads();
         const int32_t own = labr[v];
         const int64_t kv = a.kdeg[v];
@@ -416,14 +424,18 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, 
             }
             int32_t* nlr = a.nlab + (int64_t)r * a.m2;
             const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
-            if (a.track[r]) {
+            const bool push = a.track[2 * a.n_r + r] != 0, trk = a.track[r] != 0;
+            if (push && trk) {
                 uint8_t* aff = a.aff + (int64_t)r * a.N;
                 for (int64_t j = rb + lane; j < re; j += TILE) {
                     nlr[a.rev[j]] = d;     // neighbours now see v's new community
                     aff[a.col[j]] = 1;     // ... and are revisited next sweep (pruning)
                 }
-            } else {
+            } else if (push) {
                 for (int64_t j = rb + lane; j < re; j += TILE) nlr[a.rev[j]] = d;
+            } else if (trk) {
+                uint8_t* aff = a.aff + (int64_t)r * a.N;
+                for (int64_t j = rb + lane; j < re; j += TILE) aff[a.col[j]] = 1;
             }
         }
     }
@@ -455,6 +467,9 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
             a.track[a.n_r + r] = a.track[r];
             if (f[2] * 4 < (unsigned long long)a.N) a.track[r] = 1;
         }
+        // pull -> push once a sweep moved < N/4 vertices (push pays d writes per MOVE,
+        // pull d gathers per VISIT); the host refreshes nlab for switching replicas
+        if (!a.track[2 * a.n_r + r] && f[2] * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
         if (a.active[r]) {
             bool stop;
             if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < 1e-7;
@@ -467,9 +482,18 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
     if (threadIdx.x == 0) { n_active_out[0] = cnt; *(unsigned long long*)(n_active_out + 2) = mv; }
 }
 
-__global__ void k_nlab_init(int64_t m2, const int32_t* col, int32_t* nlab) {
+// Entering push mode: nlab[r][j] = lab[r][col[j]] for the replicas flagged in
+// track[3n_r + r] (cleared here, push flag set).
+__global__ void k_nlab_refresh(int64_t m2, int64_t N, int n_r, const int32_t* col, const int32_t* lab,
+                               int32_t* nlab, int32_t* track) {
+    const int r = blockIdx.y;
+    if (!track[3 * n_r + r]) return;
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < m2) nlab[(int64_t)blockIdx.y * m2 + j] = col[j];
+    if (j < m2) nlab[(int64_t)r * m2 + j] = lab[(int64_t)r * N + col[j]];
+}
+__global__ void k_push_on(int n_r, int32_t* track) {
+    for (int r = threadIdx.x; r < n_r; r += blockDim.x)
+        if (track[3 * n_r + r]) { track[3 * n_r + r] = 0; track[2 * n_r + r] = 1; }
 }
 
 template <typename TT>
@@ -571,8 +595,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * S + 3);
     uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
     FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));   // sweep 0 visits everyone
-    int32_t* track = ensure<int32_t>(c.track, 2 * (size_t)rcount);
-    FC_HIP(hipMemsetAsync(track, 0, 8 * (size_t)rcount, c.stream));
+    int32_t* track = ensure<int32_t>(c.track, 4 * (size_t)rcount);
+    FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
     int32_t* list = c.prune ? ensure<int32_t>(c.vlist, (size_t)B * rcount * S) : nullptr;
     int32_t* lcnt = c.prune ? ensure<int32_t>(c.vcnt, (size_t)B * rcount + (size_t)B * (rcount + 1)) : nullptr;
     int32_t* blk_off = c.prune ? lcnt + (size_t)B * rcount : nullptr;
@@ -593,7 +617,6 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     dim3 ig(nblk(N), rcount);
     if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, (int32_t*)tot, louv ? 1 : 0);
     else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, (int64_t*)tot, louv ? 1 : 0);
-    if (m2 > 0) k_nlab_init<<<dim3(nblk(m2), rcount), TB, 0, c.stream>>>(m2, g.col.as<int32_t>(), nlab);
     FC_REQUIRE(!louv || (double)g.max_kdeg * (double)g.M2 < 4.0e18, FC_ELIMIT,
                "edge weights too large for exact int64 modularity gains");
 
@@ -609,10 +632,17 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
 
     int n_act = (g.M2 > 0) ? rcount : 0;
     int sweep = 0;
+    bool any_switch = false;
+    std::vector<int32_t> h_sw(rcount);
     for (; sweep < c.max_sweeps && n_act > 0; ++sweep) {
         c.acc.cd_sweeps += n_act;
         c.prof.cd_sweeps += n_act;
         a.list = nullptr;
+        if (any_switch && m2 > 0) {   // replicas entering push mode: build their nlab copies
+            k_nlab_refresh<<<dim3(nblk(m2), rcount), TB, 0, c.stream>>>(m2, N, rcount, g.col.as<int32_t>(), lab, nlab,
+                                                                       track);
+            k_push_on<<<1, TB, 0, c.stream>>>(rcount, track);
+        }
         if (c.prune && sweep > 0) {
             // visit lists of this sweep: vertices whose neighbour moved in the previous sweep
             k_build_lists<<<(unsigned)(B * rcount), TB, 0, c.stream>>>(a, sweep, PN, list, lcnt);
@@ -645,8 +675,12 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
         FC_HIP(hipMemcpyAsync(c.hpin, n_active, 16, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(h_sw.data(), track + 3 * (size_t)rcount, 4 * (size_t)rcount, hipMemcpyDeviceToHost,
+                              c.stream));
         sync(c);
         n_act = ((int32_t*)c.hpin)[0];
+        any_switch = false;
+        for (int r = 0; r < rcount; ++r) any_switch |= h_sw[r] != 0;
         if (c.trace) {
             std::vector<unsigned long long> sa(4 * (size_t)rcount);
             FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));

@@ -115,7 +115,7 @@ struct Ctx {
     // params
     int buckets = 32, max_sweeps = 200, max_iters = 1000;
     int chunk = 0;                  // CD order granularity (0 = per vertex), FC_OPT_CHUNK
-    int prune = 0;                  // FC_OPT_PRUNE: after sweep 0 visit only vertices whose neighbour moved
+    int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     bool trace = getenv("FC_TRACE") != nullptr;  // per-sweep progress on stderr
     Timer timer;
     fc_stats acc{};                 // accumulated during a run (fc_run)

@@ -80,7 +80,7 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_MAX_SWEEPS 2  /* cap on sweeps per CD run (default 200)                      */
 #define FC_OPT_MAX_ITERS 3   /* cap on consensus iterations (default 1000)                  */
 #define FC_OPT_CHUNK 4       /* CD visit order granularity: 0 per vertex, else chunk size   */
-#define FC_OPT_PRUNE 5       /* 1: after sweep 0, a sweep visits only vertices with a moved
+#define FC_OPT_PRUNE 5       /* 1 (default): once a sweep moves < n/4 vertices, later sweeps visit only vertices with a moved
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 

@@ -199,7 +199,7 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     return lab, sw
 
 
-def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=0, prune=0):
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=0, prune=1):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels)."""
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)

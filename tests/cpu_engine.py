@@ -12,7 +12,7 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=0, prune=0):
+    def __init__(self, seed, buckets=32, chunk=0, prune=1):
         self.seed = int(seed)
         self.buckets = buckets
         self.chunk = chunk

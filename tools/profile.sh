@@ -7,7 +7,7 @@ OUT=gpurun_out/prof_$CFG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp && cd - > /dev/null
-BENCH="python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline"
+BENCH="python3 bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
 run() {  # run <name> <timeout> <rocprof args...>
     local name=$1 t=$2; shift 2
     echo "== $name"
