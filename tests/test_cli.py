@@ -1,0 +1,111 @@
+"""CLI drop-in contract (fast_consensus.py:414-466) against the reference's own CLI run
+(tests/golden/cli_*.json, produced by running the reference script): validation messages
+and exit status, output directory names, and the output files byte for byte (louvain) /
+as sets of communities (lpm, whose line order is Python set order)."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests import golden_io
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = golden_io.GOLDEN
+
+
+def _golden(name):
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        meta = json.load(f)
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return meta, z["final_labels"], z["nodes"]
+
+
+def _args(argv):
+    from fastconsensus_amd.cli import DEFAULT_TAU, build_parser
+    a = build_parser().parse_args(["-f", "graph.txt"] + argv)
+    if a.t is None:
+        a.t = DEFAULT_TAU.get(a.alg, 0.2)
+    return a
+
+
+def test_argument_errors_match_reference():
+    with open(os.path.join(GOLDEN, "cli_arg_errors.json")) as f:
+        cases = json.load(f)
+    for c in cases:
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "fast_consensus.py"),
+                            "-f", os.path.join(GOLDEN, "karate_club.txt")] + c["argv"],
+                           capture_output=True, text=True, cwd=ROOT)
+        assert p.stdout == c["stdout"], c["argv"]
+        assert p.returncode == c["returncode"] == 0
+
+
+def test_louvain_output_tree_byte_exact(tmp_path):
+    from fastconsensus_amd.cli import output_dirs, write_outputs
+    from fastconsensus_amd.core import labels_to_output
+    meta, labels, nodes = _golden("cli_karate_louvain")
+    args = _args(meta["argv"])
+    assert sorted(output_dirs(args)) == meta["dirs"]
+    write_outputs(args, labels_to_output("louvain", nodes, labels), root=str(tmp_path))
+    got = {}
+    for d in meta["dirs"]:
+        for fn in os.listdir(tmp_path / d):
+            got[d + "/" + fn] = (tmp_path / d / fn).read_text()
+    assert got == meta["files"]
+
+
+def test_lpm_output_tree_same_communities(tmp_path):
+    from fastconsensus_amd.cli import output_dirs, write_outputs
+    from fastconsensus_amd.core import labels_to_output
+    meta, labels, nodes = _golden("cli_karate_lpm")
+    args = _args(meta["argv"])
+    assert sorted(output_dirs(args)) == meta["dirs"]
+    write_outputs(args, labels_to_output("lpm", nodes, labels), root=str(tmp_path))
+    mem_dir = [d for d in meta["dirs"] if d.startswith("memberships")][0]
+    assert os.listdir(tmp_path / mem_dir) == []          # created but empty for lpm
+    for key, text in meta["files"].items():
+        ours = (tmp_path / key).read_text()
+        as_sets = lambda t: sorted(sorted(map(int, ln.split())) for ln in t.strip().split("\n"))
+        assert as_sets(ours) == as_sets(text), key
+
+
+def test_native_parser_matches_networkx(tmp_path):
+    import networkx as nx
+    from fastconsensus_amd.core import IdGraph
+    p = tmp_path / "g.txt"
+    p.write_text("# comment\n5 7\n7 9 0.5\n\n9 5\n5 7\n3 3\n11\n")  # dup, self loop, 1-col line
+    g = IdGraph.from_edgelist_file(str(p))
+    G = nx.read_edgelist(str(p), nodetype=int, data=False)
+    assert list(g.labels) == list(G.nodes())
+    edges = {tuple(sorted((int(g.labels[a]), int(g.labels[b])))) for a, b in zip(g.u, g.v)}
+    assert edges == {tuple(sorted(e)) for e in G.edges()}
+    g2 = IdGraph.from_edgelist_file(os.path.join(GOLDEN, "karate_club.txt"))
+    K = nx.read_edgelist(os.path.join(GOLDEN, "karate_club.txt"), nodetype=int)
+    assert list(g2.labels) == list(K.nodes()) and len(g2.u) == K.number_of_edges()
+
+
+def test_networkx_input_order_is_adjacency_order():
+    """IdGraph.from_networkx emits each node's later neighbours in G.adj order, which is
+    what the repair tie-break needs (fast_consensus.py:131, :194)."""
+    import networkx as nx
+    from fastconsensus_amd.core import IdGraph
+    G = nx.Graph()
+    G.add_edges_from([(3, 1), (1, 2), (3, 0), (2, 0), (1, 0)])
+    g = IdGraph.from_networkx(G)
+    assert list(g.labels) == [3, 1, 2, 0]
+    # node 1 (id 1): later neighbours in adjacency order: 2 (id 2), then 0 (id 3)
+    pairs = list(zip(g.u.tolist(), g.v.tolist()))
+    assert pairs.index((1, 2)) < pairs.index((1, 3))
+
+
+def test_unknown_and_out_of_scope_algorithms():
+    import networkx as nx
+    import fastconsensus_amd as fc
+    G = nx.karate_club_graph()
+    assert fc.fast_consensus(G, algorithm="no-such-alg") is None   # reference: returns None
+    for alg in ("infomap", "leiden", "cnm"):
+        with pytest.raises(NotImplementedError):
+            fc.fast_consensus(G, algorithm=alg)
