@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--buckets", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=-1, help="CD visit-order chunk (engine option; -1 = default)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) in production; gloo to rehearse N>1 on one GPU")
     ap.add_argument("--prune", type=int, default=-1, help="CD vertex pruning (engine option; -1 = default)")
     ap.add_argument("--ids", default="generator", choices=["generator", "planted"],
                     help="experiment: renumber node ids by planted community before loading")
@@ -118,9 +119,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     dev = "cuda:%d" % local
 
     t0 = time.time()

@@ -116,7 +116,7 @@ struct Ctx {
     int buckets = 32, max_sweeps = 200, max_iters = 1000;
     int chunk = 0;                  // CD order granularity (0 = per vertex), FC_OPT_CHUNK
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
-    bool trace = getenv("FC_TRACE") != nullptr;  // per-sweep progress on stderr
+    bool trace = getenv("FC_TRACE") && *getenv("FC_TRACE") && *getenv("FC_TRACE") != '0';  // per-sweep stderr
     Timer timer;
     fc_stats acc{};                 // accumulated during a run (fc_run)
     fc_stats prof{};                // accumulated since the last fc_collect_timing
