@@ -336,3 +336,54 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune):
     np.testing.assert_array_equal(labels2, labels)
     assert st2["partition_edges"] == st["partition_edges"]
     eng.close()
+
+
+# ------------------------------------------------------------------------- full BASELINE sizes
+@pytest.fixture(scope="module")
+def lfr1m():
+    from fastconsensus_amd import synth
+    u, v, planted = synth.lfr(1_000_000, 0.5, seed=42)
+    return 1_000_000, u, v, planted
+
+
+def test_c4_consensus_update_bit_exact_full_size(fcmod, lfr1m):
+    """BASELINE configs[3] size (n=1M, m~13.8M, n_p=64): one consensus update on device
+    labelings (64 Louvain replicas) is bit-exact against the oracle's literal rule."""
+    n, u, v, _ = lfr1m
+    eng = fcmod.Engine(seed=3)
+    eng.load_graph(n, u, v)
+    eng.cd(0, 0, 64, 64, 0)
+    lab = eng.get_labels(64)
+    part = dev_i32(eng.m)
+    eng.consensus_partial(0, part)
+    conv, kept, unc = eng.consensus_apply(0, 64, 0.2, 0.02, part)
+    g = orc.EdgeGraph.from_lines(n, np.stack([u, v], 1))
+    w_ref = orc.consensus(0, g, lab, 64)
+    keep = orc.threshold(w_ref, 0.2, 64)
+    ku, kv, kw, _ = eng.get_nextgraph()
+    assert kept == int(keep.sum())
+    np.testing.assert_array_equal(kw, w_ref[keep])
+    np.testing.assert_array_equal(ku, g.u[keep])
+    assert (conv, unc) == orc.check(w_ref[keep], 64, 0.02)
+    eng.close()
+
+
+def test_c4_run_properties_full_size(fcmod, lfr1m):
+    """Whole louvain consensus at the metric's size: deterministic for a seed, partitions are
+    well-formed, every node is covered, and NMI to the planted communities is high."""
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    n, u, v, planted = lfr1m
+    outs = []
+    for _ in range(2):
+        eng = fcmod.Engine(seed=11)
+        eng.load_graph(n, u, v)
+        labels, st = eng.run(0, 64, 0.2, 0.02)
+        outs.append((labels, st, eng.get_graph()[2].sum()))
+        eng.close()
+    (l1, s1, w1), (l2, s2, w2) = outs
+    np.testing.assert_array_equal(l1, l2)
+    assert s1["partition_edges"] == s2["partition_edges"] and w1 == w2
+    assert s1["exit_check"] in (1, 2) and not s1["hit_iter_cap"]
+    for row in l1[:4]:
+        assert row.min() == 0 and row[0] == 0 and row.max() + 1 == len(np.unique(row))
+    assert nmi(planted, l1[0]) > 0.8
