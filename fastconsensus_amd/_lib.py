@@ -13,13 +13,13 @@ LIB_PATH = os.path.join(PKG, "lib", "libfastconsensus_amd.so")
 
 FC_ALGO_LOUVAIN = 0
 FC_ALGO_LPM = 1
-OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5}
+OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6}
 ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 
 # Every symbol declared in include/fastconsensus_amd.h (checked by tests/test_capi_symbols.py)
 SYMBOLS = [
     "fc_last_error", "fc_version", "fc_create", "fc_destroy", "fc_set_stream", "fc_set_timing",
-    "fc_collect_timing", "fc_set_params", "fc_set_option", "fc_load_graph", "fc_graph_info", "fc_reset_graph", "fc_get_graph", "fc_get_nextgraph", "fc_run",
+    "fc_collect_timing", "fc_set_params", "fc_set_option", "fc_load_graph", "fc_graph_info", "fc_get_node_map", "fc_reset_graph", "fc_get_graph", "fc_get_nextgraph", "fc_run",
     "fc_cd", "fc_set_labels", "fc_get_labels", "fc_consensus_partial", "fc_consensus_apply",
     "fc_closure_sample", "fc_closure_set_pairs", "fc_closure_partial", "fc_closure_apply",
     "fc_generate_lfr", "fc_generate_sbm", "fc_read_edgelist",
@@ -75,6 +75,7 @@ def load():
     L.fc_set_option.argtypes = [vp, c_int, i64]
     L.fc_load_graph.argtypes = [vp, i64, i64, _i32p, _i32p]
     L.fc_reset_graph.argtypes = [vp]
+    L.fc_get_node_map.argtypes = [vp, _i32p]
     L.fc_graph_info.argtypes = [vp, P(i64), P(i64), P(i64)]
     L.fc_get_graph.argtypes = [vp, vp, vp, vp, vp]
     L.fc_get_nextgraph.argtypes = [vp, P(i64), vp, vp, vp, vp]

@@ -79,6 +79,12 @@ class Engine:
         assert u.shape == v.shape
         check(self._L.fc_load_graph(self._ctx, int(n), len(u), u, v))
 
+    def node_map(self):
+        """sigma[node id] = the engine's internal vertex id."""
+        out = np.empty(self.n, np.int32)
+        check(self._L.fc_get_node_map(self._ctx, out))
+        return out
+
     def reset_graph(self):
         check(self._L.fc_reset_graph(self._ctx))
 

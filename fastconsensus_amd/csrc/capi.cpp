@@ -131,7 +131,8 @@ void fc_destroy(fc_ctx* ctx) {
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
                       &c.hit, &c.mkey, &c.mkey2, &c.midx, &c.midx2, &c.sort_tmp, &c.nodetmp, &c.nodetmp2,
-                      &c.nodetmp3, &c.part, &c.ccount};
+                      &c.nodetmp3, &c.part, &c.ccount, &c.sigma, &c.npos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
+                      &c.st_lab};
     for (auto* b : bufs) b->release();
     for (auto e : c.timer.pool) (void)hipEventDestroy(e);
     if (c.hpin) (void)hipHostFree(c.hpin);
@@ -175,6 +176,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
             c.chunk = (int)value;
             break;
         case FC_OPT_PRUNE: c.prune = value != 0; break;
+        case FC_OPT_RELABEL: c.relabel = value != 0; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }
     FC_API_END
@@ -186,6 +188,14 @@ int fc_load_graph(fc_ctx* ctx, int64_t n, int64_t m, const int32_t* u, const int
     FC_REQUIRE(m == 0 || (u && v), FC_EINVAL, "null edge arrays");
     graph_load(c, n, m, u, v);
     c.n_r = 0;
+    FC_API_END
+}
+
+int fc_get_node_map(fc_ctx* ctx, int32_t* sigma) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.N > 0 && sigma, FC_ESTATE, "no graph loaded");
+    std::memcpy(sigma, c.h_sigma.data(), 4 * (size_t)c.N);
     FC_API_END
 }
 
@@ -209,14 +219,8 @@ int fc_graph_info(fc_ctx* ctx, int64_t* n, int64_t* m, int64_t* m0) {
 int fc_get_graph(fc_ctx* ctx, int32_t* u, int32_t* v, int32_t* w, int64_t* age) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    const int64_t m = c.g.m;
-    if (m > 0) {
-        if (u) FC_HIP(hipMemcpyAsync(u, c.g.eu.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
-        if (v) FC_HIP(hipMemcpyAsync(v, c.g.ev.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
-        if (w) FC_HIP(hipMemcpyAsync(w, c.g.ew.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
-        if (age) FC_HIP(hipMemcpyAsync(age, c.g.eage.p, 8 * m, hipMemcpyDeviceToHost, c.stream));
-    }
-    sync(c);
+    graph_to_host(c, c.g.m, c.g.eu.as<int32_t>(), c.g.ev.as<int32_t>(), c.g.ew.as<int32_t>(),
+                  c.g.eage.as<int64_t>(), u, v, w, age);
     FC_API_END
 }
 
@@ -225,13 +229,9 @@ int fc_get_nextgraph(fc_ctx* ctx, int64_t* m_out, int32_t* u, int32_t* v, int32_
     FC_API_BEGIN
     const int64_t m = c.kept_m;
     if (m_out) *m_out = m;
-    if (m > 0) {
-        if (u) FC_HIP(hipMemcpyAsync(u, c.ku.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
-        if (v) FC_HIP(hipMemcpyAsync(v, c.kv.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
-        if (w) FC_HIP(hipMemcpyAsync(w, c.kw.p, 4 * m, hipMemcpyDeviceToHost, c.stream));
-        if (age) FC_HIP(hipMemcpyAsync(age, c.kage.p, 8 * m, hipMemcpyDeviceToHost, c.stream));
-    }
-    sync(c);
+    if (u || v || w || age)
+        graph_to_host(c, m, c.ku.as<int32_t>(), c.kv.as<int32_t>(), c.kw.as<int32_t>(), c.kage.as<int64_t>(), u, v,
+                      w, age);
     FC_API_END
 }
 
@@ -248,10 +248,7 @@ int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels) {
     FC_API_BEGIN
     FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
     FC_REQUIRE(count >= 1 && labels, FC_EINVAL, "bad labelings");
-    const size_t n = (size_t)count * c.N;
-    int32_t* lab = ensure<int32_t>(c.lab, n);
-    FC_HIP(hipMemcpyAsync(lab, labels, 4 * n, hipMemcpyHostToDevice, c.stream));
-    sync(c);
+    labels_from_host(c, count, labels);
     c.n_r = count; c.rbase = 0; c.n_p_total = count;
     c.labT_valid = false;
     FC_API_END
@@ -261,9 +258,7 @@ int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber) {
     FC_CTX(ctx)
     FC_API_BEGIN
     FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings");
-    if (renumber) labels_renumber(c);
-    FC_HIP(hipMemcpyAsync(labels, c.lab.p, 4 * (size_t)c.n_r * c.N, hipMemcpyDeviceToHost, c.stream));
-    sync(c);
+    labels_to_host(c, labels, renumber != 0);
     FC_API_END
 }
 
@@ -302,9 +297,13 @@ int fc_closure_set_pairs(fc_ctx* ctx, int64_t npairs, const int32_t* pairs, int 
     FC_CTX(ctx)
     FC_API_BEGIN
     FC_REQUIRE(npairs == 0 || pairs, FC_EINVAL, "null pairs");
-    for (int64_t i = 0; i < 2 * npairs; ++i)
+    std::vector<int32_t> mapped(2 * (size_t)npairs);
+    for (int64_t i = 0; i < 2 * npairs; ++i) {
         FC_REQUIRE(pairs[i] >= 0 && pairs[i] < c.N, FC_EINVAL, "pair endpoint out of range");
-    closure_from_pairs(c, npairs, pairs, iteration);
+        mapped[i] = c.h_sigma[pairs[i]];
+    }
+    closure_from_pairs(c, npairs, mapped.data(), iteration);
+    sync(c);
     if (n_cand) *n_cand = c.n_cand;
     FC_API_END
 }
@@ -381,8 +380,7 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
     a.partition_edges += (int64_t)n_p * c.g.m;
     a.m_final = c.g.m;
     if (labels_out) {
-        labels_renumber(c);
-        FC_HIP(hipMemcpyAsync(labels_out, c.lab.p, 4 * (size_t)n_p * c.N, hipMemcpyDeviceToHost, c.stream));
+        labels_to_host(c, labels_out, true);
     }
     sync(c);
     if (st) *st = a;  // *_ms / decide_launches stay 0: fc_collect_timing() fills them

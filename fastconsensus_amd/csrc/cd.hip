@@ -744,39 +744,64 @@ __global__ void k_first_init(int64_t total, int32_t* first) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < total) first[i] = 0x7fffffff;
 }
-__global__ void k_first_min(int64_t N, const int32_t* lab, int32_t* first) {
+// first[r][c] = earliest NODE position of community c
+__global__ void k_first_min(int64_t N, const int32_t* lab, const int32_t* npos, int32_t* first) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
-    if (v < N) atomicMin(&first[(int64_t)r * N + lab[(int64_t)r * N + v]], (int32_t)v);
+    if (v < N) atomicMin(&first[(int64_t)r * N + lab[(int64_t)r * N + v]], npos[v]);
 }
-__global__ void k_first_flag(int64_t N, int64_t total, const int32_t* lab, const int32_t* first, int32_t* flag) {
+// over node order t: out[r][t] = raw label of node t; flag = t opens its community
+__global__ void k_node_order(int64_t N, int64_t total, const int32_t* lab, const int32_t* sigma,
+                             const int32_t* first, int32_t* out, int32_t* flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > total) return;
-    if (i == total) { flag[i] = 0; return; }
-    const int64_t r = i / N, v = i % N;
-    flag[i] = first[r * N + lab[i]] == (int32_t)v ? 1 : 0;
+    if (i == total) { if (flag) flag[i] = 0; return; }
+    const int64_t r = i / N, t = i % N;
+    const int32_t c = lab[r * N + sigma[t]];
+    out[i] = c;
+    if (flag) flag[i] = first[r * N + c] == (int32_t)t ? 1 : 0;
 }
-__global__ void k_relabel(int64_t N, int32_t* lab, const int32_t* first, const int32_t* rank) {
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int r = blockIdx.y;
-    if (v >= N) return;
-    const int64_t base = (int64_t)r * N;
-    lab[base + v] = rank[base + first[base + lab[base + v]]] - rank[base];
+__global__ void k_relabel_out(int64_t N, int64_t total, int32_t* out, const int32_t* first, const int32_t* rank) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t base = (i / N) * N;
+    out[i] = rank[base + first[base + out[i]]] - rank[base];
 }
-// Community ids -> 0..k-1 in order of each community's first node (node order).
-void labels_renumber(Ctx& c) {
+// Local labelings -> host in NODE order; renumber: community ids 0..k-1 by first node.
+void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
     const int64_t N = c.N, total = (int64_t)c.n_r * N;
-    FC_REQUIRE(total < (int64_t(1) << 31), FC_ELIMIT, "n_p * n too large for renumbering");
-    int32_t* first = ensure<int32_t>(c.dec, total + 1);     // CD scratch is free now
-    int32_t* flag = ensure<int32_t>(c.wnew, total + 1);
-    int32_t* rank = ensure<int32_t>(c.hit, total + 1);
-    k_first_init<<<nblk(total), TB, 0, c.stream>>>(total, first);
-    dim3 g(nblk(N), c.n_r);
-    k_first_min<<<g, TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), first);
-    k_first_flag<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), first, flag);
-    exclusive_scan(c, flag, rank, total + 1);
-    k_relabel<<<g, TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), first, rank);
-    c.labT_valid = false;
+    FC_REQUIRE(total < (int64_t(1) << 31), FC_ELIMIT, "n_p * n too large for one labelling export");
+    int32_t* out = ensure<int32_t>(c.st_lab, total + 1);
+    int32_t* first = renumber ? ensure<int32_t>(c.dec, total + 1) : nullptr;   // CD scratch is free now
+    int32_t* flag = renumber ? ensure<int32_t>(c.wnew, total + 1) : nullptr;
+    int32_t* rank = renumber ? ensure<int32_t>(c.hit, total + 1) : nullptr;
+    if (renumber) {
+        k_first_init<<<nblk(total), TB, 0, c.stream>>>(total, first);
+        k_first_min<<<dim3(nblk(N), c.n_r), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), c.npos.as<int32_t>(), first);
+    }
+    k_node_order<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), c.sigma.as<int32_t>(), first,
+                                                       out, flag);
+    if (renumber) {
+        exclusive_scan(c, flag, rank, total + 1);
+        k_relabel_out<<<nblk(total), TB, 0, c.stream>>>(N, total, out, first, rank);
+    }
+    FC_HIP(hipMemcpyAsync(host, out, 4 * (size_t)total, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+}
+__global__ void k_from_node_order(int64_t N, int64_t total, const int32_t* in, const int32_t* sigma, int32_t* lab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t r = i / N, t = i % N;
+    lab[r * N + sigma[t]] = in[i];   // label values only matter through equality
+}
+// Host labelings in node order -> local replicas (replay).
+void labels_from_host(Ctx& c, int count, const int32_t* host) {
+    const int64_t N = c.N, total = (int64_t)count * N;
+    int32_t* in = ensure<int32_t>(c.st_lab, total + 1);
+    FC_HIP(hipMemcpyAsync(in, host, 4 * (size_t)total, hipMemcpyHostToDevice, c.stream));
+    int32_t* lab = ensure<int32_t>(c.lab, (size_t)total);
+    k_from_node_order<<<nblk(total), TB, 0, c.stream>>>(N, total, in, c.sigma.as<int32_t>(), lab);
+    sync(c);
 }
 
 }  // namespace fc

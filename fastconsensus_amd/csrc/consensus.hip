@@ -339,29 +339,36 @@ __global__ void k_deg_add(int64_t k, const int32_t* cu, const int32_t* cv, int64
     atomicAdd((unsigned long long*)&deg[cu[i]], 1ull);
     atomicAdd((unsigned long long*)&deg[cv[i]], 1ull);
 }
-__global__ void k_iso_flags(int64_t n, const int64_t* deg, const int64_t* rowptr, int64_t* flag) {
-    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x > n) return;
+// Indexed by NODE ORDER t (x = sigma[t]): nx.isolates visits nodes in node order.
+__global__ void k_iso_flags(int64_t n, const int32_t* sigma, const int64_t* deg, const int64_t* rowptr,
+                            int64_t* flag) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > n) return;
+    if (t == n) { flag[t] = 0; return; }
+    const int32_t x = sigma[t];
     // isolated in nextgraph and has a neighbour in graph (else the reference raises)
-    flag[x] = (x < n && deg[x] == 0 && rowptr[x + 1] > rowptr[x]) ? 1 : 0;
+    flag[t] = (deg[x] == 0 && rowptr[x + 1] > rowptr[x]) ? 1 : 0;
 }
 // Target of isolated node x: its neighbour in the OLD graph with the minimum old weight;
 // ties -> first in networkx adjacency order = earlier neighbours ascending, then later
 // neighbours by creation age (proof: DESIGN.md; pinned by tests/golden adj snapshots).
-__global__ void k_iso_target(int64_t n, const int64_t* flag, const int64_t* pos, const int64_t* rowptr,
-                             const int32_t* col, const int32_t* cw, const int32_t* ceid, const int64_t* eage,
-                             int32_t* iso, int64_t* isoidx, int32_t* target, int32_t* tw) {
-    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= n) return;
-    if (!flag[x]) { isoidx[x] = -1; return; }
-    const int64_t i = pos[x];
+__global__ void k_iso_target(int64_t n, const int32_t* sigma, const int32_t* npos, const int64_t* flag,
+                             const int64_t* pos, const int64_t* rowptr, const int32_t* col, const int32_t* cw,
+                             const int32_t* ceid, const int64_t* eage, int32_t* iso, int64_t* isoidx,
+                             int32_t* target, int32_t* tw) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int32_t x = sigma[t];
+    if (!flag[t]) { isoidx[x] = -1; return; }
+    const int64_t i = pos[t];
     isoidx[x] = i;
-    iso[i] = (int32_t)x;
+    iso[i] = x;
     int32_t bw = 0x7fffffff, by = -1;
     int64_t bs = 0x7fffffffffffffffll;
     for (int64_t j = rowptr[x]; j < rowptr[x + 1]; ++j) {
         const int32_t y = col[j], w = cw[j];
-        const int64_t sec = (y < x) ? (int64_t)y : ((int64_t)1 << 62) + eage[ceid[j]];
+        const int32_t py = npos[y];
+        const int64_t sec = (py < (int32_t)t) ? (int64_t)py : ((int64_t)1 << 62) + eage[ceid[j]];
         if (w < bw || (w == bw && sec < bs)) { bw = w; bs = sec; by = y; }
     }
     target[i] = by;
@@ -369,13 +376,13 @@ __global__ void k_iso_target(int64_t n, const int64_t* flag, const int64_t* pos,
 }
 // Sequential live-isolates semantics (nx.isolates is a lazy generator): x is skipped iff
 // an earlier repaired node chose x.  Resolved by Jacobi sweeps over the DAG x' -> T(x').
-__global__ void k_iso_hit(int64_t k, const int32_t* iso, const int64_t* isoidx, const int32_t* target,
-                          const int32_t* active, int32_t* hit) {
+__global__ void k_iso_hit(int64_t k, const int32_t* npos, const int32_t* iso, const int64_t* isoidx,
+                          const int32_t* target, const int32_t* active, int32_t* hit) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k || !active[i]) return;
     const int32_t y = target[i];
     const int64_t j = isoidx[y];
-    if (j >= 0 && y > iso[i]) hit[j] = 1;
+    if (j >= 0 && npos[y] > npos[iso[i]]) hit[j] = 1;   // y comes later in node order
 }
 __global__ void k_iso_update(int64_t k, const int32_t* hit, int32_t* active, int32_t* changed) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -388,9 +395,9 @@ __global__ void k_iso_flag64(int64_t k, const int32_t* active, int64_t* f) {
     if (i < k) f[i] = active[i];
     else if (i == k) f[i] = 0;
 }
-__global__ void k_repair_edges(int64_t k, const int64_t* f, const int64_t* p, const int32_t* iso,
-                               const int32_t* target, const int32_t* tw, int64_t base, int64_t off, int32_t* cu,
-                               int32_t* cv, int32_t* cw, int64_t* cage) {
+__global__ void k_repair_edges(int64_t k, const int32_t* npos, const int64_t* f, const int64_t* p,
+                               const int32_t* iso, const int32_t* target, const int32_t* tw, int64_t base, int64_t off,
+                               int32_t* cu, int32_t* cv, int32_t* cw, int64_t* cage) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k || !f[i]) return;
     const int32_t x = iso[i], y = target[i];
@@ -398,7 +405,7 @@ __global__ void k_repair_edges(int64_t k, const int64_t* f, const int64_t* p, co
     cu[q] = x < y ? x : y;
     cv[q] = x < y ? y : x;
     cw[q] = tw[i];                 // carries the old weight (:195)
-    cage[q] = base + AGE_REPAIR_OFFSET + x;
+    cage[q] = base + AGE_REPAIR_OFFSET + npos[x];   // added in node order
 }
 
 static int64_t repair(Ctx& c, int iteration) {
@@ -409,7 +416,9 @@ static int64_t repair(Ctx& c, int iteration) {
     if (c.n_cand > 0) k_deg_add<<<nblk(c.n_cand), TB, 0, c.stream>>>(c.n_cand, c.cu.as<int32_t>(), c.cv.as<int32_t>(), deg);
     int64_t* fl = ensure<int64_t>(c.nodetmp, n + 1);
     int64_t* ps = ensure<int64_t>(c.nodetmp2, n + 1);
-    k_iso_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, deg, g.rowptr.as<int64_t>(), fl);
+    const int32_t* sigma = c.sigma.as<int32_t>();
+    const int32_t* npos = c.npos.as<int32_t>();
+    k_iso_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, sigma, deg, g.rowptr.as<int64_t>(), fl);
     exclusive_scan(c, fl, ps, n + 1);
     const int64_t k = read_i64(c, ps + n);
     c.n_iso = k;
@@ -418,7 +427,7 @@ static int64_t repair(Ctx& c, int iteration) {
     int64_t* isoidx = ensure<int64_t>(c.isoflag, n);
     int32_t* target = ensure<int32_t>(c.target, k);
     int32_t* tw = ensure<int32_t>(c.tw, k);
-    k_iso_target<<<nblk(n), TB, 0, c.stream>>>(n, fl, ps, g.rowptr.as<int64_t>(), g.col.as<int32_t>(),
+    k_iso_target<<<nblk(n), TB, 0, c.stream>>>(n, sigma, npos, fl, ps, g.rowptr.as<int64_t>(), g.col.as<int32_t>(),
                                                 g.cw.as<int32_t>(), g.ceid.as<int32_t>(), g.eage.as<int64_t>(), iso,
                                                 isoidx, target, tw);
     int32_t* active = ensure<int32_t>(c.active, k);
@@ -427,7 +436,7 @@ static int64_t repair(Ctx& c, int iteration) {
     FC_HIP(hipMemsetAsync(active, 0, sizeof(int32_t) * k, c.stream));  // all-zero start: first pass flips all
     for (int64_t it = 0; it <= k + 1; ++it) {
         FC_HIP(hipMemsetAsync(hit, 0, sizeof(int32_t) * (k + 1), c.stream));
-        if (it > 0) k_iso_hit<<<nblk(k), TB, 0, c.stream>>>(k, iso, isoidx, target, active, hit);
+        if (it > 0) k_iso_hit<<<nblk(k), TB, 0, c.stream>>>(k, npos, iso, isoidx, target, active, hit);
         k_iso_update<<<nblk(k), TB, 0, c.stream>>>(k, hit, active, changed);
         int32_t ch = 0;
         FC_HIP(hipMemcpyAsync(&ch, changed, sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
@@ -440,7 +449,7 @@ static int64_t repair(Ctx& c, int iteration) {
     exclusive_scan(c, f, p, k + 1);
     const int64_t nrep = read_i64(c, p + k);
     const int64_t base = (int64_t)(iteration + 1) << AGE_ITER_SHIFT;
-    k_repair_edges<<<nblk(k), TB, 0, c.stream>>>(k, f, p, iso, target, tw, base, c.n_cand, c.cu.as<int32_t>(),
+    k_repair_edges<<<nblk(k), TB, 0, c.stream>>>(k, npos, f, p, iso, target, tw, base, c.n_cand, c.cu.as<int32_t>(),
                                                   c.cv.as<int32_t>(), c.cw2.as<int32_t>(), c.cage.as<int64_t>());
     return nrep;
 }

@@ -83,6 +83,11 @@ struct Ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     int64_t N = 0, m_original = 0;
+    // internal vertex numbering: internal = sigma[node], node = npos[internal] (a seeded
+    // random permutation, or the identity): engine behaviour is independent of input order
+    DevBuf sigma, npos;             // int32 [N]
+    std::vector<int32_t> h_sigma;
+    DevBuf st_u, st_v, st_w, st_age, st_lab;   // host-facing staging (node space)
     int key_bits = 1;               // bits to hold a node id (N <= 2^key_bits)
     Graph g;                        // `graph` (fast_consensus.py:131)
     Graph g0;                       // pristine G as loaded (never modified, like the caller's G)
@@ -114,7 +119,8 @@ struct Ctx {
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)
     // params
     int buckets = 32, max_sweeps = 200, max_iters = 1000;
-    int chunk = 0;                  // CD order granularity (0 = per vertex), FC_OPT_CHUNK
+    int chunk = 16;                 // CD order granularity (0 = per vertex), FC_OPT_CHUNK
+    int relabel = 1;                // FC_OPT_RELABEL (applies at the next fc_load_graph)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     bool trace = getenv("FC_TRACE") && *getenv("FC_TRACE") && *getenv("FC_TRACE") != '0';  // per-sweep stderr
     Timer timer;
@@ -131,7 +137,10 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src);
 // cd.cpp
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
 void labels_transpose(Ctx& c);
-void labels_renumber(Ctx& c);
+void labels_to_host(Ctx& c, int32_t* out, bool renumber);   // node order [n_r][N]
+void labels_from_host(Ctx& c, int count, const int32_t* in);
+void graph_to_host(Ctx& c, int64_t m, const int32_t* u, const int32_t* v, const int32_t* w, const int64_t* age,
+                   int32_t* ou, int32_t* ov, int32_t* ow, int64_t* oage);
 // consensus.cpp
 void consensus_partial(Ctx& c, int algo, int32_t* out);
 void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept,

@@ -124,6 +124,26 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
     for (int64_t i = 0; i < m; ++i)
         FC_REQUIRE(u[i] >= 0 && u[i] < n && v[i] >= 0 && v[i] < n, FC_EINVAL, "edge endpoint out of range");
     c.N = n;
+    // internal numbering (see Ctx::sigma); input edges are mapped on the host
+    c.h_sigma.resize(n);
+    for (int64_t i = 0; i < n; ++i) c.h_sigma[i] = (int32_t)i;
+    if (c.relabel) {
+        uint64_t st = mix64(c.seed ^ 0x51A7E5EDull);
+        for (int64_t i = n - 1; i > 0; --i) {
+            st = mix64(st + 0x9E3779B97F4A7C15ull);
+            const int64_t j = (int64_t)(((unsigned __int128)st * (uint64_t)(i + 1)) >> 64);
+            std::swap(c.h_sigma[i], c.h_sigma[j]);
+        }
+    }
+    std::vector<int32_t> h_npos(n);
+    for (int64_t i = 0; i < n; ++i) h_npos[c.h_sigma[i]] = (int32_t)i;
+    ensure<int32_t>(c.sigma, n); ensure<int32_t>(c.npos, n);
+    FC_HIP(hipMemcpyAsync(c.sigma.p, c.h_sigma.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
+    FC_HIP(hipMemcpyAsync(c.npos.p, h_npos.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
+    std::vector<int32_t> mu_(m), mv_(m);
+    for (int64_t i = 0; i < m; ++i) { mu_[i] = c.h_sigma[u[i]]; mv_[i] = c.h_sigma[v[i]]; }
+    u = mu_.data();
+    v = mv_.data();
     int bits = 1;
     while ((int64_t(1) << bits) < n) ++bits;
     c.key_bits = bits;
@@ -161,6 +181,47 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
     graph_build_csr(c, g);
     graph_copy(c, c.g0, g);
     c.labT_valid = false;
+    sync(c);   // the mapped host edge arrays die here
+}
+
+// ------------------------------------------------------------------ node-space export
+__global__ void k_export_keys(int64_t m, const int32_t* u, const int32_t* v, const int32_t* npos, int bits,
+                              uint64_t* key, int64_t* idx) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const uint64_t a = (uint64_t)npos[u[e]], b = (uint64_t)npos[v[e]];
+    key[e] = a < b ? (a << bits) | b : (b << bits) | a;
+    idx[e] = e;
+}
+__global__ void k_export_gather(int64_t m, const uint64_t* key, const int64_t* idx, int bits, const int32_t* w,
+                                const int64_t* age, int32_t* ou, int32_t* ov, int32_t* ow, int64_t* oage) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    ou[i] = (int32_t)(key[i] >> bits);
+    ov[i] = (int32_t)(key[i] & ((1ull << bits) - 1ull));
+    ow[i] = w[idx[i]];
+    oage[i] = age[idx[i]];
+}
+// An edge list in internal ids -> node ids, canonical (u<v) and sorted, on the host.
+void graph_to_host(Ctx& c, int64_t m, const int32_t* u, const int32_t* v, const int32_t* w, const int64_t* age,
+                   int32_t* ou, int32_t* ov, int32_t* ow, int64_t* oage) {
+    if (m <= 0) return;
+    uint64_t* k1 = ensure<uint64_t>(c.mkey, m);
+    uint64_t* k2 = ensure<uint64_t>(c.mkey2, m);
+    int64_t* i1 = ensure<int64_t>(c.midx, m);
+    int64_t* i2 = ensure<int64_t>(c.midx2, m);
+    int32_t* su = ensure<int32_t>(c.st_u, m);
+    int32_t* sv = ensure<int32_t>(c.st_v, m);
+    int32_t* sw = ensure<int32_t>(c.st_w, m);
+    int64_t* sa = ensure<int64_t>(c.st_age, m);
+    k_export_keys<<<nblk(m), TB, 0, c.stream>>>(m, u, v, c.npos.as<int32_t>(), c.key_bits, k1, i1);
+    sort_pairs(c, k1, k2, i1, i2, m, 2 * c.key_bits);
+    k_export_gather<<<nblk(m), TB, 0, c.stream>>>(m, k2, i2, c.key_bits, w, age, su, sv, sw, sa);
+    if (ou) FC_HIP(hipMemcpyAsync(ou, su, 4 * m, hipMemcpyDeviceToHost, c.stream));
+    if (ov) FC_HIP(hipMemcpyAsync(ov, sv, 4 * m, hipMemcpyDeviceToHost, c.stream));
+    if (ow) FC_HIP(hipMemcpyAsync(ow, sw, 4 * m, hipMemcpyDeviceToHost, c.stream));
+    if (oage) FC_HIP(hipMemcpyAsync(oage, sa, 8 * m, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
 }
 
 // graph = G.copy() (fast_consensus.py:131): device-to-device, the input stays resident.

@@ -79,7 +79,9 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_BUCKETS 1     /* rounds per CD sweep (default 32)                            */
 #define FC_OPT_MAX_SWEEPS 2  /* cap on sweeps per CD run (default 200)                      */
 #define FC_OPT_MAX_ITERS 3   /* cap on consensus iterations (default 1000)                  */
-#define FC_OPT_CHUNK 4       /* CD visit order granularity: 0 per vertex, else chunk size   */
+#define FC_OPT_CHUNK 4       /* CD visit order granularity: 0 per vertex, 16 (default) chunks */
+#define FC_OPT_RELABEL 6     /* 1 (default): engine-internal random vertex numbering (set it
+                                before fc_load_graph); results are reported in node order     */
 #define FC_OPT_PRUNE 5       /* 1 (default): once a sweep moves < n/4 vertices, later sweeps visit only vertices with a moved
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
@@ -90,6 +92,8 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value);
  * are set to 1 (fast_consensus.py:135-136). */
 int fc_load_graph(fc_ctx* ctx, int64_t n, int64_t m, const int32_t* u, const int32_t* v);
 int fc_graph_info(fc_ctx* ctx, int64_t* n, int64_t* m, int64_t* m_original);
+/* The engine's internal vertex numbering: sigma[node id] = internal id (testing aid). */
+int fc_get_node_map(fc_ctx* ctx, int32_t* sigma);
 /* graph <- the loaded G (device-to-device; fc_run does this itself, like graph = G.copy()
  * at fast_consensus.py:131).  The step API calls it before a new run. */
 int fc_reset_graph(fc_ctx* ctx);

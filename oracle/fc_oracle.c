@@ -173,7 +173,7 @@ static int cmp_adj(const void* a, const void* b) {
     return 0;
 }
 void orc_adjacency_order(i64 N, i64 m, const i32* eu, const i32* ev, const i32* w,
-                         const i64* age, i64* ptr, i32* nbr, i32* nw) {
+                         const i64* age, const i32* npos, i64* ptr, i32* nbr, i32* nw) {
     memset(ptr, 0, sizeof(i64) * (size_t)(N + 1));
     for (i64 e = 0; e < m; ++e) { ptr[eu[e] + 1]++; ptr[ev[e] + 1]++; }
     for (i64 x = 0; x < N; ++x) ptr[x + 1] += ptr[x];
@@ -181,9 +181,12 @@ void orc_adjacency_order(i64 N, i64 m, const i32* eu, const i32* ev, const i32* 
     i64* fill = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
     memcpy(fill, ptr, sizeof(i64) * (size_t)N);
     for (i64 e = 0; e < m; ++e) {
-        i32 u = eu[e], v = ev[e];                 /* u < v in node order */
-        /* in row v, u is an earlier neighbour: key = u (ascending node order) */
-        adj_t a = {u, (i64)u, w[e]};
+        /* ids may be an internal numbering; node order is npos[] (NULL: the ids themselves) */
+        i32 u = eu[e], v = ev[e];
+        if (npos && npos[u] > npos[v]) { i32 t = u; u = v; v = t; }     /* u earlier in node order */
+        const i64 pu = npos ? npos[u] : u;
+        /* in row v, u is an earlier neighbour: key = its node position (ascending) */
+        adj_t a = {u, pu, w[e]};
         tmp[fill[v]++] = a;
         /* in row u, v is a later neighbour: key = N + age (after all earlier ones) */
         adj_t b = {v, (i64)N + age[e], w[e]};
@@ -203,13 +206,20 @@ void orc_adjacency_order(i64 N, i64 m, const i32* eu, const i32* ev, const i32* 
  * Returns the number of repair edges written to out_u/out_v/out_w (canonical u<v) in
  * the order they are added; out_x (may be NULL) receives the repaired node x. */
 i64 orc_repair(i64 N, i64 m_old, const i32* ou, const i32* ov, const i32* ow, const i64* oage,
-               i64* deg, i32* out_u, i32* out_v, i32* out_w, i64* out_x) {
+               const i32* sigma, i64* deg, i32* out_u, i32* out_v, i32* out_w, i64* out_x) {
+    /* sigma (may be NULL): node position -> id; nodes are visited in node order */
     i64* ptr = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
     i32* nbr = (i32*)malloc(sizeof(i32) * (size_t)(2 * m_old + 1));
     i32* nw = (i32*)malloc(sizeof(i32) * (size_t)(2 * m_old + 1));
-    orc_adjacency_order(N, m_old, ou, ov, ow, oage, ptr, nbr, nw);
+    i32* npos = NULL;
+    if (sigma) {
+        npos = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+        for (i64 t = 0; t < N; ++t) npos[sigma[t]] = (i32)t;
+    }
+    orc_adjacency_order(N, m_old, ou, ov, ow, oage, npos, ptr, nbr, nw);
     i64 k = 0;
-    for (i64 x = 0; x < N; ++x) {
+    for (i64 t = 0; t < N; ++t) {
+        const i64 x = sigma ? sigma[t] : t;
         if (deg[x] != 0) continue;
         if (ptr[x + 1] == ptr[x]) continue;        /* reference would raise IndexError */
         i64 best = ptr[x];
@@ -217,11 +227,11 @@ i64 orc_repair(i64 N, i64 m_old, const i32* ou, const i32* ov, const i32* ow, co
             if (nw[j] < nw[best]) best = j;          /* strict: first minimum wins */
         i32 y = nbr[best];
         out_u[k] = (i32)(x < y ? x : y); out_v[k] = (i32)(x < y ? y : x); out_w[k] = nw[best];
-        if (out_x) out_x[k] = x;   /* creation order of repair edges = node order of x */
+        if (out_x) out_x[k] = t;   /* creation order of repair edges = node order of x */
         ++k;
         deg[x]++; deg[y]++;
     }
-    free(ptr); free(nbr); free(nw);
+    free(ptr); free(nbr); free(nw); free(npos);
     return k;
 }
 

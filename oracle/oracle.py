@@ -50,8 +50,10 @@ def lib():
         L.orc_closure_pairs.argtypes = [ctypes.c_int, i64, _i32p, _i32p, i64, _i32p, ctypes.c_int, i64, _i32p,
                                         _i32p, _i32p, _i32p, _i64p]
         L.orc_closure_pairs.restype = i64
-        L.orc_adjacency_order.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, _i64p, _i32p, _i32p]
-        L.orc_repair.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, _i64p, _i32p, _i32p, _i32p, _i64p]
+        L.orc_adjacency_order.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, ctypes.c_void_p, _i64p, _i32p,
+                                          _i32p]
+        L.orc_repair.argtypes = [i64, i64, _i32p, _i32p, _i32p, _i64p, ctypes.c_void_p, _i64p, _i32p, _i32p, _i32p,
+                                 _i64p]
         L.orc_repair.restype = i64
         L.orc_sort_edges.argtypes = [i64, _i32p, _i32p, _i64p]
         L.orc_louvain_level0.argtypes = [i64, _i64p, _i32p, _i32p, u64, _i32p]
@@ -125,7 +127,7 @@ class EdgeGraph:
         ptr = np.empty(self.N + 1, np.int64)
         nbr = np.empty(2 * self.m, np.int32)
         nw = np.empty(2 * self.m, np.int32)
-        lib().orc_adjacency_order(self.N, self.m, self.u, self.v, self.w, self.age, ptr, nbr, nw)
+        lib().orc_adjacency_order(self.N, self.m, self.u, self.v, self.w, self.age, None, ptr, nbr, nw)
         return ptr, nbr, nw
 
     def degrees(self):
@@ -182,12 +184,16 @@ def closure_sample_pairs(kept, attempts, seed, iteration):
     return pairs[:attempts]
 
 
-def repair(old, deg):
-    """deg: int64 degrees of nextgraph after closure (updated in place)."""
+def repair(old, deg, sigma=None):
+    """deg: int64 degrees of nextgraph after closure (updated in place).  sigma: node
+    position -> id when ids are an internal numbering (visit and tie-break in node order);
+    the returned x are node positions."""
     k_max = old.N
     ou, ov, ow = (np.empty(max(k_max, 1), np.int32) for _ in range(3))
     ox = np.empty(max(k_max, 1), np.int64)
-    k = lib().orc_repair(old.N, old.m, old.u, old.v, old.w, old.age, deg, ou, ov, ow, ox)
+    sg = None if sigma is None else np.ascontiguousarray(sigma, dtype=np.int32)
+    k = lib().orc_repair(old.N, old.m, old.u, old.v, old.w, old.age, None if sg is None else sg.ctypes.data, deg,
+                         ou, ov, ow, ox)
     return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), ox[:k].copy()
 
 
@@ -199,8 +205,9 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     return lab, sw
 
 
-def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=0, prune=1):
-    """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels)."""
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1):
+    """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels); defaults = the
+    engine's defaults (fc_ctx.h)."""
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)

@@ -12,16 +12,23 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=0, prune=1):
+    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None):
+        """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity."""
         self.seed = int(seed)
         self.buckets = buckets
         self.chunk = chunk
         self.prune = prune
+        self.sigma = None if sigma is None else np.asarray(sigma, np.int32)
         self.lab = None
 
     # graph -----------------------------------------------------------------------------
     def load_graph(self, n, u, v):
-        self.g0 = orc.EdgeGraph.from_lines(n, np.stack([np.asarray(u), np.asarray(v)], 1))
+        u, v = np.asarray(u), np.asarray(v)
+        if self.sigma is None:
+            self.sigma = np.arange(n, dtype=np.int32)
+        self.npos = np.empty(n, np.int32)
+        self.npos[self.sigma] = np.arange(n, dtype=np.int32)
+        self.g0 = orc.EdgeGraph.from_lines(n, np.stack([self.sigma[u], self.sigma[v]], 1))
         self.m0 = self.g0.m
         self.reset_graph()
 
@@ -89,14 +96,19 @@ class OracleEngine:
         parts = [self.kept, closure]
         if algo == 0:
             deg = self.kept.degrees() + closure.degrees()
-            ru, rv, rw, rx = orc.repair(self.g, deg)
+            ru, rv, rw, rx = orc.repair(self.g, deg, self.sigma)
             parts.append(orc.EdgeGraph(self.g.N, ru, rv, rw, base + orc.AGE_REPAIR_OFFSET + rx))
         self.g = orc.concat(parts)
         conv, _ = orc.check(self.g.w, n_p, delta)
         return conv, self.g.m
 
     def get_labels(self, count, renumber=False):
-        return orc.renumber(self.lab) if renumber else self.lab.copy()
+        node_order = self.lab[:, self.sigma]          # [r][t] = label of node t
+        return orc.renumber(node_order) if renumber else node_order.copy()
 
     def get_graph(self):
-        return self.g.u, self.g.v, self.g.w, self.g.age
+        """Node space, canonical and sorted (fc_get_graph)."""
+        a, b = self.npos[self.g.u], self.npos[self.g.v]
+        u, v = np.minimum(a, b), np.maximum(a, b)
+        o = np.lexsort((v, u))
+        return u[o], v[o], self.g.w[o], self.g.age[o]

@@ -56,3 +56,19 @@ def test_product_package_never_imports_oracle():
                 src = open(os.path.join(dirpath, fn)).read()
                 for pat in (r"^\s*(from|import)\s+oracle", r"fcoracle", r"\borc_[a-z]", r"oracle\.oracle"):
                     assert not re.search(pat, src, flags=re.M), (fn, pat)
+
+
+def test_cpu_twin_defaults_match_engine_defaults():
+    """orc.engine_cd / OracleEngine defaults are the engine's (fc_ctx.h), so a bare call of the
+    twin is the bit-exact target of a bare Engine.cd."""
+    import inspect
+    from oracle import oracle as orc
+    from tests.cpu_engine import OracleEngine
+    src = open(os.path.join(ROOT, "fastconsensus_amd", "csrc", "fc_ctx.h")).read()
+    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune")}
+    twin = inspect.signature(orc.engine_cd).parameters
+    model = inspect.signature(OracleEngine.__init__).parameters
+    for k, v in eng.items():
+        assert twin[k].default == v, k
+        if k in model:
+            assert model[k].default == v, k

@@ -20,6 +20,11 @@ def _graph():
     return case.N, case.edges_file
 
 
+def _sigma(N):
+    """A fixed internal numbering (the engine draws one per seed; any permutation works)."""
+    return np.random.default_rng(5).permutation(N).astype(np.int32)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -36,7 +41,7 @@ def _worker(rank, world, port, algo, n_p, tau, delta, out_path):
         from fastconsensus_amd.distributed import run_sharded
         from tests.cpu_engine import OracleEngine
         N, e = _graph()
-        eng = OracleEngine(seed=17)
+        eng = OracleEngine(seed=17, sigma=_sigma(N))
         eng.load_graph(N, e[:, 0], e[:, 1])
         labels, st = run_sharded(eng, algo, n_p, tau, delta, device="cpu", max_iters=50)
         if rank == 0:
@@ -51,7 +56,7 @@ def _single(algo, n_p, tau, delta):
     from fastconsensus_amd.distributed import run_sharded
     from tests.cpu_engine import OracleEngine
     N, e = _graph()
-    eng = OracleEngine(seed=17)
+    eng = OracleEngine(seed=17, sigma=_sigma(N))
     eng.load_graph(N, e[:, 0], e[:, 1])
     labels, st = run_sharded(eng, algo, n_p, tau, delta, device="cpu", max_iters=50)
     return labels, eng.get_graph(), st

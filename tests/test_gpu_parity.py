@@ -140,6 +140,16 @@ def test_consensus_second_iteration_weights(fcmod):
 
 
 # ------------------------------------------------------------------------- CD kernels vs CPU twin
+def _twin(eng, algo, N, e, count, r0, iteration, seed, **kw):
+    """The CPU twin on the engine's internal numbering (fc_get_node_map), labels returned
+    in node order like fc_get_labels."""
+    sigma = eng.node_map()
+    assert np.array_equal(np.sort(sigma), np.arange(N))
+    g_int = orc.EdgeGraph.from_lines(N, np.stack([sigma[e[:, 0]], sigma[e[:, 1]]], 1))
+    lab, sw = orc.engine_cd(algo, g_int, count, r0, iteration, seed, **kw)
+    return lab[:, sigma], sw
+
+
 def _lfr1k_graph():
     case = golden_io.load("lfr1k_louvain_np20")
     return case, orc.EdgeGraph.from_lines(case.N, case.edges_file)
@@ -158,7 +168,7 @@ def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune):
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 4)
     got = eng.get_labels(n_r)
-    exp, sw = orc.engine_cd(algo, g, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune)
+    exp, sw = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune)
     np.testing.assert_array_equal(got, exp)
     # sharding invariance: replicas 2..4 alone give the same labelings
     eng.cd(algo, 2, 3, n_r, 4)
@@ -190,14 +200,13 @@ def _heavy_graph(seed, hub_deg):
 @pytest.mark.parametrize("hub_deg,chunk,prune", [(300, 0, 0), (3000, 0, 0), (3000, 16, 0), (3000, 0, 1)])
 def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune):
     N, e = _heavy_graph(5, hub_deg)
-    g = orc.EdgeGraph.from_lines(N, e)
     eng = fcmod.Engine(seed=7)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
     eng.load_graph(N, e[:, 0], e[:, 1])
     eng.cd(algo, 0, 4, 4, 1)
     got = eng.get_labels(4)
-    exp, _ = orc.engine_cd(algo, g, 4, 0, 1, 7, chunk=chunk, prune=prune)
+    exp, _ = _twin(eng, algo, N, e, 4, 0, 1, 7, chunk=chunk, prune=prune)
     np.testing.assert_array_equal(got, exp)
     eng.close()
 
@@ -307,9 +316,10 @@ def test_closure_sampler_properties(fcmod):
 
 
 # ------------------------------------------------------------------------- whole runs, bit-exact
-@pytest.mark.parametrize("algo,n_p,tau,chunk,prune", [(0, 10, 0.2, 0, 0), (0, 12, 0.2, 16, 0), (1, 4, 0.8, 0, 0),
-                                                       (0, 20, 0.2, 0, 0), (0, 10, 0.2, 0, 1), (1, 6, 0.8, 16, 1)])
-def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune):
+@pytest.mark.parametrize("algo,n_p,tau,chunk,prune,relabel",
+                         [(0, 10, 0.2, 0, 0, 0), (0, 12, 0.2, 16, 0, 1), (1, 4, 0.8, 0, 0, 0), (0, 20, 0.2, 0, 0, 1),
+                          (0, 10, 0.2, 0, 1, 1), (1, 6, 0.8, 16, 1, 1), (0, 10, 0.2, 16, 1, 1)])
+def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
     loop (bucketed CD twin, consensus rule, Philox closure sampler, repair, ages): final
     partitions AND the final graph are identical (n_p=10 runs 9 iterations)."""
@@ -317,14 +327,18 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune):
     from tests.cpu_engine import OracleEngine
     case, _ = _lfr1k_graph()
     e = case.edges_file
-    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune)
-    cpu.load_graph(case.N, e[:, 0], e[:, 1])
-    exp_labels, exp_st = run_sharded(cpu, algo, n_p, tau, 0.02, device="cpu", max_iters=50)
     eng = fcmod.Engine(seed=17)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
+    eng.set_option("relabel", relabel)
     eng.set_params(max_iters=50)
     eng.load_graph(case.N, e[:, 0], e[:, 1])
+    sigma = eng.node_map()
+    if not relabel:
+        assert np.array_equal(sigma, np.arange(case.N))
+    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune, sigma=sigma)
+    cpu.load_graph(case.N, e[:, 0], e[:, 1])
+    exp_labels, exp_st = run_sharded(cpu, algo, n_p, tau, 0.02, device="cpu", max_iters=50)
     labels, st = eng.run(algo, n_p, tau, 0.02)
     assert st["iterations"] == exp_st["iterations"]
     assert st["partition_edges"] == exp_st["partition_edges"]
