@@ -21,6 +21,8 @@
 // rows go to a workgroup-per-vertex kernel (LDS table up to 4096 slots, else global).
 #include <hipcub/hipcub.hpp>
 
+#include <chrono>
+
 #include "fc_ctx.h"
 #include "fc_device.h"
 
@@ -29,9 +31,11 @@ namespace fc {
 template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
 
 static constexpr int TB = 256;
-static constexpr int TILE = 16;
+static constexpr int TILE = 16;         // lanes per decision in k_apply's row scatter
 static constexpr int TILES = TB / TILE;
-static constexpr int HCAP = 128;        // slots per tile table
+static constexpr int LT = 8;            // lanes per vertex in k_decide_light
+static constexpr int LNT = TB / LT;     // vertices per k_decide_light block
+static constexpr int HCAP = 64;         // slots per tile table (>= LIGHT_MAX_DEG: every insert finds a slot)
 static constexpr int LIGHT_MAX_DEG = 64;
 static constexpr int HEAVY_LDS_SLOTS = 4096;
 static constexpr int HEAVY_GRID = 256;
@@ -64,7 +68,7 @@ struct CDArgs {
     const int32_t* rev;          // reverse adjacency entry of j
     int64_t m2;                  // 2m (adjacency entries)
     void* tot;                   // int32 [n_r][N] when 2M < 2^31, else int64
-    int32_t* dec;
+    int2* dec;                   // [n_r][S] (target community or -1, vertex)
     int32_t* active;
     // Sharded per-replica counters [n_r][NSH][RF]: one hot address per replica would
     // serialise every block's atomic (~12 ns each, MI355X_MICROARCH.md "fanin").
@@ -74,7 +78,7 @@ struct CDArgs {
     int32_t* track;              // [n_r] moves mark neighbours affected this sweep; [n_r..2n_r) list filters;
                                  // [2n_r..3n_r) push mode: nlab is current (else decide gathers lab[col])
     int prune;
-    const int32_t* list;         // [B][n_r][S] bucket positions to visit, or nullptr = every position
+    const int32_t* list;         // [B][n_r][S] vertices to visit (bucket order), or nullptr = every position
     const int32_t* lcnt;         // [B][n_r] list lengths
     const int32_t* blk_off;      // [B][n_r+1] light-kernel block offsets per replica
     int32_t* heavy;              // (r, dec index, position) triples
@@ -157,26 +161,30 @@ __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t 
     }
 }
 
-// One 16-lane tile per vertex.  Every lane first issues ALL of its (<= 4) neighbour
-// gathers (col, weight, neighbour label) so up to 4 misses per lane are in flight, then
-// inserts them into the tile's LDS hash table; the lane that creates a slot owns it and
-// evaluates that candidate community (its tot gather batched likewise).
-template <bool LOUV, typename TT>
+// One LT-lane tile per vertex (LT = 8: 32 vertices per block, so twice the visits of a
+// 16-lane tile are in flight per CU; the visit is a chain of dependent gathers, so that
+// is what sets the rate).  The vertex's own label, degree and own-community total are
+// fetched first, alongside the row; then every lane issues ALL of its (<= PER) neighbour
+// gathers before it inserts them into the tile's LDS hash table; the lane that creates a
+// slot owns it and evaluates that candidate community (its Sigma gather batched likewise).
+template <bool LOUV, typename TT, int LT>
 __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep, int64_t blen,
                                                       int64_t chunks) {
-    __shared__ __attribute__((aligned(16))) int32_t s_key[TILES * HCAP];
-    __shared__ __attribute__((aligned(16))) int32_t s_val[TILES * HCAP];
-    __shared__ unsigned long long s_red[TILES][5];
-    constexpr int PER = LIGHT_MAX_DEG / TILE;   // neighbours per lane
-    const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
+    constexpr int NT = TB / LT;                 // tiles (vertices) per block
+    constexpr int PER = LIGHT_MAX_DEG / LT;     // neighbours per lane
+    __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
+    __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
+    __shared__ unsigned long long s_red[TB / 64][5];
+    const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
     int r;
     int64_t chunk;
-    int64_t di, i;             // decision slot (dec index) and position inside the bucket
+    int64_t di;                // decision slot
     bool in_range;
+    int32_t v = -1;
     if (!a.list) {
         xcd_remap(blockIdx.x, (int64_t)gridDim.x, chunks, &r, &chunk);
-        di = i = chunk * TILES + tile;
-        in_range = i < blen;
+        di = chunk * NT + tile;
+        in_range = di < blen;
     } else {
         int rr;
         int64_t w;
@@ -185,37 +193,42 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         int lo = 0, hi = a.n_r;            // last replica with bo[r] <= w (uniform search)
         while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (bo[mid] <= w) lo = mid; else hi = mid; }
         r = lo;
-        di = (w - bo[r]) * TILES + tile;
+        di = (w - bo[r]) * NT + tile;
         const int64_t seg = ((int64_t)bucket * a.n_r + r);
         in_range = di < a.lcnt[seg];
-        i = in_range ? a.list[seg * a.S + di] : 0;
+        if (in_range) v = a.list[seg * a.S + di];   // lists hold vertex ids
     }
     const int rg = a.rbase + r;
     const bool rep_on = r < a.n_r && a.active[r];
     bool valid = rep_on && in_range;
-    int32_t v = 0;
-    int64_t rb = 0, d = 0;
-    if (valid) {
+    if (valid && !a.list) {
         const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
-        v = pos_vertex(a, P, bucket * a.S + i);
+        v = pos_vertex(a, P, bucket * a.S + di);
         valid = v >= 0;
     }
+    const int32_t* labr = a.lab + (int64_t)r * a.N;
+    const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
+    int64_t rb = 0, d = 0;
+    int32_t own = 0;
+    int64_t kv = 0;
+    TT tot_own = 0;
     if (valid) {
         rb = a.rowptr[v];
         d = a.rowptr[v + 1] - rb;
+        own = labr[v];
+        if (LOUV) kv = a.kdeg[v];
     }
     const bool heavy = valid && d > LIGHT_MAX_DEG;
     const bool work = valid && !heavy && d > 0;
-    const int32_t* labr = a.lab + (int64_t)r * a.N;
+    if (LOUV && work) tot_own = totr[own];       // in flight with the row loads below
     const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-    const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
     // ---- push mode: the row's neighbour labels are STREAMED from nlab; pull mode (early,
     // move-heavy sweeps): gathered from lab[col[j]] -- the same values either way
     const bool push = a.track[2 * a.n_r + r] != 0;
     int32_t cq[PER], wq[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        const int64_t j = rb + lane + TILE * q;
+        const int64_t j = rb + lane + LT * q;
         const bool ok = work && j < rb + d;
         cq[q] = ok ? (push ? nlr[j] : a.col[j]) : -1;
         wq[q] = ok ? (LOUV ? a.cw[j] : 1) : 0;
@@ -224,15 +237,13 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
 #pragma unroll
         for (int q = 0; q < PER; ++q) cq[q] = cq[q] >= 0 ? labr[cq[q]] : -1;
     }
-    const int32_t own = work ? labr[v] : 0;
-    const int64_t kv = (LOUV && work) ? a.kdeg[v] : 0;
     // ---- tile table: clear (16-byte stores), insert, owners evaluate
     int32_t* keys = s_key + tile * HCAP;
     int32_t* vals = s_val + tile * HCAP;
     {
         int4* k4 = reinterpret_cast<int4*>(keys);
         int4* v4 = reinterpret_cast<int4*>(vals);
-        for (int s = lane; s < HCAP / 4; s += TILE) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
+        for (int s = lane; s < HCAP / 4; s += LT) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
     }
     __syncthreads();
     int slot[PER];
@@ -242,18 +253,19 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     TT tq[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) tq[q] = (LOUV && slot[q] >= 0 && cq[q] != own) ? totr[cq[q]] : (TT)0;
-    long long best_s = LLONG_MIN, kown = 0;
-    uint32_t best_h = 0;
-    int32_t best_c = 0x7fffffff;
-    int have = 0, ncand = 0;
-    const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
+    // candidates ranked lexicographically by (score, tie hash, -id); key2 packs the last two
+    long long best_s = LLONG_MIN;
+    unsigned long long best_k = 0;
+    TT kown = 0;
+    int ncand = 0;
+    const uint32_t tvh = hash32(stream_key(a.seed, rg, a.iter, sweep, 2) ^ (uint32_t)v);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (slot[q] < 0) continue;
         const int32_t key = cq[q];
         const int32_t val = vals[slot[q]];
         ++ncand;
-        if (key == own) kown = val;
+        if (key == own) kown = (TT)val;
         long long sc;
         if (LOUV) {
             if (key == own) continue;
@@ -261,41 +273,60 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         } else {
             sc = val;
         }
-        const uint32_t h = tie_hash(tbk, v, key);
-        if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
+        const unsigned long long k2 = ((unsigned long long)hash32(tvh ^ (uint32_t)key) << 32) | (uint32_t)~key;
+        if (sc > best_s || (sc == best_s && k2 > best_k)) { best_s = sc; best_k = k2; }
     }
 #pragma unroll
-    for (int off = TILE / 2; off > 0; off >>= 1) {
-        const long long os = __shfl_xor(best_s, off, TILE);
-        const uint32_t oh = (uint32_t)__shfl_xor((int)best_h, off, TILE);
-        const int32_t oc = __shfl_xor(best_c, off, TILE);
-        const int oh_ = __shfl_xor(have, off, TILE);
-        if (oh_ && (!have || better(os, oh, oc, best_s, best_h, best_c))) { best_s = os; best_h = oh; best_c = oc; have = 1; }
-        kown += __shfl_xor(kown, off, TILE);
-        ncand += __shfl_xor(ncand, off, TILE);
+    for (int off = LT / 2; off > 0; off >>= 1) {
+        const long long os = __shfl_xor(best_s, off, LT);
+        const unsigned long long ok2 = __shfl_xor(best_k, off, LT);
+        if (os > best_s || (os == best_s && ok2 > best_k)) { best_s = os; best_k = ok2; }
+        kown += __shfl_xor(kown, off, LT);
+        ncand += __shfl_xor(ncand, off, LT);
     }
+    // (best_s == LLONG_MIN: no candidate other than the own community)
     unsigned long long dq = 0;
-    int unst = 0;
+    int unst = 0, dcs = -1;
+    if (work && best_s != LLONG_MIN) {
+        const int32_t best_c = (int32_t)~(uint32_t)best_k;
+        if (LOUV) {
+            const long long G = best_s - (long long)kown * a.M2 + kv * ((long long)tot_own - kv);
+            if (G > 0) {
+                const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+                dq = (unsigned long long)llrint(dqd * DQ_SCALE);
+                dcs = best_c;
+            }
+        } else {
+            unst = (long long)kown != best_s;   // own label not dominant
+            dcs = best_c != own ? best_c : -1;
+        }
+    }
     if (lane == 0) {
-        int32_t dcs = -1;
-        if (work) dcs = decide_final<LOUV, TT>(a, r, v, own, best_s, best_c, kown, have, &dq, &unst);
-        if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = dcs;   // heavy rows: overwritten by k_decide_heavy
+        if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = make_int2(dcs, v);   // heavy: rewritten later
         if (heavy) {
             const int q = atomicAdd(a.heavy_cnt, 1);
             a.heavy[3 * q] = r;
             a.heavy[3 * q + 1] = (int32_t)di;
-            a.heavy[3 * q + 2] = (int32_t)i;
+            a.heavy[3 * q + 2] = v;
         }
-        s_red[tile][0] = dq;
-        s_red[tile][1] = (unsigned long long)unst;
-        s_red[tile][2] = work ? 1ull : 0ull;
-        s_red[tile][3] = work ? (unsigned long long)d : 0ull;
-        s_red[tile][4] = work ? (unsigned long long)ncand : 0ull;
+    }
+    // ---- block counters: tile lane 0 holds them; wave sums, then one add per field
+    unsigned long long f0 = lane == 0 ? dq : 0, f1 = lane == 0 ? (unsigned long long)unst : 0;
+    unsigned long long f2 = (lane == 0 && work) ? 1ull : 0, f3 = (lane == 0 && work) ? (unsigned long long)d : 0;
+    unsigned long long f4 = (lane == 0 && work) ? (unsigned long long)ncand : 0;
+#pragma unroll
+    for (int off = LT; off < 64; off <<= 1) {
+        f0 += __shfl_xor(f0, off); f1 += __shfl_xor(f1, off); f2 += __shfl_xor(f2, off);
+        f3 += __shfl_xor(f3, off); f4 += __shfl_xor(f4, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        const int w = threadIdx.x >> 6;
+        s_red[w][0] = f0; s_red[w][1] = f1; s_red[w][2] = f2; s_red[w][3] = f3; s_red[w][4] = f4;
     }
     __syncthreads();
     if (threadIdx.x < 5 && rep_on) {
         unsigned long long s = 0;
-        for (int t = 0; t < TILES; ++t) s += s_red[t][threadIdx.x];
+        for (int w = 0; w < TB / 64; ++w) s += s_red[w][threadIdx.x];
         // fields: s_red 0 dq -> 0, 1 unstable -> 1, 2 verts -> 3, 3 entries -> 4, 4 cands -> 5
         if (s) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), s);
     }
@@ -315,11 +346,9 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
         const int r = a.heavy[3 * item];
         const int64_t di = a.heavy[3 * item + 1];
-        const int64_t i = a.heavy[3 * item + 2];
+        const int32_t v = a.heavy[3 * item + 2];
         const int rg = a.rbase + r;
-        const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
         const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
-        const int32_t v = pos_vertex(a, P, bucket * a.S + i);
         const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
         uint32_t slots = 1;
         while (slots < 2 * (uint32_t)d) slots <<= 1;
@@ -380,7 +409,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
             unsigned long long dq = 0;
             int unst = 0;
             const int32_t dcs = decide_final<LOUV, TT>(a, r, v, own, r_s[0], r_c[0], r_kown[0], r_have[0], &dq, &unst);
-            a.dec[(int64_t)r * a.S + di] = dcs;
+            a.dec[(int64_t)r * a.S + di] = make_int2(dcs, v);
             if (dq) atomicAdd(red_slot(a, r, 0), dq);
             if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
         }
@@ -388,11 +417,50 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     }
 }
 
-// Apply a bucket's decisions: one 16-lane tile per decision slot; lane 0 updates the
-// label and the community totals, the tile scatters the new label into the reverse
-// adjacency entries (nlab) and, while tracking, flags the neighbours for the next sweep.
+// Apply a bucket's decisions, label + community totals only (no replica pushes or
+// tracks this sweep): one thread per decision slot.
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, int64_t blen) {
+__global__ __launch_bounds__(256) void k_apply_lab(CDArgs a, int bucket, int64_t blen) {
+    const int r = blockIdx.y;
+    const int64_t di = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int64_t seg = (int64_t)bucket * a.n_r + r;
+    const bool in_range = a.list ? di < a.lcnt[seg] : di < blen;
+    int moved = 0;
+    if (in_range && a.active[r]) {
+        const int2 dv = a.dec[(int64_t)r * a.S + di];
+        if (dv.x >= 0) {
+            int32_t* l = a.lab + (int64_t)r * a.N + dv.y;
+            const int32_t old = *l;
+            *l = dv.x;
+            if (LOUV) {
+                TT* tot = (TT*)a.tot + (int64_t)r * a.N;
+                const TT kv = (TT)a.kdeg[dv.y];
+                if constexpr (sizeof(TT) == 8) {
+                    atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
+                    atomicAdd((unsigned long long*)&tot[dv.x], (unsigned long long)kv);
+                } else {
+                    atomicAdd((int*)&tot[old], -(int)kv);
+                    atomicAdd((int*)&tot[dv.x], (int)kv);
+                }
+            }
+            moved = 1;
+        }
+    }
+    const unsigned long long b = __ballot(moved);
+    __shared__ unsigned long long s_mv;
+    if (threadIdx.x == 0) s_mv = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&s_mv, (unsigned long long)__popcll(b));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_mv) atomicAdd(red_slot(a, r, 2), s_mv);
+}
+
+// Same, for sweeps in which some replica pushes labels or tracks moves: one 16-lane tile
+// per decision slot; lane 0 updates the label and the community totals, the tile scatters
+// the new label into the reverse adjacency entries (nlab) and, while tracking, flags the
+// neighbours for the next sweep.
+template <bool LOUV, typename TT>
+__global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int64_t blen) {
     const int r = blockIdx.y;
     const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
     const int64_t di = (int64_t)blockIdx.x * TILES + tile;
@@ -400,11 +468,9 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int sweep, 
     const int64_t seg = (int64_t)bucket * a.n_r + r;
     const bool in_range = a.list ? di < a.lcnt[seg] : di < blen;
     if (in_range && a.active[r]) {
-        const int32_t d = a.dec[(int64_t)r * a.S + di];
+        const int2 dv = a.dec[(int64_t)r * a.S + di];
+        const int32_t d = dv.x, v = dv.y;
         if (d >= 0) {
-            const int64_t i = a.list ? a.list[seg * a.S + di] : di;
-            const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
-            const int32_t v = pos_vertex(a, P, bucket * a.S + i);
             if (lane == 0) {
                 int32_t* l = a.lab + (int64_t)r * a.N + v;
                 const int32_t old = *l;
@@ -505,8 +571,8 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
     if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
 }
 
-// Pruned sweep: per (bucket, replica) the positions whose vertex is flagged affected, in
-// position order (deterministic); flags are read and cleared here, moves of this sweep
+// Pruned sweep: per (bucket, replica) the vertices flagged affected, in position order
+// (deterministic); flags are read and cleared here, moves of this sweep
 // set them again for the next one.  One block per (bucket, replica) segment.
 __global__ __launch_bounds__(256) void k_build_lists(CDArgs a, int sweep, int64_t PN, int32_t* list, int32_t* lcnt) {
     const int k = blockIdx.x / a.n_r, r = blockIdx.x % a.n_r;
@@ -525,8 +591,9 @@ __global__ __launch_bounds__(256) void k_build_lists(CDArgs a, int sweep, int64_
     for (int64_t i0 = 0; i0 < blen; i0 += TB) {
         const int64_t i = i0 + threadIdx.x;
         bool f = false;
+        int32_t v = -1;
         if (i < blen) {
-            const int32_t v = pos_vertex(a, P, (int64_t)k * a.S + i);
+            v = pos_vertex(a, P, (int64_t)k * a.S + i);
             if (v >= 0) { f = filter ? aff[v] != 0 : true; aff[v] = 0; }
         }
         const unsigned long long b = __ballot(f);
@@ -536,7 +603,7 @@ __global__ __launch_bounds__(256) void k_build_lists(CDArgs a, int sweep, int64_
         for (int w = 0; w < wave; ++w) off += s_w[w];
         int tot = 0;
         for (int w = 0; w < TB / 64; ++w) tot += s_w[w];
-        if (f) list[seg * a.S + off + __popcll(b & ((1ull << lane) - 1ull))] = (int32_t)i;
+        if (f) list[seg * a.S + off + __popcll(b & ((1ull << lane) - 1ull))] = v;
         base += tot;
         __syncthreads();
     }
@@ -545,21 +612,22 @@ __global__ __launch_bounds__(256) void k_build_lists(CDArgs a, int sweep, int64_
 
 // One bucket: decide (light + heavy rows) against the state left by earlier buckets, apply.
 // Full mode: grid = all bucket positions of every replica.  List mode: light blocks =
-// light_blocks (sum over replicas of ceil(list length / 16)), apply covers max_len.
+// light_blocks (sum over replicas of ceil(list length / LNT)), apply covers max_len.
+// rows: some replica pushes labels or tracks moves this sweep (row-scatter apply).
 template <bool LOUV, typename TT>
 static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, int64_t blen, bool any_heavy,
-                      int64_t light_blocks, int64_t max_len) {
-    const int64_t chunks = (blen + TILES - 1) / TILES;
+                      int64_t light_blocks, int64_t max_len, bool rows) {
+    const int64_t chunks = (blen + LNT - 1) / LNT;
     const int64_t nb = a.list ? light_blocks : chunks * a.n_r;
     const int64_t alen = a.list ? max_len : blen;
     if (nb <= 0) return;
-    FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
+    if (any_heavy) FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     const int ev = timer_begin(c);
-    k_decide_light<LOUV, TT><<<(unsigned)nb, TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
+    k_decide_light<LOUV, TT, LT><<<(unsigned)nb, TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
-    dim3 ag((unsigned)((alen + TILES - 1) / TILES), a.n_r);
-    k_apply<LOUV, TT><<<ag, TB, 0, c.stream>>>(a, k, sweep, blen);
+    if (rows) k_apply<LOUV, TT><<<dim3((unsigned)((alen + TILES - 1) / TILES), a.n_r), TB, 0, c.stream>>>(a, k, blen);
+    else k_apply_lab<LOUV, TT><<<dim3((unsigned)((alen + TB - 1) / TB), a.n_r), TB, 0, c.stream>>>(a, k, blen);
 }
 
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
@@ -582,7 +650,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // tot in int32 whenever every community total fits (all <= 2M < 2^31): half the gathers
     const bool tot32 = g.M2 <= 0x7fffffffll;
     void* tot = louv ? (void*)ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
-    int32_t* dec = ensure<int32_t>(c.dec, (size_t)rcount * S);
+    int2* dec = ensure<int2>(c.dec, (size_t)rcount * S);
     const int64_t m2 = 2 * g.m;
     int32_t* nlab = ensure<int32_t>(c.nlab, (size_t)rcount * (m2 > 0 ? m2 : 1));
     // per-replica state: active i32 [n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active
@@ -632,8 +700,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
 
     int n_act = (g.M2 > 0) ? rcount : 0;
     int sweep = 0;
-    bool any_switch = false;
-    std::vector<int32_t> h_sw(rcount);
+    bool any_switch = false, rows = false;
+    std::vector<int32_t> h_tr(4 * (size_t)rcount);
     for (; sweep < c.max_sweeps && n_act > 0; ++sweep) {
         c.acc.cd_sweeps += n_act;
         c.prof.cd_sweeps += n_act;
@@ -653,7 +721,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                 for (int r = 0; r < rcount; ++r) {
                     const int64_t n = h_cnt[(size_t)k * rcount + r];
                     h_off[(size_t)k * (rcount + 1) + r] = (int32_t)acc;
-                    acc += (n + TILES - 1) / TILES;
+                    acc += (n + LNT - 1) / LNT;
                     mx = std::max(mx, n);
                 }
                 h_off[(size_t)k * (rcount + 1) + rcount] = (int32_t)acc;
@@ -667,28 +735,35 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             const int64_t blen = std::min<int64_t>(S, PN - (int64_t)k * S);
             if (blen <= 0) continue;
             const bool hv = g.max_deg > LIGHT_MAX_DEG;
-            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k]);
-            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k]);
-            else sub_round<true, int64_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k]);
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k], rows);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k], rows);
+            else sub_round<true, int64_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k], rows);
         }
         if (a.list) sync(c);   // h_off (pageable) must outlive its async upload
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
         FC_HIP(hipMemcpyAsync(c.hpin, n_active, 16, hipMemcpyDeviceToHost, c.stream));
-        FC_HIP(hipMemcpyAsync(h_sw.data(), track + 3 * (size_t)rcount, 4 * (size_t)rcount, hipMemcpyDeviceToHost,
-                              c.stream));
+        FC_HIP(hipMemcpyAsync(h_tr.data(), track, 16 * (size_t)rcount, hipMemcpyDeviceToHost, c.stream));
         sync(c);
         n_act = ((int32_t*)c.hpin)[0];
-        any_switch = false;
-        for (int r = 0; r < rcount; ++r) any_switch |= h_sw[r] != 0;
+        // next sweep: replicas entering push mode; whether any replica pushes or tracks
+        any_switch = rows = false;
+        for (int r = 0; r < rcount; ++r) {
+            any_switch |= h_tr[3 * (size_t)rcount + r] != 0;
+            rows |= h_tr[r] != 0 || h_tr[2 * (size_t)rcount + r] != 0 || h_tr[3 * (size_t)rcount + r] != 0;
+        }
         if (c.trace) {
             std::vector<unsigned long long> sa(4 * (size_t)rcount);
             FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
             sync(c);
             unsigned long long vv = 0;
             for (int r = 0; r < rcount; ++r) vv += sa[4 * r];
-            fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu moves=%llu\n", iteration,
-                    sweep, n_act, vv, (unsigned long long)c.hpin[1]);
+            static auto t_last = std::chrono::steady_clock::now();
+            const auto t_now = std::chrono::steady_clock::now();
+            fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu moves=%llu push=%d dt_us=%.0f\n",
+                    iteration, sweep, n_act, vv, (unsigned long long)c.hpin[1], (int)any_switch,
+                    1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
+            t_last = t_now;
         }
     }
     // light-kernel traffic counters for the roofline model
