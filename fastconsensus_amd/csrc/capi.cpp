@@ -172,7 +172,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_MAX_SWEEPS: FC_REQUIRE(value >= 1, FC_EINVAL, "max_sweeps >= 1"); c.max_sweeps = (int)value; break;
         case FC_OPT_MAX_ITERS: FC_REQUIRE(value >= 1, FC_EINVAL, "max_iters >= 1"); c.max_iters = (int)value; break;
         case FC_OPT_CHUNK:
-            FC_REQUIRE(value == 0 || value == 16, FC_EINVAL, "chunk must be 0 or 16 (one block of tiles)");
+            FC_REQUIRE(value == 0 || value == 16, FC_EINVAL, "chunk must be 0 or 16");
             c.chunk = (int)value;
             break;
         case FC_OPT_PRUNE: c.prune = value != 0; break;

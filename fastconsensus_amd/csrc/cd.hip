@@ -76,7 +76,9 @@ struct CDArgs {
     // pruning (list mode): per sweep >= 1 only vertices whose neighbour moved are visited
     uint8_t* aff;                // [n_r][N] affected flags (set by moves, read+cleared by list build)
     int32_t* track;              // [n_r] moves mark neighbours affected this sweep; [n_r..2n_r) list filters;
-                                 // [2n_r..3n_r) push mode: nlab is current (else decide gathers lab[col])
+                                 // [2n_r..3n_r) push mode: nlab is current (else decide gathers lab[col]);
+                                 // [3n_r..4n_r) transition sweep: decide writes the nlab rows it gathers,
+                                 // moves push (every vertex is visited), push mode from the next sweep
     int prune;
     const int32_t* list;         // [B][n_r][S] vertices to visit (bucket order), or nullptr = every position
     const int32_t* lcnt;         // [B][n_r] list lengths
@@ -86,17 +88,21 @@ struct CDArgs {
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
     int64_t heavy_slots;         // slots per global table (power of 2)
     unsigned long long* sacc;    // [n_r][4] light-kernel vertices / entries / candidates, summed by k_sweep_end
+    int dbg;                     // FC_DBG ablation bits (timing experiments only; results become wrong)
 };
 
 __device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
     return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
 }
 
-// Vertex visited at sweep position p, or -1 for a padding slot of the last chunk.
+// Vertex visited at sweep position p, or -1 for a padding slot of the last chunk
+// (chunk is 0 or CHUNK, FC_OPT_CHUNK; positions fit 32 bits since N < 2^31).
+static constexpr int CHUNK = 16;
 __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, int64_t p) {
-    if (!a.chunk) return (int32_t)perm_apply(P, (uint32_t)p);
-    const int64_t v = (int64_t)perm_apply(P, (uint32_t)(p / a.chunk)) * a.chunk + (p % a.chunk);
-    return v < a.N ? (int32_t)v : -1;
+    const uint32_t p32 = (uint32_t)p;
+    if (!a.chunk) return (int32_t)perm_apply(P, p32);
+    const uint32_t v = perm_apply(P, p32 / CHUNK) * CHUNK + (p32 % CHUNK);
+    return v < (uint32_t)a.N ? (int32_t)v : -1;
 }
 
 // Block -> (replica, chunk) with all chunks of a replica on as few XCDs as possible
@@ -234,8 +240,15 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         wq[q] = ok ? (LOUV ? a.cw[j] : 1) : 0;
     }
     if (!push) {
+        if (!(a.dbg & 2))
 #pragma unroll
-        for (int q = 0; q < PER; ++q) cq[q] = cq[q] >= 0 ? labr[cq[q]] : -1;
+            for (int q = 0; q < PER; ++q) cq[q] = cq[q] >= 0 ? labr[cq[q]] : -1;
+        if (a.track[3 * a.n_r + r]) {    // transition sweep: this row's nlab entries, as seen now
+            int32_t* nlw = a.nlab + (int64_t)r * a.m2;
+#pragma unroll
+            for (int q = 0; q < PER; ++q)
+                if (cq[q] >= 0) nlw[rb + lane + LT * q] = cq[q];
+        }
     }
     // ---- tile table: clear (16-byte stores), insert, owners evaluate
     int32_t* keys = s_key + tile * HCAP;
@@ -246,41 +259,112 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         for (int s = lane; s < HCAP / 4; s += LT) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
     }
     __syncthreads();
+    // insert: every lane's first probes are issued back to back (one LDS round trip for
+    // all of them; a wave's LDS operations execute in order, so entries of one key agree
+    // on its slot), collisions then probe linearly; the lane whose CAS created a slot owns it
     int slot[PER];
+    {
+        uint32_t hq[PER];
+        int32_t pv[PER];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) slot[q] = cq[q] >= 0 ? tbl_insert_owner(keys, vals, HCAP - 1, cq[q], wq[q]) : -1;
+        for (int q = 0; q < PER; ++q) {
+            hq[q] = hash32((uint32_t)cq[q]) & (HCAP - 1);
+            pv[q] = cq[q] >= 0 ? atomicCAS(&keys[hq[q]], -1, cq[q]) : cq[q];
+        }
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            slot[q] = -1;
+            if (cq[q] < 0) continue;
+            while (pv[q] != -1 && pv[q] != cq[q]) {
+                hq[q] = (hq[q] + 1) & (HCAP - 1);
+                pv[q] = atomicCAS(&keys[hq[q]], -1, cq[q]);
+            }
+            atomicAdd(&vals[hq[q]], wq[q]);
+            if (pv[q] == -1) slot[q] = (int)hq[q];
+        }
+    }
     __syncthreads();
+    // ---- evaluate.  Candidates rank lexicographically by (score, tie hash, -id); key2 packs
+    // the last two.  Louvain: score_c = val_c*2M - k_v*Sigma_c <= val_c*2M, so only the
+    // candidates of maximal val need their Sigma gathered, unless a lower one's bound still
+    // reaches the best exact score (rare: needs k_v*Sigma_best >= 2M) -- the same argmax
+    // with a fraction of the random Sigma gathers.  LPA: score = val (own label included).
+    int32_t vq[PER];
+    int vm = INT_MIN;
+    TT kown = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        vq[q] = slot[q] >= 0 ? vals[slot[q]] : 0;
+        if (slot[q] >= 0) {
+            if (cq[q] == own) kown = (TT)vq[q];
+            else vm = max(vm, vq[q]);
+        }
+    }
+    if (LOUV) {
+#pragma unroll
+        for (int off = LT / 2; off > 0; off >>= 1) vm = max(vm, __shfl_xor(vm, off, LT));
+    }
     TT tq[PER];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) tq[q] = (LOUV && slot[q] >= 0 && cq[q] != own) ? totr[cq[q]] : (TT)0;
-    // candidates ranked lexicographically by (score, tie hash, -id); key2 packs the last two
+    for (int q = 0; q < PER; ++q)
+        tq[q] = (LOUV && slot[q] >= 0 && cq[q] != own && vq[q] == vm && !(a.dbg & 1)) ? totr[cq[q]] : (TT)0;
     long long best_s = LLONG_MIN;
     unsigned long long best_k = 0;
-    TT kown = 0;
     int ncand = 0;
     const uint32_t tvh = hash32(stream_key(a.seed, rg, a.iter, sweep, 2) ^ (uint32_t)v);
+    // exact int64 score; with int32 totals 2M < 2^31, so 32x32->64 products suffice
+    auto score = [&](int32_t val, TT t) -> long long {
+        if constexpr (sizeof(TT) == 4)
+            return (long long)val * (int32_t)a.M2 - (long long)(int32_t)kv * (int32_t)t;
+        else
+            return (long long)val * a.M2 - kv * (long long)t;
+    };
+    auto consider = [&](int32_t key, long long sc) {
+        const unsigned long long k2 = ((unsigned long long)hash32(tvh ^ (uint32_t)key) << 32) | (uint32_t)~key;
+        if (sc > best_s || (sc == best_s && k2 > best_k)) { best_s = sc; best_k = k2; }
+    };
+    auto tile_best = [&]() {
+#pragma unroll
+        for (int off = LT / 2; off > 0; off >>= 1) {
+            const long long os = __shfl_xor(best_s, off, LT);
+            const unsigned long long ok2 = __shfl_xor(best_k, off, LT);
+            if (os > best_s || (os == best_s && ok2 > best_k)) { best_s = os; best_k = ok2; }
+        }
+    };
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         if (slot[q] < 0) continue;
-        const int32_t key = cq[q];
-        const int32_t val = vals[slot[q]];
-        ++ncand;
-        if (key == own) kown = (TT)val;
-        long long sc;
         if (LOUV) {
-            if (key == own) continue;
-            sc = (long long)val * a.M2 - kv * (long long)tq[q];
+            if (cq[q] == own || vq[q] != vm) continue;
+            ++ncand;
+            consider(cq[q], score(vq[q], tq[q]));
         } else {
-            sc = val;
+            ++ncand;
+            consider(cq[q], vq[q]);
         }
-        const unsigned long long k2 = ((unsigned long long)hash32(tvh ^ (uint32_t)key) << 32) | (uint32_t)~key;
-        if (sc > best_s || (sc == best_s && k2 > best_k)) { best_s = sc; best_k = k2; }
+    }
+    tile_best();
+    if (LOUV) {
+        bool need = false;
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+            need |= slot[q] >= 0 && cq[q] != own && vq[q] < vm && (long long)vq[q] * a.M2 >= best_s;
+        if (__any(need)) {        // wave-uniform
+#pragma unroll
+            for (int q = 0; q < PER; ++q)
+                tq[q] = (slot[q] >= 0 && cq[q] != own && vq[q] < vm && (long long)vq[q] * a.M2 >= best_s)
+                            ? totr[cq[q]] : (TT)-1;
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                if (tq[q] < 0) continue;
+                ++ncand;
+                consider(cq[q], score(vq[q], tq[q]));
+            }
+            tile_best();
+        }
     }
 #pragma unroll
     for (int off = LT / 2; off > 0; off >>= 1) {
-        const long long os = __shfl_xor(best_s, off, LT);
-        const unsigned long long ok2 = __shfl_xor(best_k, off, LT);
-        if (os > best_s || (os == best_s && ok2 > best_k)) { best_s = os; best_k = ok2; }
         kown += __shfl_xor(kown, off, LT);
         ncand += __shfl_xor(ncand, off, LT);
     }
@@ -364,9 +448,12 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         __syncthreads();
         const int32_t* labr = a.lab + (int64_t)r * a.N;
         const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-        const bool push = a.track[2 * a.n_r + r] != 0;
-        for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB)
-            tbl_insert(keys, vals, slots - 1, push ? nlr[j] : labr[a.col[j]], LOUV ? a.cw[j] : 1);
+        const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
+        for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB) {
+            const int32_t lj = push ? nlr[j] : labr[a.col[j]];
+            if (trans) a.nlab[(int64_t)r * a.m2 + j] = lj;   // transition sweep (see k_decide_light)
+            tbl_insert(keys, vals, slots - 1, lj, LOUV ? a.cw[j] : 1);
+        }
         __syncthreads();
         const int32_t own = labr[v];
         const int64_t kv = a.kdeg[v];
@@ -490,7 +577,7 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int64_t ble
             }
             int32_t* nlr = a.nlab + (int64_t)r * a.m2;
             const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
-            const bool push = a.track[2 * a.n_r + r] != 0, trk = a.track[r] != 0;
+            const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
             if (push && trk) {
                 uint8_t* aff = a.aff + (int64_t)r * a.N;
                 for (int64_t j = rb + lane; j < re; j += TILE) {
@@ -534,8 +621,9 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
             if (f[2] * 4 < (unsigned long long)a.N) a.track[r] = 1;
         }
         // pull -> push once a sweep moved < N/4 vertices (push pays d writes per MOVE,
-        // pull d gathers per VISIT); the host refreshes nlab for switching replicas
-        if (!a.track[2 * a.n_r + r] && f[2] * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
+        // pull d gathers per VISIT), through one transition sweep that builds nlab
+        if (a.track[3 * a.n_r + r]) { a.track[3 * a.n_r + r] = 0; a.track[2 * a.n_r + r] = 1; }
+        else if (!a.track[2 * a.n_r + r] && f[2] * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
         if (a.active[r]) {
             bool stop;
             if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < 1e-7;
@@ -546,20 +634,6 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
     }
     __syncthreads();
     if (threadIdx.x == 0) { n_active_out[0] = cnt; *(unsigned long long*)(n_active_out + 2) = mv; }
-}
-
-// Entering push mode: nlab[r][j] = lab[r][col[j]] for the replicas flagged in
-// track[3n_r + r] (cleared here, push flag set).
-__global__ void k_nlab_refresh(int64_t m2, int64_t N, int n_r, const int32_t* col, const int32_t* lab,
-                               int32_t* nlab, int32_t* track) {
-    const int r = blockIdx.y;
-    if (!track[3 * n_r + r]) return;
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < m2) nlab[(int64_t)r * m2 + j] = lab[(int64_t)r * N + col[j]];
-}
-__global__ void k_push_on(int n_r, int32_t* track) {
-    for (int r = threadIdx.x; r < n_r; r += blockDim.x)
-        if (track[3 * n_r + r]) { track[3 * n_r + r] = 0; track[2 * n_r + r] = 1; }
 }
 
 template <typename TT>
@@ -696,6 +770,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
+    a.dbg = getenv("FC_DBG") ? atoi(getenv("FC_DBG")) : 0;
     a.aff = aff; a.list = nullptr; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
 
     int n_act = (g.M2 > 0) ? rcount : 0;
@@ -706,11 +781,6 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         c.acc.cd_sweeps += n_act;
         c.prof.cd_sweeps += n_act;
         a.list = nullptr;
-        if (any_switch && m2 > 0) {   // replicas entering push mode: build their nlab copies
-            k_nlab_refresh<<<dim3(nblk(m2), rcount), TB, 0, c.stream>>>(m2, N, rcount, g.col.as<int32_t>(), lab, nlab,
-                                                                       track);
-            k_push_on<<<1, TB, 0, c.stream>>>(rcount, track);
-        }
         if (c.prune && sweep > 0) {
             // visit lists of this sweep: vertices whose neighbour moved in the previous sweep
             k_build_lists<<<(unsigned)(B * rcount), TB, 0, c.stream>>>(a, sweep, PN, list, lcnt);
@@ -746,7 +816,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         FC_HIP(hipMemcpyAsync(h_tr.data(), track, 16 * (size_t)rcount, hipMemcpyDeviceToHost, c.stream));
         sync(c);
         n_act = ((int32_t*)c.hpin)[0];
-        // next sweep: replicas entering push mode; whether any replica pushes or tracks
+        // next sweep: any replica in its transition sweep; whether any replica pushes or tracks
         any_switch = rows = false;
         for (int r = 0; r < rcount; ++r) {
             any_switch |= h_tr[3 * (size_t)rcount + r] != 0;
@@ -774,7 +844,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     for (int r = 0; r < rcount; ++r) { c.hpin[0] += sa[4 * r]; c.hpin[1] += sa[4 * r + 1]; c.hpin[2] += sa[4 * r + 2]; }
     // algorithmic bytes of the light decide kernel: per vertex rowptr 16 + kdeg 8 + own
     // label 4 + own tot (4|8) + decision 4; per adjacency entry neighbour label 4 +
-    // weight 4; per distinct candidate community its tot (4|8) (louvain).  LPA: no
+    // weight 4; per Sigma gathered (candidates of maximal val) its tot (4|8) (louvain).  LPA: no
     // kdeg/tot/weights.
     const int64_t tsz = tot32 ? 4 : 8;
     const int64_t db = louv ? c.hpin[0] * (32 + tsz) + c.hpin[1] * 8 + c.hpin[2] * tsz
