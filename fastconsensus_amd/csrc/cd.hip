@@ -31,6 +31,11 @@ namespace fc {
 template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
 
 static constexpr int TB = 256;
+// Sweep order: vertices, or chunks of CHUNK consecutive vertices (chunk = 0 or CHUNK,
+// FC_OPT_CHUNK), in a random order; position p of vertex v is the inverse permutation
+// (k_list_build).  Positions fit 32 bits since N < 2^31.
+static constexpr int CHUNK = 16;
+
 static constexpr int TILE = 16;         // lanes per decision in k_apply's row scatter
 static constexpr int TILES = TB / TILE;
 static constexpr int LT = 8;            // lanes per vertex in k_decide_light
@@ -53,6 +58,7 @@ static inline unsigned nblk(int64_t n, int tb = TB) {
 struct CDArgs {
     int64_t N;
     int64_t S;          // bucket size (positions per bucket)
+    int64_t PN;         // positions per sweep (N, or N rounded up to whole chunks)
     int chunk;          // 0: vertex-level random order; else order over chunks of `chunk` vertices
     uint32_t perm_n;    // permutation domain: N, or the number of chunks
     int n_r, rbase;
@@ -82,7 +88,9 @@ struct CDArgs {
     int prune;
     const int32_t* list;         // [B][n_r][S] vertices to visit (bucket order), or nullptr = every position
     const int32_t* lcnt;         // [B][n_r] list lengths
-    const int32_t* blk_off;      // [B][n_r+1] light-kernel block offsets per replica
+    const int32_t* blk_off;      // [B][n_r+1] light-kernel item offsets per replica
+    const int32_t* itemrep;      // [B][wmax] replica of each light-kernel item
+    int64_t wmax;                // items per bucket, upper bound: n_r * ceil(S / LNT)
     int32_t* heavy;              // (r, dec index, position) triples
     int32_t* heavy_cnt;
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
@@ -91,18 +99,19 @@ struct CDArgs {
     int dbg;                     // FC_DBG ablation bits (timing experiments only; results become wrong)
 };
 
-__device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
-    return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
-}
-
-// Vertex visited at sweep position p, or -1 for a padding slot of the last chunk
-// (chunk is 0 or CHUNK, FC_OPT_CHUNK; positions fit 32 bits since N < 2^31).
-static constexpr int CHUNK = 16;
+// Vertex at sweep position p, or -1 for a padding slot of the last chunk.
 __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, int64_t p) {
     const uint32_t p32 = (uint32_t)p;
     if (!a.chunk) return (int32_t)perm_apply(P, p32);
     const uint32_t v = perm_apply(P, p32 / CHUNK) * CHUNK + (p32 % CHUNK);
     return v < (uint32_t)a.N ? (int32_t)v : -1;
+}
+// Replica r's sweep visits every position (no pruning filter yet): its "list" is implicit,
+// entry di of bucket k = position k*S + di.
+__device__ __forceinline__ bool rep_full(const CDArgs& a, int r) { return !(a.prune && a.track[a.n_r + r]); }
+
+__device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
+    return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
 }
 
 // Block -> (replica, chunk) with all chunks of a replica on as few XCDs as possible
@@ -173,45 +182,41 @@ __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t 
 // fetched first, alongside the row; then every lane issues ALL of its (<= PER) neighbour
 // gathers before it inserts them into the tile's LDS hash table; the lane that creates a
 // slot owns it and evaluates that candidate community (its Sigma gather batched likewise).
+//
+// Work: the bucket's visit lists of all replicas, cut into items of NT consecutive list
+// entries of one replica (item offsets per replica in blk_off, built on the device).  The
+// grid is fixed; block b takes a contiguous run of items (XCD-contiguous block order, so a
+// replica's items stay on few XCDs), so no host round trip sizes the launch.
 template <bool LOUV, typename TT, int LT>
-__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep, int64_t blen,
-                                                      int64_t chunks) {
+__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
     constexpr int NT = TB / LT;                 // tiles (vertices) per block
     constexpr int PER = LIGHT_MAX_DEG / LT;     // neighbours per lane
     __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
     __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
     __shared__ unsigned long long s_red[TB / 64][5];
     const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
-    int r;
-    int64_t chunk;
-    int64_t di;                // decision slot
-    bool in_range;
-    int32_t v = -1;
-    if (!a.list) {
-        xcd_remap(blockIdx.x, (int64_t)gridDim.x, chunks, &r, &chunk);
-        di = chunk * NT + tile;
-        in_range = di < blen;
-    } else {
-        int rr;
-        int64_t w;
-        xcd_remap(blockIdx.x, (int64_t)gridDim.x, (int64_t)gridDim.x, &rr, &w);
-        const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
-        int lo = 0, hi = a.n_r;            // last replica with bo[r] <= w (uniform search)
-        while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (bo[mid] <= w) lo = mid; else hi = mid; }
-        r = lo;
-        di = (w - bo[r]) * NT + tile;
-        const int64_t seg = ((int64_t)bucket * a.n_r + r);
-        in_range = di < a.lcnt[seg];
-        if (in_range) v = a.list[seg * a.S + di];   // lists hold vertex ids
-    }
+    const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
+    const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
+    // one item per block; XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the
+    // contiguous items [x*q, (x+1)*q), so a replica's items share an L2
+    const int64_t q = (W + 7) / 8, j = blockIdx.x >> 3;
+    const int64_t w = (blockIdx.x & 7) * q + j;
+    if (j >= q || w >= W) return;
+    // (readfirstlane: values loaded from global memory are not known to be uniform, and a
+    // vector r would move the per-replica arithmetic -- permutation keys, addresses -- to VALU)
+    const int r = __builtin_amdgcn_readfirstlane(a.itemrep[(int64_t)bucket * a.wmax + w]);
+    const int64_t seg = ((int64_t)bucket * a.n_r + r);
+    const int64_t di = (w - __builtin_amdgcn_readfirstlane(bo[r])) * NT + tile;   // decision slot
+    const bool in_range = di < __builtin_amdgcn_readfirstlane(a.lcnt[seg]);
     const int rg = a.rbase + r;
-    const bool rep_on = r < a.n_r && a.active[r];
-    bool valid = rep_on && in_range;
-    if (valid && !a.list) {
-        const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
-        v = pos_vertex(a, P, bucket * a.S + di);
-        valid = v >= 0;
+    int32_t v = -1;
+    if (in_range) {
+        if (rep_full(a, r)) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
+                                           bucket * a.S + di);
+        else v = a.list[seg * a.S + di];   // lists hold vertex ids
     }
+    const bool rep_on = a.active[r] != 0;
+    const bool valid = rep_on && in_range && v >= 0;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
     int64_t rb = 0, d = 0;
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         }
     }
     if (lane == 0) {
-        if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = make_int2(dcs, v);   // heavy: rewritten later
+        if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = make_int2(v >= 0 ? dcs : -1, v);   // heavy: rewritten later
         if (heavy) {
             const int q = atomicAdd(a.heavy_cnt, 1);
             a.heavy[3 * q] = r;
@@ -504,110 +509,79 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     }
 }
 
-// Apply a bucket's decisions, label + community totals only (no replica pushes or
-// tracks this sweep): one thread per decision slot.
+// Apply a bucket's decisions (fixed grid: blockIdx.y = replica, blocks stride over the
+// replica's list).  Label + community totals only (the replica neither pushes nor tracks
+// this sweep): one thread per decision slot.  Otherwise one 16-lane tile per slot: lane 0
+// updates the label and the totals, the tile scatters the new label into the reverse
+// adjacency entries (nlab) and, while tracking, flags the neighbours for the next sweep.
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_apply_lab(CDArgs a, int bucket, int64_t blen) {
-    const int r = blockIdx.y;
-    const int64_t di = (int64_t)blockIdx.x * TB + threadIdx.x;
-    const int64_t seg = (int64_t)bucket * a.n_r + r;
-    const bool in_range = a.list ? di < a.lcnt[seg] : di < blen;
-    int moved = 0;
-    if (in_range && a.active[r]) {
-        const int2 dv = a.dec[(int64_t)r * a.S + di];
-        if (dv.x >= 0) {
-            int32_t* l = a.lab + (int64_t)r * a.N + dv.y;
-            const int32_t old = *l;
-            *l = dv.x;
-            if (LOUV) {
-                TT* tot = (TT*)a.tot + (int64_t)r * a.N;
-                const TT kv = (TT)a.kdeg[dv.y];
-                if constexpr (sizeof(TT) == 8) {
-                    atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
-                    atomicAdd((unsigned long long*)&tot[dv.x], (unsigned long long)kv);
-                } else {
-                    atomicAdd((int*)&tot[old], -(int)kv);
-                    atomicAdd((int*)&tot[dv.x], (int)kv);
-                }
-            }
-            moved = 1;
+__device__ __forceinline__ void apply_move(const CDArgs& a, int r, int32_t d, int32_t v) {
+    int32_t* l = a.lab + (int64_t)r * a.N + v;
+    const int32_t old = *l;
+    *l = d;
+    if (LOUV) {
+        TT* tot = (TT*)a.tot + (int64_t)r * a.N;
+        const TT kv = (TT)a.kdeg[v];
+        if constexpr (sizeof(TT) == 8) {
+            atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
+            atomicAdd((unsigned long long*)&tot[d], (unsigned long long)kv);
+        } else {
+            atomicAdd((int*)&tot[old], -(int)kv);
+            atomicAdd((int*)&tot[d], (int)kv);
         }
     }
-    const unsigned long long b = __ballot(moved);
-    __shared__ unsigned long long s_mv;
-    if (threadIdx.x == 0) s_mv = 0;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&s_mv, (unsigned long long)__popcll(b));
-    __syncthreads();
-    if (threadIdx.x == 0 && s_mv) atomicAdd(red_slot(a, r, 2), s_mv);
 }
-
-// Same, for sweeps in which some replica pushes labels or tracks moves: one 16-lane tile
-// per decision slot; lane 0 updates the label and the community totals, the tile scatters
-// the new label into the reverse adjacency entries (nlab) and, while tracking, flags the
-// neighbours for the next sweep.
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket, int64_t blen) {
+__global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
     const int r = blockIdx.y;
-    const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
-    const int64_t di = (int64_t)blockIdx.x * TILES + tile;
-    int moved = 0;
+    if (!a.active[r]) return;
     const int64_t seg = (int64_t)bucket * a.n_r + r;
-    const bool in_range = a.list ? di < a.lcnt[seg] : di < blen;
-    if (in_range && a.active[r]) {
-        const int2 dv = a.dec[(int64_t)r * a.S + di];
-        const int32_t d = dv.x, v = dv.y;
-        if (d >= 0) {
-            if (lane == 0) {
-                int32_t* l = a.lab + (int64_t)r * a.N + v;
-                const int32_t old = *l;
-                *l = d;
-                if (LOUV) {
-                    TT* tot = (TT*)a.tot + (int64_t)r * a.N;
-                    const TT kv = (TT)a.kdeg[v];
-                    if constexpr (sizeof(TT) == 8) {
-                        atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
-                        atomicAdd((unsigned long long*)&tot[d], (unsigned long long)kv);
-                    } else {
-                        atomicAdd((int*)&tot[old], -(int)kv);
-                        atomicAdd((int*)&tot[d], (int)kv);
-                    }
-                }
-                moved = 1;
-            }
-            int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+    const int64_t len = a.lcnt[seg];
+    const int2* decr = a.dec + (int64_t)r * a.S;
+    const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
+    int moved = 0;
+    if (!push && !trk) {
+        for (int64_t di = (int64_t)blockIdx.x * TB + threadIdx.x; di < len; di += (int64_t)gridDim.x * TB) {
+            const int2 dv = decr[di];
+            if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv.x, dv.y); ++moved; }
+        }
+    } else {
+        const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
+        int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+        uint8_t* aff = a.aff + (int64_t)r * a.N;
+        for (int64_t di = (int64_t)blockIdx.x * TILES + tile; di < len; di += (int64_t)gridDim.x * TILES) {
+            const int2 dv = decr[di];
+            const int32_t d = dv.x, v = dv.y;
+            if (d < 0) continue;
+            if (lane == 0) { apply_move<LOUV, TT>(a, r, d, v); ++moved; }
             const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
-            const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
             if (push && trk) {
-                uint8_t* aff = a.aff + (int64_t)r * a.N;
                 for (int64_t j = rb + lane; j < re; j += TILE) {
                     nlr[a.rev[j]] = d;     // neighbours now see v's new community
                     aff[a.col[j]] = 1;     // ... and are revisited next sweep (pruning)
                 }
             } else if (push) {
                 for (int64_t j = rb + lane; j < re; j += TILE) nlr[a.rev[j]] = d;
-            } else if (trk) {
-                uint8_t* aff = a.aff + (int64_t)r * a.N;
+            } else {
                 for (int64_t j = rb + lane; j < re; j += TILE) aff[a.col[j]] = 1;
             }
         }
     }
-    const unsigned long long b = __ballot(moved);
-    __shared__ unsigned long long s_mv;
+    __shared__ int s_mv;
     if (threadIdx.x == 0) s_mv = 0;
     __syncthreads();
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&s_mv, (unsigned long long)__popcll(b));
+    if (moved) atomicAdd(&s_mv, moved);
     __syncthreads();
-    if (threadIdx.x == 0 && s_mv) atomicAdd(red_slot(a, r, 2), s_mv);
+    if (threadIdx.x == 0 && s_mv) atomicAdd(red_slot(a, r, 2), (unsigned long long)s_mv);
 }
 
 // End of sweep: python-louvain stops a level when the pass gained < 1e-7 modularity or
 // moved nothing; igraph LPA stops when no visited vertex was unstable.
 template <bool LOUV>
 __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
-    __shared__ int cnt;
+    __shared__ int cnt, cnt0;
     __shared__ unsigned long long mv;
-    if (threadIdx.x == 0) { cnt = 0; mv = 0; }
+    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; mv = 0; }
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -625,6 +599,7 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         if (a.track[3 * a.n_r + r]) { a.track[3 * a.n_r + r] = 0; a.track[2 * a.n_r + r] = 1; }
         else if (!a.track[2 * a.n_r + r] && f[2] * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
         if (a.active[r]) {
+            atomicAdd(&cnt0, 1);
             bool stop;
             if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < 1e-7;
             else stop = f[1] == 0;
@@ -633,7 +608,12 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) { n_active_out[0] = cnt; *(unsigned long long*)(n_active_out + 2) = mv; }
+    // n_active_out: [0] active after, [2..3] u64 moves, [4..5] u64 replica-sweeps so far
+    if (threadIdx.x == 0) {
+        n_active_out[0] = cnt;
+        *(unsigned long long*)(n_active_out + 2) = mv;
+        *(unsigned long long*)(n_active_out + 4) += (unsigned long long)cnt0;
+    }
 }
 
 template <typename TT>
@@ -645,63 +625,85 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
     if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
 }
 
-// Pruned sweep: per (bucket, replica) the vertices flagged affected, in position order
-// (deterministic); flags are read and cleared here, moves of this sweep
-// set them again for the next one.  One block per (bucket, replica) segment.
-__global__ __launch_bounds__(256) void k_build_lists(CDArgs a, int sweep, int64_t PN, int32_t* list, int32_t* lcnt) {
-    const int k = blockIdx.x / a.n_r, r = blockIdx.x % a.n_r;
-    const int64_t seg = blockIdx.x;
-    __shared__ int s_w[TB / 64];
-    if (!a.active[r]) {
-        if (threadIdx.x == 0) lcnt[seg] = 0;
+// Visit lists of one sweep, per replica: every vertex (sweeps before tracking starts, or
+// pruning off), or those flagged affected by the previous sweep's moves -- bucketed by the
+// vertex's position in this sweep's random order (inverse permutation).  The order inside
+// a bucket is immaterial: a bucket's decisions all read the state the earlier buckets
+// left, and its moves commute (distinct vertices, integer atomics), so entries land in
+// any order.  Flags are read and cleared here.  Cost: one pass over aff plus work per
+// listed vertex (no per-position scan).  Dynamic LDS: 2 * B ints.
+static constexpr int LB_PER = 16;        // vertices per thread in k_list_build
+__global__ __launch_bounds__(256) void k_list_build(CDArgs a, int sweep, int B, int32_t* list, int32_t* lcnt) {
+    extern __shared__ int s_lb[];
+    int* s_cnt = s_lb;
+    int* s_base = s_lb + B;
+    const int r = blockIdx.y;
+    if (!a.active[r]) return;
+    for (int k = threadIdx.x; k < B; k += TB) s_cnt[k] = 0;
+    __syncthreads();
+    if (rep_full(a, r)) {     // every position: implicit list (no flag can be set before tracking starts)
+        if (blockIdx.x == 0)
+            for (int k = threadIdx.x; k < B; k += TB)
+                lcnt[(int64_t)k * a.n_r + r] = (int32_t)min(a.S, a.PN - (int64_t)k * a.S);
         return;
     }
-    const int64_t blen = min((int64_t)a.S, PN - (int64_t)k * a.S);
     const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
     uint8_t* aff = a.aff + (int64_t)r * a.N;
-    const bool filter = a.track[a.n_r + r] != 0;   // moves were tracked during the previous sweep
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int base = 0;
-    for (int64_t i0 = 0; i0 < blen; i0 += TB) {
-        const int64_t i = i0 + threadIdx.x;
-        bool f = false;
-        int32_t v = -1;
-        if (i < blen) {
-            v = pos_vertex(a, P, (int64_t)k * a.S + i);
-            if (v >= 0) { f = filter ? aff[v] != 0 : true; aff[v] = 0; }
-        }
-        const unsigned long long b = __ballot(f);
-        if (lane == 0) s_w[wave] = __popcll(b);
-        __syncthreads();
-        int off = base;
-        for (int w = 0; w < wave; ++w) off += s_w[w];
-        int tot = 0;
-        for (int w = 0; w < TB / 64; ++w) tot += s_w[w];
-        if (f) list[seg * a.S + off + __popcll(b & ((1ull << lane) - 1ull))] = v;
-        base += tot;
-        __syncthreads();
+    int bk[LB_PER], loc[LB_PER];
+    const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < LB_PER; ++i) {
+        const int64_t v = v0 + (int64_t)i * TB;
+        bk[i] = -1;
+        if (v >= a.N) continue;
+        if (!aff[v]) continue;    // filter: vertices whose neighbour moved last sweep
+        aff[v] = 0;
+        uint32_t pos;
+        if (a.chunk) pos = perm_invert(P, (uint32_t)v / CHUNK) * CHUNK + (uint32_t)v % CHUNK;
+        else pos = perm_invert(P, (uint32_t)v);
+        bk[i] = (int)(pos / (uint32_t)a.S);
+        loc[i] = atomicAdd(&s_cnt[bk[i]], 1);
     }
-    if (threadIdx.x == 0) lcnt[seg] = base;
+    __syncthreads();
+    for (int k = threadIdx.x; k < B; k += TB)
+        s_base[k] = s_cnt[k] ? atomicAdd(&lcnt[(int64_t)k * a.n_r + r], s_cnt[k]) : 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < LB_PER; ++i)
+        if (bk[i] >= 0) list[((int64_t)bk[i] * a.n_r + r) * a.S + s_base[bk[i]] + loc[i]] = (int32_t)(v0 + (int64_t)i * TB);
+}
+// Per bucket: light-decide item offsets per replica (items of LNT list entries) and the
+// replica of every item.
+__global__ __launch_bounds__(256) void k_list_offsets(int n_r, int64_t wmax, const int32_t* lcnt, int32_t* blk_off,
+                                                      int32_t* itemrep) {
+    const int k = blockIdx.x;
+    int32_t* bo = blk_off + (int64_t)k * (n_r + 1);
+    if (threadIdx.x == 0) {
+        int32_t acc = 0;
+        for (int r = 0; r < n_r; ++r) {
+            bo[r] = acc;
+            acc += (lcnt[(int64_t)k * n_r + r] + LNT - 1) / LNT;
+        }
+        bo[n_r] = acc;
+    }
+    __syncthreads();
+    for (int r = 0; r < n_r; ++r)
+        for (int32_t w = bo[r] + threadIdx.x; w < bo[r + 1]; w += blockDim.x) itemrep[(int64_t)k * wmax + w] = r;
 }
 
 // One bucket: decide (light + heavy rows) against the state left by earlier buckets, apply.
-// Full mode: grid = all bucket positions of every replica.  List mode: light blocks =
-// light_blocks (sum over replicas of ceil(list length / LNT)), apply covers max_len.
-// rows: some replica pushes labels or tracks moves this sweep (row-scatter apply).
+// Every grid is fixed and every size is read on the device, so a sweep never waits on
+// the host.
 template <bool LOUV, typename TT>
-static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, int64_t blen, bool any_heavy,
-                      int64_t light_blocks, int64_t max_len, bool rows) {
-    const int64_t chunks = (blen + LNT - 1) / LNT;
-    const int64_t nb = a.list ? light_blocks : chunks * a.n_r;
-    const int64_t alen = a.list ? max_len : blen;
-    if (nb <= 0) return;
+static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy) {
     if (any_heavy) FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     const int ev = timer_begin(c);
-    k_decide_light<LOUV, TT, LT><<<(unsigned)nb, TB, 0, c.stream>>>(a, k, sweep, blen, chunks);
+    // one item per block; grid = the bound wmax = n_r * ceil(S / LNT) (blocks past the
+    // bucket's item count return at once)
+    k_decide_light<LOUV, TT, LT><<<(unsigned)((a.wmax + 7) & ~int64_t(7)), TB, 0, c.stream>>>(a, k, sweep);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
-    if (rows) k_apply<LOUV, TT><<<dim3((unsigned)((alen + TILES - 1) / TILES), a.n_r), TB, 0, c.stream>>>(a, k, blen);
-    else k_apply_lab<LOUV, TT><<<dim3((unsigned)((alen + TB - 1) / TB), a.n_r), TB, 0, c.stream>>>(a, k, blen);
+    k_apply<LOUV, TT><<<dim3((unsigned)c.apply_blocks, a.n_r), TB, 0, c.stream>>>(a, k);
 }
 
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
@@ -713,11 +715,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     Graph& g = c.g;
     c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
     c.labT_valid = false;
-    // sweep positions: vertices in a random order, or whole chunks of `chunk` consecutive
-    // vertices in a random chunk order (coalesced per-vertex accesses inside a block)
+    // sweep positions: vertices in a random order, or whole chunks of CHUNK consecutive
+    // vertices in a random chunk order (coalesced per-vertex accesses)
     const int CH = c.chunk;
     const int64_t NC = CH ? (N + CH - 1) / CH : N;
-    const int64_t PN = CH ? NC * CH : N;
     const int B = (int)std::min<int64_t>(c.buckets, NC);
     const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
@@ -732,18 +733,18 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int32_t* active = (int32_t*)rs;
     unsigned long long* red = (unsigned long long*)(rs + (((size_t)rcount * 4 + 255) & ~size_t(255)));
     unsigned long long* sacc = red + (size_t)rcount * NSH * RF;
-    int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);   // [0] active, [2..3] u64 moves
-    const size_t zero_bytes = (char*)(n_active + 4) - (char*)red;
+    int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);   // see k_sweep_end
+    const size_t zero_bytes = (char*)(n_active + 8) - (char*)red;
     int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * S + 3);
     uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
-    FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));   // sweep 0 visits everyone
+    FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));
     int32_t* track = ensure<int32_t>(c.track, 4 * (size_t)rcount);
     FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
-    int32_t* list = c.prune ? ensure<int32_t>(c.vlist, (size_t)B * rcount * S) : nullptr;
-    int32_t* lcnt = c.prune ? ensure<int32_t>(c.vcnt, (size_t)B * rcount + (size_t)B * (rcount + 1)) : nullptr;
-    int32_t* blk_off = c.prune ? lcnt + (size_t)B * rcount : nullptr;
-    std::vector<int32_t> h_cnt(c.prune ? (size_t)B * rcount : 0), h_off(c.prune ? (size_t)B * (rcount + 1) : 0);
-    std::vector<int64_t> light_blocks(B, 0), max_len(B, 0);
+    int32_t* list = ensure<int32_t>(c.vlist, (size_t)B * rcount * S);
+    int32_t* lcnt = ensure<int32_t>(c.vcnt, (size_t)B * rcount + (size_t)B * (rcount + 1));
+    int32_t* blk_off = lcnt + (size_t)B * rcount;
+    const int64_t wmax = (int64_t)rcount * ((S + LNT - 1) / LNT);
+    int32_t* itemrep = ensure<int32_t>(c.itemrep, (size_t)B * wmax);
     int32_t* heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
     int64_t heavy_slots = 1;
     while (heavy_slots < 2 * (int64_t)g.max_deg) heavy_slots <<= 1;
@@ -763,7 +764,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                "edge weights too large for exact int64 modularity gains");
 
     CDArgs a;
-    a.N = N; a.S = S; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
+    a.N = N; a.S = S; a.PN = CH ? ((N + CH - 1) / CH) * CH : N; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
@@ -771,58 +772,37 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
     a.dbg = getenv("FC_DBG") ? atoi(getenv("FC_DBG")) : 0;
-    a.aff = aff; a.list = nullptr; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
+    a.aff = aff; a.list = list; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
+    a.itemrep = itemrep; a.wmax = wmax;
 
-    int n_act = (g.M2 > 0) ? rcount : 0;
+    // The host enqueues sweeps ahead and reads the active count of sweep s - LAG (pinned
+    // ring c.hpin[8..15], one event per slot): no per-sweep round trip.  Sweeps enqueued
+    // after every replica stopped find no active replica and do nothing.
+    const int LAG = c.trace ? 0 : 2;
+    if (c.sweep_ev.empty()) {
+        c.sweep_ev.resize(8);
+        for (auto& e : c.sweep_ev) FC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    int32_t* ring = (int32_t*)(c.hpin + 8);
+    const bool hv = g.max_deg > LIGHT_MAX_DEG;
+    const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
     int sweep = 0;
-    bool any_switch = false, rows = false;
-    std::vector<int32_t> h_tr(4 * (size_t)rcount);
-    for (; sweep < c.max_sweeps && n_act > 0; ++sweep) {
-        c.acc.cd_sweeps += n_act;
-        c.prof.cd_sweeps += n_act;
-        a.list = nullptr;
-        if (c.prune && sweep > 0) {
-            // visit lists of this sweep: vertices whose neighbour moved in the previous sweep
-            k_build_lists<<<(unsigned)(B * rcount), TB, 0, c.stream>>>(a, sweep, PN, list, lcnt);
-            FC_HIP(hipMemcpyAsync(h_cnt.data(), lcnt, 4 * h_cnt.size(), hipMemcpyDeviceToHost, c.stream));
-            sync(c);
-            for (int k = 0; k < B; ++k) {
-                int64_t acc = 0, mx = 0;
-                for (int r = 0; r < rcount; ++r) {
-                    const int64_t n = h_cnt[(size_t)k * rcount + r];
-                    h_off[(size_t)k * (rcount + 1) + r] = (int32_t)acc;
-                    acc += (n + LNT - 1) / LNT;
-                    mx = std::max(mx, n);
-                }
-                h_off[(size_t)k * (rcount + 1) + rcount] = (int32_t)acc;
-                light_blocks[k] = acc;
-                max_len[k] = mx;
-            }
-            FC_HIP(hipMemcpyAsync(blk_off, h_off.data(), 4 * h_off.size(), hipMemcpyHostToDevice, c.stream));
-            a.list = list;
-        }
+    for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
+        FC_HIP(hipMemsetAsync(lcnt, 0, sizeof(int32_t) * (size_t)B * rcount, c.stream));
+        k_list_build<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, B, list, lcnt);
+        k_list_offsets<<<B, TB, 0, c.stream>>>(rcount, a.wmax, lcnt, blk_off, itemrep);
         for (int k = 0; k < B; ++k) {
-            const int64_t blen = std::min<int64_t>(S, PN - (int64_t)k * S);
-            if (blen <= 0) continue;
-            const bool hv = g.max_deg > LIGHT_MAX_DEG;
-            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k], rows);
-            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k], rows);
-            else sub_round<true, int64_t>(c, a, k, sweep, blen, hv, light_blocks[k], max_len[k], rows);
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv);
+            else sub_round<true, int64_t>(c, a, k, sweep, hv);
         }
-        if (a.list) sync(c);   // h_off (pageable) must outlive its async upload
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
-        FC_HIP(hipMemcpyAsync(c.hpin, n_active, 16, hipMemcpyDeviceToHost, c.stream));
-        FC_HIP(hipMemcpyAsync(h_tr.data(), track, 16 * (size_t)rcount, hipMemcpyDeviceToHost, c.stream));
-        sync(c);
-        n_act = ((int32_t*)c.hpin)[0];
-        // next sweep: any replica in its transition sweep; whether any replica pushes or tracks
-        any_switch = rows = false;
-        for (int r = 0; r < rcount; ++r) {
-            any_switch |= h_tr[3 * (size_t)rcount + r] != 0;
-            rows |= h_tr[r] != 0 || h_tr[2 * (size_t)rcount + r] != 0 || h_tr[3 * (size_t)rcount + r] != 0;
-        }
+        const int slot = sweep & 7;
+        FC_HIP(hipMemcpyAsync(ring + 2 * slot, n_active, 8, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipEventRecord(c.sweep_ev[slot], c.stream));
         if (c.trace) {
+            sync(c);
             std::vector<unsigned long long> sa(4 * (size_t)rcount);
             FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
             sync(c);
@@ -830,25 +810,33 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             for (int r = 0; r < rcount; ++r) vv += sa[4 * r];
             static auto t_last = std::chrono::steady_clock::now();
             const auto t_now = std::chrono::steady_clock::now();
-            fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu moves=%llu push=%d dt_us=%.0f\n",
-                    iteration, sweep, n_act, vv, (unsigned long long)c.hpin[1], (int)any_switch,
+            fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu dt_us=%.0f\n",
+                    iteration, sweep, ring[2 * slot], vv,
                     1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
             t_last = t_now;
         }
+        if (sweep >= LAG) {
+            const int chk = (sweep - LAG) & 7;
+            FC_HIP(hipEventSynchronize(c.sweep_ev[chk]));
+            if (ring[2 * chk] == 0) { ++sweep; break; }
+        }
     }
-    // light-kernel traffic counters for the roofline model
-    std::vector<unsigned long long> sa(4 * (size_t)rcount);
+    // replica-sweeps and light-kernel traffic counters for the roofline model
+    std::vector<unsigned long long> sa(4 * (size_t)rcount + 4);
     FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
     sync(c);
+    const unsigned long long rep_sweeps = sa[4 * (size_t)rcount + 2];   // n_active[4..5]
+    c.acc.cd_sweeps += (int64_t)rep_sweeps;
+    c.prof.cd_sweeps += (int64_t)rep_sweeps;
     c.hpin[0] = c.hpin[1] = c.hpin[2] = 0;
     for (int r = 0; r < rcount; ++r) { c.hpin[0] += sa[4 * r]; c.hpin[1] += sa[4 * r + 1]; c.hpin[2] += sa[4 * r + 2]; }
     // algorithmic bytes of the light decide kernel: per vertex rowptr 16 + kdeg 8 + own
-    // label 4 + own tot (4|8) + decision 4; per adjacency entry neighbour label 4 +
-    // weight 4; per Sigma gathered (candidates of maximal val) its tot (4|8) (louvain).  LPA: no
-    // kdeg/tot/weights.
+    // label 4 + own tot (4|8) + decision 8 + list entry 4; per adjacency entry neighbour
+    // label 4 + weight 4; per Sigma gathered (candidates of maximal val) its tot (4|8)
+    // (louvain).  LPA: no kdeg/tot/weights.
     const int64_t tsz = tot32 ? 4 : 8;
-    const int64_t db = louv ? c.hpin[0] * (32 + tsz) + c.hpin[1] * 8 + c.hpin[2] * tsz
-                            : c.hpin[0] * 24 + c.hpin[1] * 4;
+    const int64_t db = louv ? c.hpin[0] * (40 + tsz) + c.hpin[1] * 8 + c.hpin[2] * tsz
+                            : c.hpin[0] * 32 + c.hpin[1] * 4;
     for (fc_stats* s : {&c.acc, &c.prof}) {
         s->cd_vertex_visits += c.hpin[0];
         s->cd_edge_visits += c.hpin[1];

@@ -121,6 +121,9 @@ struct Ctx {
     int buckets = 32, max_sweeps = 200, max_iters = 1000;
     int chunk = 16;                 // CD order granularity (0 = per vertex), FC_OPT_CHUNK
     int relabel = 1;                // FC_OPT_RELABEL (applies at the next fc_load_graph)
+    int64_t apply_blocks = getenv("FC_APPLY_BLOCKS") ? atoll(getenv("FC_APPLY_BLOCKS")) : 32;   // per replica
+    std::vector<hipEvent_t> sweep_ev;   // per-sweep completion ring (cd_run)
+    DevBuf itemrep;                 // CD: replica of each light-decide item, per bucket
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     bool trace = getenv("FC_TRACE") && *getenv("FC_TRACE") && *getenv("FC_TRACE") != '0';  // per-sweep stderr
     Timer timer;

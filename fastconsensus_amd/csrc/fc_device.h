@@ -60,6 +60,19 @@ FC_HD uint32_t perm_apply(const Perm& p, uint32_t x) {
     do { x = feistel_round(x, p); } while (x >= p.n);
     return x;
 }
+// Inverse: position of element y (rounds undone in reverse; cycle walking backwards).
+FC_HD uint32_t feistel_round_inv(uint32_t y, const Perm& p) {
+    uint32_t L = y >> p.hb, R = y & p.mask, t;
+    t = L; L = R ^ (hash32(L ^ p.k3) & p.mask); R = t;
+    t = L; L = R ^ (hash32(L ^ p.k2) & p.mask); R = t;
+    t = L; L = R ^ (hash32(L ^ p.k1) & p.mask); R = t;
+    t = L; L = R ^ (hash32(L ^ p.k0) & p.mask); R = t;
+    return (L << p.hb) | R;
+}
+FC_HD uint32_t perm_invert(const Perm& p, uint32_t y) {
+    do { y = feistel_round_inv(y, p); } while (y >= p.n);
+    return y;
+}
 
 // Philox4x32-10 (Salmon et al., SC'11): counter-based, so attempt t of iteration it draws
 // the same numbers on every rank.

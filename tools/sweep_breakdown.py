@@ -16,7 +16,7 @@ for r in rows:
         cur["_wall"] = (int(r["End_Timestamp"]) - t0) / 1e3
         t0 = int(r["End_Timestamp"])
         sweeps.append(cur); cur = defaultdict(float)
-keys = ["k_decide_light", "k_decide_heavy", "k_apply_lab", "k_apply", "k_build_lists", "__amd_rocclr_fillBufferAligned", "_wall"]
+keys = ["k_decide_light", "k_decide_heavy", "k_apply", "k_list_build", "k_list_offsets", "__amd_rocclr_fillBufferAligned", "_wall"]
 print("sweep " + " ".join("%10s" % k[-10:] for k in keys))
 for i, s in enumerate(sweeps[:int(sys.argv[2]) if len(sys.argv) > 2 else 40]):
     print("%5d " % i + " ".join("%10.0f" % s.get(k, 0) for k in keys))
