@@ -187,36 +187,20 @@ __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t 
 // entries of one replica (item offsets per replica in blk_off, built on the device).  The
 // grid is fixed; block b takes a contiguous run of items (XCD-contiguous block order, so a
 // replica's items stay on few XCDs), so no host round trip sizes the launch.
+// One vertex visit (LT lanes; every thread of the block calls it: it holds two block
+// barriers).  Louvain: move iff the best gain is > 0; LPA: the most frequent label.
+struct Visit {
+    int32_t dcs;               // target community, or -1
+    unsigned long long dq;     // predicted modularity gain (fixed point, Louvain)
+    int unst;                  // LPA: own label not dominant
+    int ncand;                 // Sigma gathers (Louvain) / candidates (LPA)
+    int64_t d;                 // degree
+    bool work, heavy;
+};
 template <bool LOUV, typename TT, int LT>
-__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
-    constexpr int NT = TB / LT;                 // tiles (vertices) per block
+__device__ __forceinline__ Visit decide_visit(const CDArgs& a, int r, int rg, int sweep, bool valid, int32_t v,
+                                              int32_t* keys, int32_t* vals, int lane) {
     constexpr int PER = LIGHT_MAX_DEG / LT;     // neighbours per lane
-    __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
-    __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
-    __shared__ unsigned long long s_red[TB / 64][5];
-    const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
-    const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
-    const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
-    // one item per block; XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the
-    // contiguous items [x*q, (x+1)*q), so a replica's items share an L2
-    const int64_t q = (W + 7) / 8, j = blockIdx.x >> 3;
-    const int64_t w = (blockIdx.x & 7) * q + j;
-    if (j >= q || w >= W) return;
-    // (readfirstlane: values loaded from global memory are not known to be uniform, and a
-    // vector r would move the per-replica arithmetic -- permutation keys, addresses -- to VALU)
-    const int r = __builtin_amdgcn_readfirstlane(a.itemrep[(int64_t)bucket * a.wmax + w]);
-    const int64_t seg = ((int64_t)bucket * a.n_r + r);
-    const int64_t di = (w - __builtin_amdgcn_readfirstlane(bo[r])) * NT + tile;   // decision slot
-    const bool in_range = di < __builtin_amdgcn_readfirstlane(a.lcnt[seg]);
-    const int rg = a.rbase + r;
-    int32_t v = -1;
-    if (in_range) {
-        if (rep_full(a, r)) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
-                                           bucket * a.S + di);
-        else v = a.list[seg * a.S + di];   // lists hold vertex ids
-    }
-    const bool rep_on = a.active[r] != 0;
-    const bool valid = rep_on && in_range && v >= 0;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
     int64_t rb = 0, d = 0;
@@ -256,8 +240,6 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         }
     }
     // ---- tile table: clear (16-byte stores), insert, owners evaluate
-    int32_t* keys = s_key + tile * HCAP;
-    int32_t* vals = s_val + tile * HCAP;
     {
         int4* k4 = reinterpret_cast<int4*>(keys);
         int4* v4 = reinterpret_cast<int4*>(vals);
@@ -390,6 +372,47 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
             dcs = best_c != own ? best_c : -1;
         }
     }
+    Visit out;
+    out.dcs = dcs; out.dq = dq; out.unst = unst; out.ncand = ncand; out.d = d; out.work = work; out.heavy = heavy;
+    return out;
+}
+
+template <bool LOUV, typename TT, int LT>
+__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
+    constexpr int NT = TB / LT;                 // tiles (vertices) per block
+    constexpr int PER = LIGHT_MAX_DEG / LT;     // neighbours per lane
+    __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
+    __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
+    __shared__ unsigned long long s_red[TB / 64][5];
+    const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
+    const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
+    const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
+    // one item per block; XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the
+    // contiguous items [x*q, (x+1)*q), so a replica's items share an L2
+    const int64_t q = (W + 7) / 8, j = blockIdx.x >> 3;
+    const int64_t w = (blockIdx.x & 7) * q + j;
+    if (j >= q || w >= W) return;
+    // (readfirstlane: values loaded from global memory are not known to be uniform, and a
+    // vector r would move the per-replica arithmetic -- permutation keys, addresses -- to VALU)
+    const int r = __builtin_amdgcn_readfirstlane(a.itemrep[(int64_t)bucket * a.wmax + w]);
+    const int64_t seg = ((int64_t)bucket * a.n_r + r);
+    const int64_t di = (w - __builtin_amdgcn_readfirstlane(bo[r])) * NT + tile;   // decision slot
+    const bool in_range = di < __builtin_amdgcn_readfirstlane(a.lcnt[seg]);
+    const int rg = a.rbase + r;
+    int32_t v = -1;
+    if (in_range) {
+        if (rep_full(a, r)) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
+                                           bucket * a.S + di);
+        else v = a.list[seg * a.S + di];   // lists hold vertex ids
+    }
+    const bool rep_on = a.active[r] != 0;
+    const bool valid = rep_on && in_range && v >= 0;
+    const Visit vis = decide_visit<LOUV, TT, LT>(a, r, rg, sweep, valid, v, s_key + tile * HCAP, s_val + tile * HCAP, lane);
+    const int32_t dcs = vis.dcs;
+    const unsigned long long dq = vis.dq;
+    const int unst = vis.unst, ncand = vis.ncand;
+    const int64_t d = vis.d;
+    const bool work = vis.work, heavy = vis.heavy;
     if (lane == 0) {
         if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = make_int2(v >= 0 ? dcs : -1, v);   // heavy: rewritten later
         if (heavy) {
@@ -421,91 +444,107 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     }
 }
 
-// Workgroup per high-degree vertex.  Table in LDS when it fits, else a global slice.
+// A high-degree vertex decided by a whole 256-thread block (every thread calls it).  Table
+// in LDS when it fits, else the block's global slice `scratch`.  Returns the decision on
+// thread 0 (dq / unstable through the pointers).
+struct HeavyShared {
+    int32_t key[HEAVY_LDS_SLOTS];
+    int32_t val[HEAVY_LDS_SLOTS];
+    long long s[TB];
+    uint32_t h[TB];
+    int32_t c[TB];
+    int have[TB];
+    long long kown[TB];
+};
+template <bool LOUV, typename TT>
+__device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, HeavyShared& sh, int32_t* scratch,
+                               unsigned long long* dq_out, int* unst_out) {
+    const int rg = a.rbase + r;
+    const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
+    const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
+    uint32_t slots = 1;
+    while (slots < 2 * (uint32_t)d) slots <<= 1;
+    int32_t* keys;
+    int32_t* vals;
+    if (slots <= HEAVY_LDS_SLOTS) { keys = sh.key; vals = sh.val; }
+    else {
+        slots = (uint32_t)a.heavy_slots;
+        keys = scratch;
+        vals = keys + slots;
+    }
+    for (uint32_t s = threadIdx.x; s < slots; s += TB) { keys[s] = -1; vals[s] = 0; }
+    __syncthreads();
+    const int32_t* labr = a.lab + (int64_t)r * a.N;
+    const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+    const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
+    for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB) {
+        const int32_t lj = push ? nlr[j] : labr[a.col[j]];
+        if (trans) a.nlab[(int64_t)r * a.m2 + j] = lj;   // transition sweep (see decide_visit)
+        tbl_insert(keys, vals, slots - 1, lj, LOUV ? a.cw[j] : 1);
+    }
+    __syncthreads();
+    const int32_t own = labr[v];
+    const int64_t kv = a.kdeg[v];
+    const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
+    long long best_s = LLONG_MIN, kown = 0;
+    uint32_t best_h = 0;
+    int32_t best_c = 0x7fffffff;
+    int have = 0;
+    for (uint32_t s = threadIdx.x; s < slots; s += TB) {
+        const int32_t key = keys[s];
+        if (key < 0) continue;
+        const int32_t val = vals[s];
+        if (key == own) kown = val;
+        long long sc;
+        if (LOUV) {
+            if (key == own) continue;
+            sc = (long long)val * a.M2 - kv * (long long)totr[key];
+        } else {
+            sc = val;
+        }
+        const uint32_t h = tie_hash(tbk, v, key);
+        if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
+    }
+    sh.s[threadIdx.x] = best_s; sh.h[threadIdx.x] = best_h; sh.c[threadIdx.x] = best_c;
+    sh.have[threadIdx.x] = have; sh.kown[threadIdx.x] = kown;
+    __syncthreads();
+    for (int o = TB / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            const int t2 = threadIdx.x + o;
+            if (sh.have[t2] && (!sh.have[threadIdx.x] ||
+                                better(sh.s[t2], sh.h[t2], sh.c[t2], sh.s[threadIdx.x], sh.h[threadIdx.x], sh.c[threadIdx.x]))) {
+                sh.s[threadIdx.x] = sh.s[t2]; sh.h[threadIdx.x] = sh.h[t2]; sh.c[threadIdx.x] = sh.c[t2];
+                sh.have[threadIdx.x] = 1;
+            }
+            sh.kown[threadIdx.x] += sh.kown[t2];
+        }
+        __syncthreads();
+    }
+    int32_t dcs = -1;
+    if (threadIdx.x == 0)
+        dcs = decide_final<LOUV, TT>(a, r, v, own, sh.s[0], sh.c[0], sh.kown[0], sh.have[0], dq_out, unst_out);
+    __syncthreads();
+    return dcs;
+}
+
+// Workgroup per high-degree vertex of the bucket (listed by k_decide_light).
 template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int sweep) {
-    __shared__ int32_t s_key[HEAVY_LDS_SLOTS];
-    __shared__ int32_t s_val[HEAVY_LDS_SLOTS];
-    __shared__ long long r_s[TB];
-    __shared__ uint32_t r_h[TB];
-    __shared__ int32_t r_c[TB];
-    __shared__ int r_have[TB];
-    __shared__ long long r_kown[TB];
+    __shared__ HeavyShared sh;
     const int cnt = *a.heavy_cnt;
     for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
         const int r = a.heavy[3 * item];
         const int64_t di = a.heavy[3 * item + 1];
         const int32_t v = a.heavy[3 * item + 2];
-        const int rg = a.rbase + r;
-        const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
-        const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
-        uint32_t slots = 1;
-        while (slots < 2 * (uint32_t)d) slots <<= 1;
-        int32_t* keys;
-        int32_t* vals;
-        if (slots <= HEAVY_LDS_SLOTS) { keys = s_key; vals = s_val; }
-        else {
-            slots = (uint32_t)a.heavy_slots;
-            keys = a.heavy_scratch + (int64_t)blockIdx.x * 2 * slots;
-            vals = keys + slots;
-        }
-        for (uint32_t s = threadIdx.x; s < slots; s += TB) { keys[s] = -1; vals[s] = 0; }
-        __syncthreads();
-        const int32_t* labr = a.lab + (int64_t)r * a.N;
-        const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-        const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
-        for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB) {
-            const int32_t lj = push ? nlr[j] : labr[a.col[j]];
-            if (trans) a.nlab[(int64_t)r * a.m2 + j] = lj;   // transition sweep (see k_decide_light)
-            tbl_insert(keys, vals, slots - 1, lj, LOUV ? a.cw[j] : 1);
-        }
-        __syncthreads();
-        const int32_t own = labr[v];
-        const int64_t kv = a.kdeg[v];
-        const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
-        long long best_s = LLONG_MIN, kown = 0;
-        uint32_t best_h = 0;
-        int32_t best_c = 0x7fffffff;
-        int have = 0;
-        for (uint32_t s = threadIdx.x; s < slots; s += TB) {
-            const int32_t key = keys[s];
-            if (key < 0) continue;
-            const int32_t val = vals[s];
-            if (key == own) kown = val;
-            long long sc;
-            if (LOUV) {
-                if (key == own) continue;
-                sc = (long long)val * a.M2 - kv * (long long)totr[key];
-            } else {
-                sc = val;
-            }
-            const uint32_t h = tie_hash(tbk, v, key);
-            if (!have || better(sc, h, key, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = key; have = 1; }
-        }
-        r_s[threadIdx.x] = best_s; r_h[threadIdx.x] = best_h; r_c[threadIdx.x] = best_c;
-        r_have[threadIdx.x] = have; r_kown[threadIdx.x] = kown;
-        __syncthreads();
-        for (int o = TB / 2; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) {
-                const int t2 = threadIdx.x + o;
-                if (r_have[t2] && (!r_have[threadIdx.x] ||
-                                   better(r_s[t2], r_h[t2], r_c[t2], r_s[threadIdx.x], r_h[threadIdx.x], r_c[threadIdx.x]))) {
-                    r_s[threadIdx.x] = r_s[t2]; r_h[threadIdx.x] = r_h[t2]; r_c[threadIdx.x] = r_c[t2];
-                    r_have[threadIdx.x] = 1;
-                }
-                r_kown[threadIdx.x] += r_kown[t2];
-            }
-            __syncthreads();
-        }
+        unsigned long long dq = 0;
+        int unst = 0;
+        const int32_t dcs = heavy_visit<LOUV, TT>(a, r, sweep, v, sh, a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots,
+                                                  &dq, &unst);
         if (threadIdx.x == 0) {
-            unsigned long long dq = 0;
-            int unst = 0;
-            const int32_t dcs = decide_final<LOUV, TT>(a, r, v, own, r_s[0], r_c[0], r_kown[0], r_have[0], &dq, &unst);
             a.dec[(int64_t)r * a.S + di] = make_int2(dcs, v);
             if (dq) atomicAdd(red_slot(a, r, 0), dq);
             if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
         }
-        __syncthreads();
     }
 }
 
@@ -580,8 +619,8 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
 template <bool LOUV>
 __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
     __shared__ int cnt, cnt0;
-    __shared__ unsigned long long mv;
-    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; mv = 0; }
+    __shared__ unsigned long long mv, vis;
+    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; mv = 0; vis = 0; }
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -590,6 +629,7 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
             for (int k = 0; k < RF; ++k) { f[k] += base[sh * RF + k]; base[sh * RF + k] = 0; }
         a.sacc[4 * r + 0] += f[3]; a.sacc[4 * r + 1] += f[4]; a.sacc[4 * r + 2] += f[5];
         atomicAdd(&mv, f[2]);
+        atomicAdd(&vis, f[3]);
         if (a.prune) {   // lists filter next sweep iff moves were tracked this sweep
             a.track[a.n_r + r] = a.track[r];
             if (f[2] * 4 < (unsigned long long)a.N) a.track[r] = 1;
@@ -608,11 +648,13 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         }
     }
     __syncthreads();
-    // n_active_out: [0] active after, [2..3] u64 moves, [4..5] u64 replica-sweeps so far
+    // n_active_out: [0] active after, [2..3] u64 moves, [4..5] u64 replica-sweeps so far,
+    // [6..7] u64 light-kernel visits of this sweep
     if (threadIdx.x == 0) {
         n_active_out[0] = cnt;
         *(unsigned long long*)(n_active_out + 2) = mv;
         *(unsigned long long*)(n_active_out + 4) += (unsigned long long)cnt0;
+        *(unsigned long long*)(n_active_out + 6) = vis;
     }
 }
 
@@ -623,6 +665,170 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
     if (v >= n) return;
     lab[(int64_t)r * n + v] = (int32_t)v;
     if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
+}
+
+// ------------------------------------------------------------------ tail sweeps
+// Once pruning has shrunk the sweeps to a few thousand visits per replica, a multi-kernel
+// sweep is bound by its ~100 launches, not by work.  k_cd_tail then runs every remaining
+// sweep of one replica inside one workgroup, with exactly the semantics of the
+// multi-kernel path (same visit sets, buckets, decisions, pruning and mode bookkeeping):
+//   * the visit list of the next sweep is a worklist: a move's neighbours are appended
+//     when their mark (int32 epoch stamp, tailmark[r][N]) is raised to this sweep -- the
+//     set the aff flags would hold -- so no pass over all N vertices;
+//   * the worklist is bucketed by inverse permutation (counting sort in LDS);
+//   * per bucket: light decisions (8-lane tiles, 32 per pass), heavy rows (whole block),
+//     barrier, moves applied, barrier.
+// The initial worklist is the aff flags left by the last multi-kernel sweep.
+static constexpr int TAIL_MAXB = 256;
+template <bool LOUV, typename TT>
+__global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_sweeps, int B, int32_t* tbuf,
+                                                 int32_t* tmark, unsigned long long* tail_acc, int32_t* n_active_out) {
+    constexpr int NT = TB / LT;
+    __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
+    __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
+    __shared__ HeavyShared sh;
+    __shared__ int s_off[TAIL_MAXB + 1], s_cur[TAIL_MAXB];
+    __shared__ int s_n, s_nnext, s_nheavy, s_stop;
+    __shared__ unsigned long long s_acc[6];   // dq, unstable, moves, verts, entries, cands
+    const int r = blockIdx.x;
+    if (!a.active[r]) return;                 // block-uniform
+    const int rg = a.rbase + r;
+    const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
+    int32_t* wl = tbuf + (int64_t)r * 3 * a.N;
+    int32_t* wl2 = wl + a.N;
+    int32_t* bl = wl2 + a.N;
+    int32_t* mark = tmark + (int64_t)r * a.N;
+    const uint8_t* aff = a.aff + (int64_t)r * a.N;
+    int2* decr = a.dec + (int64_t)r * a.S;
+    int32_t* hv = a.heavy + (int64_t)r * a.S;
+    int32_t* scratch = a.heavy_scratch ? a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots : nullptr;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    if (!rep_full(a, r)) {                    // initial worklist: the flagged vertices
+        for (int64_t v0 = 0; v0 < a.N; v0 += TB) {
+            const int64_t v = v0 + threadIdx.x;
+            const bool f = v < a.N && aff[v];
+            const unsigned long long b = __ballot(f);
+            int base = 0;
+            if ((threadIdx.x & 63) == 0 && b) base = atomicAdd(&s_n, __popcll(b));
+            base = __shfl(base, 0);
+            if (f) wl[base + __popcll(b & ((1ull << (threadIdx.x & 63)) - 1ull))] = (int32_t)v;
+        }
+    }
+    __syncthreads();
+    for (int sweep = sweep0; sweep < max_sweeps; ++sweep) {
+        const bool full = rep_full(a, r);
+        const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
+        const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
+        const int32_t stamp = sweep + 1;
+        for (int k = threadIdx.x; k <= B; k += TB) s_off[k] = 0;
+        if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
+        if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; }
+        __syncthreads();
+        const int n = s_n;
+        if (!full) {                          // bucket the worklist (order inside a bucket is immaterial)
+            for (int i = threadIdx.x; i < n; i += TB) {
+                const uint32_t v = (uint32_t)wl[i];
+                const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
+                atomicAdd(&s_off[pos / (uint32_t)a.S + 1], 1);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (int k = 0; k < B; ++k) { s_off[k + 1] += s_off[k]; s_cur[k] = s_off[k]; }
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += TB) {
+                const uint32_t v = (uint32_t)wl[i];
+                const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
+                bl[atomicAdd(&s_cur[pos / (uint32_t)a.S], 1)] = (int32_t)v;
+            }
+            __syncthreads();
+        }
+        for (int k = 0; k < B; ++k) {
+            const int64_t nk = full ? min(a.S, a.PN - (int64_t)k * a.S) : (int64_t)(s_off[k + 1] - s_off[k]);
+            if (threadIdx.x == 0) s_nheavy = 0;
+            __syncthreads();
+            for (int64_t base = 0; base < nk; base += NT) {   // block-uniform
+                const int64_t idx = base + tile;
+                int32_t v = -1;
+                if (idx < nk) v = full ? pos_vertex(a, P, (int64_t)k * a.S + idx) : bl[s_off[k] + idx];
+                const Visit vis = decide_visit<LOUV, TT, LT>(a, r, rg, sweep, idx < nk && v >= 0, v,
+                                                             s_key + tile * HCAP, s_val + tile * HCAP, lane);
+                if (lane == 0 && idx < nk) {
+                    decr[idx] = make_int2(v >= 0 ? vis.dcs : -1, v);
+                    if (vis.heavy) hv[atomicAdd(&s_nheavy, 1)] = (int32_t)idx;
+                    if (vis.dq) atomicAdd(&s_acc[0], vis.dq);
+                    if (vis.unst) atomicAdd(&s_acc[1], 1ull);
+                    if (vis.work) {
+                        atomicAdd(&s_acc[3], 1ull);
+                        atomicAdd(&s_acc[4], (unsigned long long)vis.d);
+                        atomicAdd(&s_acc[5], (unsigned long long)vis.ncand);
+                    }
+                }
+            }
+            __syncthreads();
+            const int nh = s_nheavy;
+            for (int h = 0; h < nh; ++h) {    // block-uniform
+                const int32_t idx = hv[h];
+                const int32_t v = decr[idx].y;
+                unsigned long long dq = 0;
+                int unst = 0;
+                const int32_t dcs = heavy_visit<LOUV, TT>(a, r, sweep, v, sh, scratch, &dq, &unst);
+                if (threadIdx.x == 0) {
+                    decr[idx] = make_int2(dcs, v);
+                    if (dq) atomicAdd(&s_acc[0], dq);
+                    if (unst) atomicAdd(&s_acc[1], 1ull);
+                }
+            }
+            __syncthreads();
+            // apply the bucket's moves; while tracking, neighbours join the next worklist
+            int moved = 0;
+            if (!push && !trk) {
+                for (int64_t di = threadIdx.x; di < nk; di += TB) {
+                    const int2 dv = decr[di];
+                    if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv.x, dv.y); ++moved; }
+                }
+            } else {
+                const int t16 = threadIdx.x / TILE, l16 = threadIdx.x % TILE;
+                int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+                for (int64_t di = t16; di < nk; di += TILES) {
+                    const int2 dv = decr[di];
+                    const int32_t d = dv.x, v = dv.y;
+                    if (d < 0) continue;
+                    if (l16 == 0) { apply_move<LOUV, TT>(a, r, d, v); ++moved; }
+                    const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
+                    for (int64_t j = rb + l16; j < re; j += TILE) {
+                        if (push) nlr[a.rev[j]] = d;
+                        if (trk) {
+                            const int32_t u = a.col[j];
+                            if (atomicMax(&mark[u], stamp) < stamp) wl2[atomicAdd(&s_nnext, 1)] = u;
+                        }
+                    }
+                }
+            }
+            if (moved) atomicAdd(&s_acc[2], (unsigned long long)moved);
+            __syncthreads();
+        }
+        // end of sweep: the same bookkeeping as k_sweep_end, for this replica
+        if (threadIdx.x == 0) {
+            const unsigned long long moves = s_acc[2];
+            tail_acc[4 * r + 0] += s_acc[3]; tail_acc[4 * r + 1] += s_acc[4]; tail_acc[4 * r + 2] += s_acc[5];
+            atomicAdd((unsigned long long*)(n_active_out + 4), 1ull);
+            if (a.prune) {
+                a.track[a.n_r + r] = a.track[r];
+                if (moves * 4 < (unsigned long long)a.N) a.track[r] = 1;
+            }
+            if (a.track[3 * a.n_r + r]) { a.track[3 * a.n_r + r] = 0; a.track[2 * a.n_r + r] = 1; }
+            else if (!a.track[2 * a.n_r + r] && moves * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
+            bool stop;
+            if (LOUV) stop = moves == 0 || ((double)s_acc[0] / DQ_SCALE) < 1e-7;
+            else stop = s_acc[1] == 0;
+            if (stop) { a.active[r] = 0; s_stop = 1; }
+            s_n = s_nnext;
+        }
+        __syncthreads();
+        if (s_stop) break;
+        int32_t* t = wl; wl = wl2; wl2 = t;
+    }
 }
 
 // Visit lists of one sweep, per replica: every vertex (sweeps before tracking starts, or
@@ -729,12 +935,13 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int64_t m2 = 2 * g.m;
     int32_t* nlab = ensure<int32_t>(c.nlab, (size_t)rcount * (m2 > 0 ? m2 : 1));
     // per-replica state: active i32 [n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active
-    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * (4 + 8 * NSH * RF + 32) + 256);
+    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * (4 + 8 * NSH * RF + 64) + 256);
     int32_t* active = (int32_t*)rs;
     unsigned long long* red = (unsigned long long*)(rs + (((size_t)rcount * 4 + 255) & ~size_t(255)));
     unsigned long long* sacc = red + (size_t)rcount * NSH * RF;
     int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);   // see k_sweep_end
-    const size_t zero_bytes = (char*)(n_active + 8) - (char*)red;
+    unsigned long long* tail_acc = (unsigned long long*)(n_active + 8);   // [n_r][4] k_cd_tail visits
+    const size_t zero_bytes = (char*)(tail_acc + 4 * (size_t)rcount) - (char*)red;
     int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * S + 3);
     uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
     FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));
@@ -749,7 +956,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int64_t heavy_slots = 1;
     while (heavy_slots < 2 * (int64_t)g.max_deg) heavy_slots <<= 1;
     int32_t* hscr = nullptr;
-    if (heavy_slots > HEAVY_LDS_SLOTS) hscr = ensure<int32_t>(c.heavy_scratch, (size_t)HEAVY_GRID * 2 * heavy_slots);
+    if (heavy_slots > HEAVY_LDS_SLOTS)   // one slice per heavy-kernel block, or per tail-kernel block (replica)
+        hscr = ensure<int32_t>(c.heavy_scratch, (size_t)std::max(HEAVY_GRID, rcount) * 2 * heavy_slots);
 
     {
         std::vector<int32_t> ones(rcount, (g.M2 > 0) ? 1 : 0);
@@ -783,7 +991,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         c.sweep_ev.resize(8);
         for (auto& e : c.sweep_ev) FC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    int32_t* ring = (int32_t*)(c.hpin + 8);
+    int32_t* ring = (int32_t*)(c.hpin + 8);   // 8 slots x 32 B: n_active[0..7] of a sweep
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
     const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
     int sweep = 0;
@@ -799,7 +1007,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
         const int slot = sweep & 7;
-        FC_HIP(hipMemcpyAsync(ring + 2 * slot, n_active, 8, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(ring + 8 * slot, n_active, 32, hipMemcpyDeviceToHost, c.stream));
         FC_HIP(hipEventRecord(c.sweep_ev[slot], c.stream));
         if (c.trace) {
             sync(c);
@@ -811,25 +1019,44 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             static auto t_last = std::chrono::steady_clock::now();
             const auto t_now = std::chrono::steady_clock::now();
             fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu dt_us=%.0f\n",
-                    iteration, sweep, ring[2 * slot], vv,
+                    iteration, sweep, ring[8 * slot], vv,
                     1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
             t_last = t_now;
         }
         if (sweep >= LAG) {
             const int chk = (sweep - LAG) & 7;
             FC_HIP(hipEventSynchronize(c.sweep_ev[chk]));
-            if (ring[2 * chk] == 0) { ++sweep; break; }
+            if (ring[8 * chk] == 0) { ++sweep; break; }
+            // small sweeps: hand every remaining sweep to the per-replica tail kernel
+            const unsigned long long visits = *(unsigned long long*)(ring + 8 * chk + 6);
+            if (c.tail_visits > 0 && (int64_t)visits <= c.tail_visits && B <= TAIL_MAXB && sweep + 1 < c.max_sweeps) {
+                int32_t* tbuf = ensure<int32_t>(c.tailbuf, (size_t)rcount * 3 * N);
+                int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
+                FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));
+                if (c.trace) fprintf(stderr, "[fc] cd it=%d tail kernel from sweep %d\n", iteration, sweep + 1);
+                if (!louv)
+                    k_cd_tail<false, int32_t><<<rcount, TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
+                else if (tot32)
+                    k_cd_tail<true, int32_t><<<rcount, TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
+                else
+                    k_cd_tail<true, int64_t><<<rcount, TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
+                break;
+            }
         }
     }
     // replica-sweeps and light-kernel traffic counters for the roofline model
-    std::vector<unsigned long long> sa(4 * (size_t)rcount + 4);
+    std::vector<unsigned long long> sa(8 * (size_t)rcount + 4);   // sacc | n_active | tail_acc
     FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
     sync(c);
     const unsigned long long rep_sweeps = sa[4 * (size_t)rcount + 2];   // n_active[4..5]
     c.acc.cd_sweeps += (int64_t)rep_sweeps;
     c.prof.cd_sweeps += (int64_t)rep_sweeps;
     c.hpin[0] = c.hpin[1] = c.hpin[2] = 0;
-    for (int r = 0; r < rcount; ++r) { c.hpin[0] += sa[4 * r]; c.hpin[1] += sa[4 * r + 1]; c.hpin[2] += sa[4 * r + 2]; }
+    int64_t tv = 0, te = 0;
+    for (int r = 0; r < rcount; ++r) {
+        c.hpin[0] += sa[4 * r]; c.hpin[1] += sa[4 * r + 1]; c.hpin[2] += sa[4 * r + 2];
+        tv += sa[4 * (size_t)rcount + 4 + 4 * r]; te += sa[4 * (size_t)rcount + 4 + 4 * r + 1];
+    }
     // algorithmic bytes of the light decide kernel: per vertex rowptr 16 + kdeg 8 + own
     // label 4 + own tot (4|8) + decision 8 + list entry 4; per adjacency entry neighbour
     // label 4 + weight 4; per Sigma gathered (candidates of maximal val) its tot (4|8)
@@ -838,9 +1065,9 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int64_t db = louv ? c.hpin[0] * (40 + tsz) + c.hpin[1] * 8 + c.hpin[2] * tsz
                             : c.hpin[0] * 32 + c.hpin[1] * 4;
     for (fc_stats* s : {&c.acc, &c.prof}) {
-        s->cd_vertex_visits += c.hpin[0];
-        s->cd_edge_visits += c.hpin[1];
-        s->decide_bytes += db;
+        s->cd_vertex_visits += c.hpin[0] + tv;   // light kernel + tail kernel
+        s->cd_edge_visits += c.hpin[1] + te;
+        s->decide_bytes += db;                   // light kernel only (its time is decide_ms)
     }
     timer_end(c, 0, sl0);
 }

@@ -155,15 +155,22 @@ def _lfr1k_graph():
     return case, orc.EdgeGraph.from_lines(case.N, case.edges_file)
 
 
+# tail: FC_OPT_TAIL_VISITS -- 0 keeps every sweep on the multi-kernel path; a huge value
+# hands every sweep after the first two to the per-replica tail kernel
+TAILS = [0, 1 << 40]
+
+
+@pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("buckets,chunk,prune", [(32, 0, 0), (5, 0, 0), (32, 16, 0), (7, 16, 0), (32, 0, 1),
                                                  (5, 16, 1)])
-def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune):
+def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail):
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=99)
     eng.set_params(buckets=buckets)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
+    eng.set_option("tail_visits", tail)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 4)
@@ -196,13 +203,15 @@ def _heavy_graph(seed, hub_deg):
     return N, e
 
 
+@pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("hub_deg,chunk,prune", [(300, 0, 0), (3000, 0, 0), (3000, 16, 0), (3000, 0, 1)])
-def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune):
+def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune, tail):
     N, e = _heavy_graph(5, hub_deg)
     eng = fcmod.Engine(seed=7)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
+    eng.set_option("tail_visits", tail)
     eng.load_graph(N, e[:, 0], e[:, 1])
     eng.cd(algo, 0, 4, 4, 1)
     got = eng.get_labels(4)
@@ -316,10 +325,11 @@ def test_closure_sampler_properties(fcmod):
 
 
 # ------------------------------------------------------------------------- whole runs, bit-exact
-@pytest.mark.parametrize("algo,n_p,tau,chunk,prune,relabel",
-                         [(0, 10, 0.2, 0, 0, 0), (0, 12, 0.2, 16, 0, 1), (1, 4, 0.8, 0, 0, 0), (0, 20, 0.2, 0, 0, 1),
-                          (0, 10, 0.2, 0, 1, 1), (1, 6, 0.8, 16, 1, 1), (0, 10, 0.2, 16, 1, 1)])
-def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel):
+@pytest.mark.parametrize("algo,n_p,tau,chunk,prune,relabel,tail",
+                         [(0, 10, 0.2, 0, 0, 0, 0), (0, 12, 0.2, 16, 0, 1, 131072), (1, 4, 0.8, 0, 0, 0, 131072),
+                          (0, 20, 0.2, 0, 0, 1, 0), (0, 10, 0.2, 0, 1, 1, 131072), (1, 6, 0.8, 16, 1, 1, 0),
+                          (1, 6, 0.8, 16, 1, 1, 131072), (0, 10, 0.2, 16, 1, 1, 0), (0, 10, 0.2, 16, 1, 1, 131072)])
+def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel, tail):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
     loop (bucketed CD twin, consensus rule, Philox closure sampler, repair, ages): final
     partitions AND the final graph are identical (n_p=10 runs 9 iterations)."""
@@ -331,6 +341,7 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
     eng.set_option("relabel", relabel)
+    eng.set_option("tail_visits", tail)
     eng.set_params(max_iters=50)
     eng.load_graph(case.N, e[:, 0], e[:, 1])
     sigma = eng.node_map()
