@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "lib", "libfastconsensus_amd.so")
+LIB_PATH = os.environ.get("FC_LIB_PATH") or os.path.join(PKG, "lib", "libfastconsensus_amd.so")
 
 FC_ALGO_LOUVAIN = 0
 FC_ALGO_LPM = 1

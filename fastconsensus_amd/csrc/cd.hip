@@ -38,8 +38,8 @@ static constexpr int CHUNK = 16;
 
 static constexpr int TILE = 16;         // lanes per decision in k_apply's row scatter
 static constexpr int TILES = TB / TILE;
-static constexpr int LT = 8;            // lanes per vertex in k_decide_light
-static constexpr int LNT = TB / LT;     // vertices per k_decide_light block
+static constexpr int WNT = 8;           // vertices per wave in the light decide (rows flattened over 64 lanes)
+static constexpr int LNT = WNT * (TB / 64);   // vertices per k_decide_light block (one item)
 static constexpr int HCAP = 64;         // slots per tile table (>= LIGHT_MAX_DEG: every insert finds a slot)
 static constexpr int LIGHT_MAX_DEG = 64;
 static constexpr int HEAVY_LDS_SLOTS = 4096;
@@ -96,7 +96,6 @@ struct CDArgs {
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
     int64_t heavy_slots;         // slots per global table (power of 2)
     unsigned long long* sacc;    // [n_r][4] light-kernel vertices / entries / candidates, summed by k_sweep_end
-    int dbg;                     // FC_DBG ablation bits (timing experiments only; results become wrong)
 };
 
 // Vertex at sweep position p, or -1 for a padding slot of the last chunk.
@@ -109,6 +108,7 @@ __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, in
 // Replica r's sweep visits every position (no pruning filter yet): its "list" is implicit,
 // entry di of bucket k = position k*S + di.
 __device__ __forceinline__ bool rep_full(const CDArgs& a, int r) { return !(a.prune && a.track[a.n_r + r]); }
+
 
 __device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
     return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
@@ -197,194 +197,272 @@ struct Visit {
     int64_t d;                 // degree
     bool work, heavy;
 };
-template <bool LOUV, typename TT, int LT>
-__device__ __forceinline__ Visit decide_visit(const CDArgs& a, int r, int rg, int sweep, bool valid, int32_t v,
-                                              int32_t* keys, int32_t* vals, int lane) {
-    constexpr int PER = LIGHT_MAX_DEG / LT;     // neighbours per lane
+#ifdef FC_PHASE_PROF
+// Diagnostic build only: cycles per phase of decide_wave, sampled on 1/64 of the blocks.
+__device__ unsigned long long g_phase[16];
+#define PST(i)                                                                          \
+    do {                                                                                \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                     \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();                     \
+        if (_samp && lane == 0) atomicAdd(&g_phase[i], _t - _tp);                       \
+        _tp = _t;                                                                       \
+    } while (0)
+#else
+#define PST(i) do { } while (0)
+#endif
+
+// LDS of one wave: 8 vertex tables + per-vertex scratch.
+struct WaveShared {
+    int32_t key[WNT * HCAP];
+    int32_t val[WNT * HCAP];
+    long long best2[WNT];        // best exact score among lower-val candidates (rare path)
+    long long tmin[WNT];         // min Sigma among the max-val candidates
+    unsigned long long k2[WNT];
+    long long kv[WNT];
+    int32_t vm[WNT], own[WNT], kown[WNT];
+    uint32_t tvh[WNT];
+};
+
+__device__ __forceinline__ void wave_sync() {
+    // one wave's LDS operations execute in order; only the compiler must not reorder
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// One wave decides 8 vertices (lane t < 8 brings vertex t; every lane of the wave calls).
+// The 8 adjacency rows are FLATTENED over the 64 lanes (entry e of their concatenation goes
+// to lane e % 64), so every lane loads and inserts useful entries (a 27-entry row on an
+// 8-lane tile left most lanes idle and every entry behind its own branch).  Rows stream
+// from nlab (push mode) or are gathered through lab[col] (pull); each vertex gets a 64-slot
+// LDS hash table and the lane whose CAS creates a slot owns that candidate.  Per vertex,
+// through LDS atomics: the max val over foreign communities; Sigma gathered only for the
+// candidates of maximal val (score = val*2M - k_v*Sigma <= val*2M, so a lower one cannot
+// win unless its bound still reaches the best exact score -- checked, rare); the best
+// score; the best tie key among equal scores.  Python-louvain's rule: move iff the gain
+// of the best community > 0; LPA: the most frequent label (own label competing).
+// Returns vertex t's visit in lane t (< 8); ncand is per lane (sum it over the wave).
+template <bool LOUV, typename TT>
+__device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int sweep, bool valid, int32_t v,
+                                             WaveShared& ws) {
+    const int lane = threadIdx.x & 63;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
-    int64_t rb = 0, d = 0;
-    int32_t own = 0;
-    int64_t kv = 0;
+    const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
+    const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
+#ifdef FC_PHASE_PROF
+    const bool _samp = (blockIdx.x & 63) == 0;
+    unsigned long long _tp = __builtin_amdgcn_s_memtime();
+#endif
+    // ---- per-vertex state, lanes 0..7
+    const bool vl = lane < WNT && valid;
+    int64_t rb = 0, d = 0, kv = 0;
+    int32_t own = -1;
     TT tot_own = 0;
-    if (valid) {
+    if (vl) {
         rb = a.rowptr[v];
         d = a.rowptr[v + 1] - rb;
         own = labr[v];
         if (LOUV) kv = a.kdeg[v];
     }
-    const bool heavy = valid && d > LIGHT_MAX_DEG;
-    const bool work = valid && !heavy && d > 0;
+    PST(0);
+    const bool heavy = vl && d > LIGHT_MAX_DEG;
+    const bool work = vl && !heavy && d > 0;
     if (LOUV && work) tot_own = totr[own];       // in flight with the row loads below
-    const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-    // ---- push mode: the row's neighbour labels are STREAMED from nlab; pull mode (early,
-    // move-heavy sweeps): gathered from lab[col[j]] -- the same values either way
-    const bool push = a.track[2 * a.n_r + r] != 0;
-    int32_t cq[PER], wq[PER];
+    const int de = work ? (int)d : 0;
+    int inc = de;                                // inclusive scan of the row lengths (lanes 0..7)
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int64_t j = rb + lane + LT * q;
-        const bool ok = work && j < rb + d;
-        cq[q] = ok ? (push ? nlr[j] : a.col[j]) : -1;
-        wq[q] = ok ? (LOUV ? a.cw[j] : 1) : 0;
+    for (int off = 1; off < WNT; off <<= 1) {
+        const int y = __shfl_up(inc, off, WNT);
+        if ((lane & (WNT - 1)) >= off) inc += y;
     }
-    if (!push) {
-        if (!(a.dbg & 2))
+    const int ex = inc - de;
+    const long long jb = (long long)rb - ex;     // entry e of vertex t is adjacency entry jb_t + e
+    {   // clear the 8 tables (16-byte stores) and the per-vertex scratch
+        int4* k4 = reinterpret_cast<int4*>(ws.key);
+        int4* v4 = reinterpret_cast<int4*>(ws.val);
 #pragma unroll
-            for (int q = 0; q < PER; ++q) cq[q] = cq[q] >= 0 ? labr[cq[q]] : -1;
-        if (a.track[3 * a.n_r + r]) {    // transition sweep: this row's nlab entries, as seen now
-            int32_t* nlw = a.nlab + (int64_t)r * a.m2;
-#pragma unroll
-            for (int q = 0; q < PER; ++q)
-                if (cq[q] >= 0) nlw[rb + lane + LT * q] = cq[q];
+        for (int s = lane; s < WNT * HCAP / 4; s += 64) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
+        if (lane < WNT) {
+            ws.best2[lane] = LLONG_MIN; ws.tmin[lane] = LLONG_MAX; ws.k2[lane] = 0; ws.vm[lane] = INT_MIN; ws.kown[lane] = 0;
+            ws.own[lane] = work ? own : -1;
+            ws.kv[lane] = kv;
+            ws.tvh[lane] = hash32(stream_key(a.seed, rg, a.iter, sweep, 2) ^ (uint32_t)v);
         }
     }
-    // ---- tile table: clear (16-byte stores), insert, owners evaluate
-    {
-        int4* k4 = reinterpret_cast<int4*>(keys);
-        int4* v4 = reinterpret_cast<int4*>(vals);
-        for (int s = lane; s < HCAP / 4; s += LT) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
-    }
-    __syncthreads();
-    // insert: every lane's first probes are issued back to back (one LDS round trip for
-    // all of them; a wave's LDS operations execute in order, so entries of one key agree
-    // on its slot), collisions then probe linearly; the lane whose CAS created a slot owns it
-    int slot[PER];
-    {
-        uint32_t hq[PER];
-        int32_t pv[PER];
+    int o[WNT];
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            hq[q] = hash32((uint32_t)cq[q]) & (HCAP - 1);
-            pv[q] = cq[q] >= 0 ? atomicCAS(&keys[hq[q]], -1, cq[q]) : cq[q];
+    for (int s = 0; s < WNT; ++s) o[s] = __shfl(ex, s);
+    const int E = __shfl(inc, WNT - 1);
+    wave_sync();
+    PST(1);
+    // ---- flattened rows: at most 2 chunks of 4 x 64 entries (8 rows of <= 64)
+    int rec[8];                                  // owned slots: (t << 8) | slot, or -1
+#pragma unroll
+    for (int it = 0; it < 8; ++it) rec[it] = -1;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (c * 256 >= E) break;                 // wave-uniform
+        int32_t kq[4], wq[4], tq[4];
+        long long jq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = c * 256 + u * 64 + lane;
+            int t = 0;
+#pragma unroll
+            for (int s = 1; s < WNT; ++s) t += (e >= o[s]) ? 1 : 0;
+            jq[u] = __shfl(jb, t) + e;
+            const bool ok = e < E;
+            kq[u] = ok ? (push ? nlr[jq[u]] : a.col[jq[u]]) : -1;
+            wq[u] = ok ? (LOUV ? a.cw[jq[u]] : 1) : 0;
+            tq[u] = t;
         }
+        PST(2);
+        if (!push) {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            slot[q] = -1;
-            if (cq[q] < 0) continue;
-            while (pv[q] != -1 && pv[q] != cq[q]) {
-                hq[q] = (hq[q] + 1) & (HCAP - 1);
-                pv[q] = atomicCAS(&keys[hq[q]], -1, cq[q]);
+            for (int u = 0; u < 4; ++u) kq[u] = kq[u] >= 0 ? labr[kq[u]] : -1;
+            if (trans) {                         // transition sweep: these nlab entries, as seen now
+                int32_t* nlw = a.nlab + (int64_t)r * a.m2;
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (kq[u] >= 0) nlw[jq[u]] = kq[u];
             }
-            atomicAdd(&vals[hq[q]], wq[q]);
-            if (pv[q] == -1) slot[q] = (int)hq[q];
         }
-    }
-    __syncthreads();
-    // ---- evaluate.  Candidates rank lexicographically by (score, tie hash, -id); key2 packs
-    // the last two.  Louvain: score_c = val_c*2M - k_v*Sigma_c <= val_c*2M, so only the
-    // candidates of maximal val need their Sigma gathered, unless a lower one's bound still
-    // reaches the best exact score (rare: needs k_v*Sigma_best >= 2M) -- the same argmax
-    // with a fraction of the random Sigma gathers.  LPA: score = val (own label included).
-    int32_t vq[PER];
-    int vm = INT_MIN;
-    TT kown = 0;
+        PST(3);
+        // insert: first probes back to back (one LDS round trip; a wave's LDS operations
+        // execute in order, so entries of one key agree on its slot), then linear probing
+        uint32_t hq[4];
+        int32_t pv[4];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        vq[q] = slot[q] >= 0 ? vals[slot[q]] : 0;
-        if (slot[q] >= 0) {
-            if (cq[q] == own) kown = (TT)vq[q];
-            else vm = max(vm, vq[q]);
+        for (int u = 0; u < 4; ++u) {
+            hq[u] = hash32((uint32_t)kq[u]) & (HCAP - 1);
+            pv[u] = kq[u] >= 0 ? atomicCAS(&ws.key[tq[u] * HCAP + hq[u]], -1, kq[u]) : kq[u];
         }
-    }
-    if (LOUV) {
 #pragma unroll
-        for (int off = LT / 2; off > 0; off >>= 1) vm = max(vm, __shfl_xor(vm, off, LT));
+        for (int u = 0; u < 4; ++u) {
+            if (kq[u] < 0) continue;
+            while (pv[u] != -1 && pv[u] != kq[u]) {
+                hq[u] = (hq[u] + 1) & (HCAP - 1);
+                pv[u] = atomicCAS(&ws.key[tq[u] * HCAP + hq[u]], -1, kq[u]);
+            }
+            atomicAdd(&ws.val[tq[u] * HCAP + hq[u]], wq[u]);
+            if (pv[u] == -1) rec[c * 4 + u] = (tq[u] << 8) | (int)hq[u];
+        }
+        PST(4);
     }
-    TT tq[PER];
+    wave_sync();
+    // ---- candidates: own-community weight; max val over the foreign ones (Louvain) or over
+    // all labels (LPA)
 #pragma unroll
-    for (int q = 0; q < PER; ++q)
-        tq[q] = (LOUV && slot[q] >= 0 && cq[q] != own && vq[q] == vm && !(a.dbg & 1)) ? totr[cq[q]] : (TT)0;
-    long long best_s = LLONG_MIN;
-    unsigned long long best_k = 0;
+    for (int it = 0; it < 8; ++it) {
+        if (rec[it] < 0) continue;
+        const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+        const int32_t key = ws.key[sl], val = ws.val[sl];
+        if (key == ws.own[t]) {
+            ws.kown[t] = val;
+            if (LOUV) { rec[it] = -1; continue; }   // LPA: the own label competes
+        }
+        atomicMax(&ws.vm[t], val);
+    }
+    wave_sync();
+    PST(5);
     int ncand = 0;
-    const uint32_t tvh = hash32(stream_key(a.seed, rg, a.iter, sweep, 2) ^ (uint32_t)v);
-    // exact int64 score; with int32 totals 2M < 2^31, so 32x32->64 products suffice
-    auto score = [&](int32_t val, TT t) -> long long {
-        if constexpr (sizeof(TT) == 4)
-            return (long long)val * (int32_t)a.M2 - (long long)(int32_t)kv * (int32_t)t;
+    auto score = [&](int32_t val, long long tt, long long kvt) -> long long {
+        if constexpr (sizeof(TT) == 4)          // 2M < 2^31: k_v and Sigma fit 32 bits
+            return (long long)val * (int32_t)a.M2 - (long long)(int32_t)kvt * (int32_t)tt;
         else
-            return (long long)val * a.M2 - kv * (long long)t;
+            return (long long)val * a.M2 - kvt * tt;
     };
-    auto consider = [&](int32_t key, long long sc) {
-        const unsigned long long k2 = ((unsigned long long)hash32(tvh ^ (uint32_t)key) << 32) | (uint32_t)~key;
-        if (sc > best_s || (sc == best_s && k2 > best_k)) { best_s = sc; best_k = k2; }
+    // best score of vertex t: Louvain max(vm*2M - k_v*min Sigma, rare lower-val best); LPA vm
+    auto best_of = [&](int t) -> long long {
+        if (!LOUV) return (long long)ws.vm[t];
+        const long long b1 = score(ws.vm[t], ws.tmin[t], ws.kv[t]);
+        return max(b1, ws.best2[t]);
     };
-    auto tile_best = [&]() {
-#pragma unroll
-        for (int off = LT / 2; off > 0; off >>= 1) {
-            const long long os = __shfl_xor(best_s, off, LT);
-            const unsigned long long ok2 = __shfl_xor(best_k, off, LT);
-            if (os > best_s || (os == best_s && ok2 > best_k)) { best_s = os; best_k = ok2; }
-        }
-    };
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        if (slot[q] < 0) continue;
-        if (LOUV) {
-            if (cq[q] == own || vq[q] != vm) continue;
-            ++ncand;
-            consider(cq[q], score(vq[q], tq[q]));
-        } else {
-            ++ncand;
-            consider(cq[q], vq[q]);
-        }
-    }
-    tile_best();
+    TT tg[8];                                    // gathered Sigma (-1: not evaluated)
     if (LOUV) {
+        // among the max-val candidates the score is vm*2M - k_v*Sigma: the smallest Sigma wins
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            tg[it] = (TT)-1;
+            if (rec[it] < 0) continue;
+            const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+            if (ws.val[sl] == ws.vm[t]) tg[it] = totr[ws.key[sl]];
+        }
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+            if (tg[it] >= 0) { ++ncand; atomicMin(&ws.tmin[rec[it] >> 8], (long long)tg[it]); }
+        wave_sync();
+        // a lower val whose bound val*2M still reaches that score (rare: k_v*Sigma >= 2M)
         bool need = false;
 #pragma unroll
-        for (int q = 0; q < PER; ++q)
-            need |= slot[q] >= 0 && cq[q] != own && vq[q] < vm && (long long)vq[q] * a.M2 >= best_s;
-        if (__any(need)) {        // wave-uniform
+        for (int it = 0; it < 8; ++it) {
+            if (rec[it] < 0 || tg[it] >= 0) continue;
+            const int t = rec[it] >> 8;
+            need |= (long long)ws.val[t * HCAP + (rec[it] & 255)] * a.M2 >= score(ws.vm[t], ws.tmin[t], ws.kv[t]);
+        }
+        if (__any(need)) {                       // wave-uniform
 #pragma unroll
-            for (int q = 0; q < PER; ++q)
-                tq[q] = (slot[q] >= 0 && cq[q] != own && vq[q] < vm && (long long)vq[q] * a.M2 >= best_s)
-                            ? totr[cq[q]] : (TT)-1;
-#pragma unroll
-            for (int q = 0; q < PER; ++q) {
-                if (tq[q] < 0) continue;
+            for (int it = 0; it < 8; ++it) {
+                if (rec[it] < 0 || tg[it] >= 0) continue;
+                const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+                const int32_t val = ws.val[sl];
+                if ((long long)val * a.M2 < score(ws.vm[t], ws.tmin[t], ws.kv[t])) continue;
+                tg[it] = totr[ws.key[sl]];
                 ++ncand;
-                consider(cq[q], score(vq[q], tq[q]));
+                atomicMax(&ws.best2[t], score(val, tg[it], ws.kv[t]));
             }
-            tile_best();
+            wave_sync();
         }
-    }
+    } else {
 #pragma unroll
-    for (int off = LT / 2; off > 0; off >>= 1) {
-        kown += __shfl_xor(kown, off, LT);
-        ncand += __shfl_xor(ncand, off, LT);
-    }
-    // (best_s == LLONG_MIN: no candidate other than the own community)
-    unsigned long long dq = 0;
-    int unst = 0, dcs = -1;
-    if (work && best_s != LLONG_MIN) {
-        const int32_t best_c = (int32_t)~(uint32_t)best_k;
-        if (LOUV) {
-            const long long G = best_s - (long long)kown * a.M2 + kv * ((long long)tot_own - kv);
-            if (G > 0) {
-                const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
-                dq = (unsigned long long)llrint(dqd * DQ_SCALE);
-                dcs = best_c;
-            }
-        } else {
-            unst = (long long)kown != best_s;   // own label not dominant
-            dcs = best_c != own ? best_c : -1;
+        for (int it = 0; it < 8; ++it) {
+            tg[it] = (TT)-1;
+            if (rec[it] >= 0) { tg[it] = 0; ++ncand; }
         }
     }
+    PST(6);
+    // tie key among the candidates at the best score: larger hash, then smaller id
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        if (tg[it] < 0) continue;
+        const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+        const int32_t key = ws.key[sl], val = ws.val[sl];
+        const long long sc = LOUV ? score(val, tg[it], ws.kv[t]) : (long long)val;
+        if (sc != best_of(t)) continue;
+        atomicMax(&ws.k2[t], ((unsigned long long)hash32(ws.tvh[t] ^ (uint32_t)key) << 32) | (uint32_t)~key);
+    }
+    wave_sync();
+    PST(7);
+    // ---- the decision, lanes 0..7
     Visit out;
-    out.dcs = dcs; out.dq = dq; out.unst = unst; out.ncand = ncand; out.d = d; out.work = work; out.heavy = heavy;
+    out.dcs = -1; out.dq = 0; out.unst = 0; out.ncand = ncand; out.d = d; out.work = work; out.heavy = heavy;
+    if (work && ws.vm[lane] != INT_MIN) {        // some candidate besides the own community (Louvain)
+        const long long best_s = best_of(lane);
+        {
+            const int32_t best_c = (int32_t)~(uint32_t)ws.k2[lane];
+            const TT kown = (TT)ws.kown[lane];
+            if (LOUV) {
+                const long long G = best_s - (long long)kown * a.M2 + kv * ((long long)tot_own - kv);
+                if (G > 0) {
+                    const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+                    out.dq = (unsigned long long)llrint(dqd * DQ_SCALE);
+                    out.dcs = best_c;
+                }
+            } else {
+                out.unst = (long long)kown != best_s;   // own label not dominant
+                out.dcs = best_c != own ? best_c : -1;
+            }
+        }
+    }
+    PST(8);
     return out;
 }
 
-template <bool LOUV, typename TT, int LT>
+template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
-    constexpr int NT = TB / LT;                 // tiles (vertices) per block
-    constexpr int PER = LIGHT_MAX_DEG / LT;     // neighbours per lane
-    __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
-    __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
+    __shared__ WaveShared s_ws[TB / 64];
     __shared__ unsigned long long s_red[TB / 64][5];
-    const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
     const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
     // one item per block; XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the
@@ -396,8 +474,8 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     // vector r would move the per-replica arithmetic -- permutation keys, addresses -- to VALU)
     const int r = __builtin_amdgcn_readfirstlane(a.itemrep[(int64_t)bucket * a.wmax + w]);
     const int64_t seg = ((int64_t)bucket * a.n_r + r);
-    const int64_t di = (w - __builtin_amdgcn_readfirstlane(bo[r])) * NT + tile;   // decision slot
-    const bool in_range = di < __builtin_amdgcn_readfirstlane(a.lcnt[seg]);
+    const int64_t di = (w - __builtin_amdgcn_readfirstlane(bo[r])) * LNT + wv * WNT + lane;   // decision slot (lane < 8)
+    const bool in_range = lane < WNT && di < __builtin_amdgcn_readfirstlane(a.lcnt[seg]);
     const int rg = a.rbase + r;
     int32_t v = -1;
     if (in_range) {
@@ -407,57 +485,54 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     }
     const bool rep_on = a.active[r] != 0;
     const bool valid = rep_on && in_range && v >= 0;
-    const Visit vis = decide_visit<LOUV, TT, LT>(a, r, rg, sweep, valid, v, s_key + tile * HCAP, s_val + tile * HCAP, lane);
-    const int32_t dcs = vis.dcs;
-    const unsigned long long dq = vis.dq;
-    const int unst = vis.unst, ncand = vis.ncand;
-    const int64_t d = vis.d;
-    const bool work = vis.work, heavy = vis.heavy;
-    if (lane == 0) {
-        if (rep_on && in_range) a.dec[(int64_t)r * a.S + di] = make_int2(v >= 0 ? dcs : -1, v);   // heavy: rewritten later
-        if (heavy) {
-            const int q = atomicAdd(a.heavy_cnt, 1);
-            a.heavy[3 * q] = r;
-            a.heavy[3 * q + 1] = (int32_t)di;
-            a.heavy[3 * q + 2] = v;
+    const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, valid, v, s_ws[wv]);
+    if (rep_on && in_range) {
+        a.dec[(int64_t)r * a.S + di] = make_int2(v >= 0 ? vis.dcs : -1, v);   // heavy: rewritten later
+        if (vis.heavy) {
+            const int hq = atomicAdd(a.heavy_cnt, 1);
+            a.heavy[3 * hq] = r;
+            a.heavy[3 * hq + 1] = (int32_t)di;
+            a.heavy[3 * hq + 2] = v;
         }
     }
-    // ---- block counters: tile lane 0 holds them; wave sums, then one add per field
-    unsigned long long f0 = lane == 0 ? dq : 0, f1 = lane == 0 ? (unsigned long long)unst : 0;
-    unsigned long long f2 = (lane == 0 && work) ? 1ull : 0, f3 = (lane == 0 && work) ? (unsigned long long)d : 0;
-    unsigned long long f4 = (lane == 0 && work) ? (unsigned long long)ncand : 0;
+    // ---- block counters: per-vertex fields on lanes 0..7, candidates on every lane
+    unsigned long long f0 = lane < WNT ? vis.dq : 0;
+    unsigned f1 = lane < WNT ? (unsigned)vis.unst : 0u, f2 = (lane < WNT && vis.work) ? 1u : 0u;
+    unsigned f3 = (lane < WNT && vis.work) ? (unsigned)vis.d : 0u, f4 = (unsigned)vis.ncand;
 #pragma unroll
-    for (int off = LT; off < 64; off <<= 1) {
-        f0 += __shfl_xor(f0, off); f1 += __shfl_xor(f1, off); f2 += __shfl_xor(f2, off);
-        f3 += __shfl_xor(f3, off); f4 += __shfl_xor(f4, off);
+    for (int off = WNT / 2; off > 0; off >>= 1) {
+        f0 += __shfl_xor(f0, off, WNT); f1 += __shfl_xor(f1, off, WNT); f2 += __shfl_xor(f2, off, WNT);
+        f3 += __shfl_xor(f3, off, WNT);
     }
-    if ((threadIdx.x & 63) == 0) {
-        const int w = threadIdx.x >> 6;
-        s_red[w][0] = f0; s_red[w][1] = f1; s_red[w][2] = f2; s_red[w][3] = f3; s_red[w][4] = f4;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) f4 += __shfl_xor(f4, off);
+    if (lane == 0) {
+        s_red[wv][0] = f0; s_red[wv][1] = f1; s_red[wv][2] = f2; s_red[wv][3] = f3; s_red[wv][4] = f4;
     }
     __syncthreads();
     if (threadIdx.x < 5 && rep_on) {
-        unsigned long long s = 0;
-        for (int w = 0; w < TB / 64; ++w) s += s_red[w][threadIdx.x];
+        unsigned long long sm = 0;
+        for (int k = 0; k < TB / 64; ++k) sm += s_red[k][threadIdx.x];
         // fields: s_red 0 dq -> 0, 1 unstable -> 1, 2 verts -> 3, 3 entries -> 4, 4 cands -> 5
-        if (s) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), s);
+        if (sm) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), sm);
     }
 }
 
 // A high-degree vertex decided by a whole 256-thread block (every thread calls it).  Table
 // in LDS when it fits, else the block's global slice `scratch`.  Returns the decision on
 // thread 0 (dq / unstable through the pointers).
+template <int NTH>
 struct HeavyShared {
     int32_t key[HEAVY_LDS_SLOTS];
     int32_t val[HEAVY_LDS_SLOTS];
-    long long s[TB];
-    uint32_t h[TB];
-    int32_t c[TB];
-    int have[TB];
-    long long kown[TB];
+    long long s[NTH];
+    uint32_t h[NTH];
+    int32_t c[NTH];
+    int have[NTH];
+    long long kown[NTH];
 };
-template <bool LOUV, typename TT>
-__device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, HeavyShared& sh, int32_t* scratch,
+template <bool LOUV, typename TT, int NTH>
+__device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, HeavyShared<NTH>& sh, int32_t* scratch,
                                unsigned long long* dq_out, int* unst_out) {
     const int rg = a.rbase + r;
     const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
@@ -472,14 +547,14 @@ __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, Hea
         keys = scratch;
         vals = keys + slots;
     }
-    for (uint32_t s = threadIdx.x; s < slots; s += TB) { keys[s] = -1; vals[s] = 0; }
+    for (uint32_t s = threadIdx.x; s < slots; s += NTH) { keys[s] = -1; vals[s] = 0; }
     __syncthreads();
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
     const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
-    for (int64_t j = rb + threadIdx.x; j < rb + d; j += TB) {
+    for (int64_t j = rb + threadIdx.x; j < rb + d; j += NTH) {
         const int32_t lj = push ? nlr[j] : labr[a.col[j]];
-        if (trans) a.nlab[(int64_t)r * a.m2 + j] = lj;   // transition sweep (see decide_visit)
+        if (trans) a.nlab[(int64_t)r * a.m2 + j] = lj;   // transition sweep (see decide_wave)
         tbl_insert(keys, vals, slots - 1, lj, LOUV ? a.cw[j] : 1);
     }
     __syncthreads();
@@ -490,7 +565,7 @@ __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, Hea
     uint32_t best_h = 0;
     int32_t best_c = 0x7fffffff;
     int have = 0;
-    for (uint32_t s = threadIdx.x; s < slots; s += TB) {
+    for (uint32_t s = threadIdx.x; s < slots; s += NTH) {
         const int32_t key = keys[s];
         if (key < 0) continue;
         const int32_t val = vals[s];
@@ -508,7 +583,7 @@ __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, Hea
     sh.s[threadIdx.x] = best_s; sh.h[threadIdx.x] = best_h; sh.c[threadIdx.x] = best_c;
     sh.have[threadIdx.x] = have; sh.kown[threadIdx.x] = kown;
     __syncthreads();
-    for (int o = TB / 2; o > 0; o >>= 1) {
+    for (int o = NTH / 2; o > 0; o >>= 1) {
         if ((int)threadIdx.x < o) {
             const int t2 = threadIdx.x + o;
             if (sh.have[t2] && (!sh.have[threadIdx.x] ||
@@ -530,7 +605,7 @@ __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, Hea
 // Workgroup per high-degree vertex of the bucket (listed by k_decide_light).
 template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int sweep) {
-    __shared__ HeavyShared sh;
+    __shared__ HeavyShared<TB> sh;
     const int cnt = *a.heavy_cnt;
     for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
         const int r = a.heavy[3 * item];
@@ -538,7 +613,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         const int32_t v = a.heavy[3 * item + 2];
         unsigned long long dq = 0;
         int unst = 0;
-        const int32_t dcs = heavy_visit<LOUV, TT>(a, r, sweep, v, sh, a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots,
+        const int32_t dcs = heavy_visit<LOUV, TT, TB>(a, r, sweep, v, sh, a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots,
                                                   &dq, &unst);
         if (threadIdx.x == 0) {
             a.dec[(int64_t)r * a.S + di] = make_int2(dcs, v);
@@ -680,20 +755,19 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
 //     barrier, moves applied, barrier.
 // The initial worklist is the aff flags left by the last multi-kernel sweep.
 static constexpr int TAIL_MAXB = 256;
-template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_sweeps, int B, int32_t* tbuf,
+static constexpr int TAIL_TB = 1024;     // threads per replica workgroup in k_cd_tail
+template <bool LOUV, typename TT, int NTH>
+__global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_sweeps, int B, int32_t* tbuf,
                                                  int32_t* tmark, unsigned long long* tail_acc, int32_t* n_active_out) {
-    constexpr int NT = TB / LT;
-    __shared__ __attribute__((aligned(16))) int32_t s_key[NT * HCAP];
-    __shared__ __attribute__((aligned(16))) int32_t s_val[NT * HCAP];
-    __shared__ HeavyShared sh;
+    __shared__ WaveShared s_ws[NTH / 64];
+    __shared__ HeavyShared<NTH> sh;
     __shared__ int s_off[TAIL_MAXB + 1], s_cur[TAIL_MAXB];
     __shared__ int s_n, s_nnext, s_nheavy, s_stop;
     __shared__ unsigned long long s_acc[6];   // dq, unstable, moves, verts, entries, cands
     const int r = blockIdx.x;
     if (!a.active[r]) return;                 // block-uniform
     const int rg = a.rbase + r;
-    const int tile = threadIdx.x / LT, lane = threadIdx.x % LT;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int32_t* wl = tbuf + (int64_t)r * 3 * a.N;
     int32_t* wl2 = wl + a.N;
     int32_t* bl = wl2 + a.N;
@@ -705,7 +779,7 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
     if (!rep_full(a, r)) {                    // initial worklist: the flagged vertices
-        for (int64_t v0 = 0; v0 < a.N; v0 += TB) {
+        for (int64_t v0 = 0; v0 < a.N; v0 += NTH) {
             const int64_t v = v0 + threadIdx.x;
             const bool f = v < a.N && aff[v];
             const unsigned long long b = __ballot(f);
@@ -721,13 +795,13 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
         const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
         const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
         const int32_t stamp = sweep + 1;
-        for (int k = threadIdx.x; k <= B; k += TB) s_off[k] = 0;
+        for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
         if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
         if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; }
         __syncthreads();
         const int n = s_n;
         if (!full) {                          // bucket the worklist (order inside a bucket is immaterial)
-            for (int i = threadIdx.x; i < n; i += TB) {
+            for (int i = threadIdx.x; i < n; i += NTH) {
                 const uint32_t v = (uint32_t)wl[i];
                 const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
                 atomicAdd(&s_off[pos / (uint32_t)a.S + 1], 1);
@@ -736,7 +810,7 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
             if (threadIdx.x == 0)
                 for (int k = 0; k < B; ++k) { s_off[k + 1] += s_off[k]; s_cur[k] = s_off[k]; }
             __syncthreads();
-            for (int i = threadIdx.x; i < n; i += TB) {
+            for (int i = threadIdx.x; i < n; i += NTH) {
                 const uint32_t v = (uint32_t)wl[i];
                 const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
                 bl[atomicAdd(&s_cur[pos / (uint32_t)a.S], 1)] = (int32_t)v;
@@ -747,13 +821,17 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
             const int64_t nk = full ? min(a.S, a.PN - (int64_t)k * a.S) : (int64_t)(s_off[k + 1] - s_off[k]);
             if (threadIdx.x == 0) s_nheavy = 0;
             __syncthreads();
-            for (int64_t base = 0; base < nk; base += NT) {   // block-uniform
-                const int64_t idx = base + tile;
+            for (int64_t base = wv * WNT; base < nk; base += WNT * (NTH / 64)) {   // wave-uniform (waves are independent)
+                const int64_t idx = base + lane;
+                const bool in = lane < WNT && idx < nk;
                 int32_t v = -1;
-                if (idx < nk) v = full ? pos_vertex(a, P, (int64_t)k * a.S + idx) : bl[s_off[k] + idx];
-                const Visit vis = decide_visit<LOUV, TT, LT>(a, r, rg, sweep, idx < nk && v >= 0, v,
-                                                             s_key + tile * HCAP, s_val + tile * HCAP, lane);
-                if (lane == 0 && idx < nk) {
+                if (in) v = full ? pos_vertex(a, P, (int64_t)k * a.S + idx) : bl[s_off[k] + idx];
+                const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, in && v >= 0, v, s_ws[wv]);
+                unsigned nc = (unsigned)vis.ncand;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) nc += __shfl_xor(nc, off);
+                if (lane == 0 && nc) atomicAdd(&s_acc[5], (unsigned long long)nc);
+                if (in) {
                     decr[idx] = make_int2(v >= 0 ? vis.dcs : -1, v);
                     if (vis.heavy) hv[atomicAdd(&s_nheavy, 1)] = (int32_t)idx;
                     if (vis.dq) atomicAdd(&s_acc[0], vis.dq);
@@ -761,7 +839,6 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
                     if (vis.work) {
                         atomicAdd(&s_acc[3], 1ull);
                         atomicAdd(&s_acc[4], (unsigned long long)vis.d);
-                        atomicAdd(&s_acc[5], (unsigned long long)vis.ncand);
                     }
                 }
             }
@@ -772,7 +849,7 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 const int32_t v = decr[idx].y;
                 unsigned long long dq = 0;
                 int unst = 0;
-                const int32_t dcs = heavy_visit<LOUV, TT>(a, r, sweep, v, sh, scratch, &dq, &unst);
+                const int32_t dcs = heavy_visit<LOUV, TT, NTH>(a, r, sweep, v, sh, scratch, &dq, &unst);
                 if (threadIdx.x == 0) {
                     decr[idx] = make_int2(dcs, v);
                     if (dq) atomicAdd(&s_acc[0], dq);
@@ -783,14 +860,14 @@ __global__ __launch_bounds__(256) void k_cd_tail(CDArgs a, int sweep0, int max_s
             // apply the bucket's moves; while tracking, neighbours join the next worklist
             int moved = 0;
             if (!push && !trk) {
-                for (int64_t di = threadIdx.x; di < nk; di += TB) {
+                for (int64_t di = threadIdx.x; di < nk; di += NTH) {
                     const int2 dv = decr[di];
                     if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv.x, dv.y); ++moved; }
                 }
             } else {
                 const int t16 = threadIdx.x / TILE, l16 = threadIdx.x % TILE;
                 int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-                for (int64_t di = t16; di < nk; di += TILES) {
+                for (int64_t di = t16; di < nk; di += NTH / TILE) {
                     const int2 dv = decr[di];
                     const int32_t d = dv.x, v = dv.y;
                     if (d < 0) continue;
@@ -906,7 +983,7 @@ static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy)
     const int ev = timer_begin(c);
     // one item per block; grid = the bound wmax = n_r * ceil(S / LNT) (blocks past the
     // bucket's item count return at once)
-    k_decide_light<LOUV, TT, LT><<<(unsigned)((a.wmax + 7) & ~int64_t(7)), TB, 0, c.stream>>>(a, k, sweep);
+    k_decide_light<LOUV, TT><<<(unsigned)((a.wmax + 7) & ~int64_t(7)), TB, 0, c.stream>>>(a, k, sweep);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
     k_apply<LOUV, TT><<<dim3((unsigned)c.apply_blocks, a.n_r), TB, 0, c.stream>>>(a, k);
@@ -979,7 +1056,6 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
-    a.dbg = getenv("FC_DBG") ? atoi(getenv("FC_DBG")) : 0;
     a.aff = aff; a.list = list; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
     a.itemrep = itemrep; a.wmax = wmax;
 
@@ -1035,11 +1111,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                 FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));
                 if (c.trace) fprintf(stderr, "[fc] cd it=%d tail kernel from sweep %d\n", iteration, sweep + 1);
                 if (!louv)
-                    k_cd_tail<false, int32_t><<<rcount, TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
+                    k_cd_tail<false, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
                 else if (tot32)
-                    k_cd_tail<true, int32_t><<<rcount, TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
+                    k_cd_tail<true, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
                 else
-                    k_cd_tail<true, int64_t><<<rcount, TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
+                    k_cd_tail<true, int64_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
                 break;
             }
         }
@@ -1070,6 +1146,15 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         s->decide_bytes += db;                   // light kernel only (its time is decide_ms)
     }
     timer_end(c, 0, sl0);
+#ifdef FC_PHASE_PROF
+    {
+        unsigned long long hp[16];
+        FC_HIP(hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_phase), sizeof(hp)));
+        fprintf(stderr, "[fc] phase cycles (cumulative, sampled):");
+        for (int i = 0; i < 9; ++i) fprintf(stderr, " %llu", hp[i]);
+        fprintf(stderr, "\n");
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ transpose / renumber

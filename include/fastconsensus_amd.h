@@ -86,7 +86,7 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 #define FC_OPT_TAIL_VISITS 7 /* once a sweep visits <= this many vertices (all replicas), the
                                 remaining sweeps run in one workgroup per replica (default
-                                131072; 0 = off).  Same results either way.                   */
+                                1048576; 0 = off).  Same results either way.                   */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */
