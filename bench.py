@@ -223,7 +223,8 @@ def main():
             "phase_ms_per_step_rank0": phases,
             "consensus_wall_ms": 1e3 * elapsed / args.steps,
         }
-    print(json.dumps(result))
+    if rank == 0:
+        print(json.dumps(result))
 
 
 if __name__ == "__main__":

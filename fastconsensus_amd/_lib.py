@@ -82,7 +82,7 @@ def load():
     L.fc_run.argtypes = [vp, c_int, c_int, dbl, dbl, vp, P(Stats)]
     L.fc_cd.argtypes = [vp, c_int, c_int, c_int, c_int, c_int]
     L.fc_set_labels.argtypes = [vp, c_int, _i32p]
-    L.fc_get_labels.argtypes = [vp, _i32p, c_int]
+    L.fc_get_labels.argtypes = [vp, vp, c_int]   # host array or device buffer
     L.fc_consensus_partial.argtypes = [vp, c_int, vp]
     L.fc_consensus_apply.argtypes = [vp, c_int, c_int, dbl, dbl, vp, P(c_int), P(i64), P(i64)]
     L.fc_closure_sample.argtypes = [vp, i64, c_int, P(i64)]

@@ -15,6 +15,11 @@ OUT_OF_SCOPE = ("infomap", "leiden", "cnm")
 FINAL_PASS_ITER = 0x40000000  # iteration salt of the final pass (matches capi.cpp fc_run)
 
 
+def torch_int32():
+    import torch
+    return torch.int32
+
+
 def algo_id(algorithm):
     if algorithm in ALGORITHMS:
         return ALGORITHMS[algorithm]
@@ -135,9 +140,15 @@ class Engine:
         labels = np.ascontiguousarray(labels, dtype=np.int32)
         check(self._L.fc_set_labels(self._ctx, labels.shape[0], labels))
 
-    def get_labels(self, count, renumber=False):
+    def get_labels(self, count, renumber=False, dev_out=None):
+        """[count][n] labelings in node order: a new numpy array, or written into the device
+        tensor `dev_out` (int32, >= count*n elements) when given."""
+        if dev_out is not None:
+            assert dev_out.dtype == torch_int32() and dev_out.numel() >= count * self.n
+            check(self._L.fc_get_labels(self._ctx, ptr(dev_out), 1 if renumber else 0))
+            return dev_out
         out = np.empty((count, self.n), np.int32)
-        check(self._L.fc_get_labels(self._ctx, out, 1 if renumber else 0))
+        check(self._L.fc_get_labels(self._ctx, ptr(out), 1 if renumber else 0))
         return out
 
     def consensus_partial(self, algo, dev_out):

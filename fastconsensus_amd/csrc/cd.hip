@@ -458,18 +458,21 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     return out;
 }
 
-template <bool LOUV, typename TT>
+template <bool LOUV, typename TT, bool LOOP>
 __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
     __shared__ WaveShared s_ws[TB / 64];
-    __shared__ unsigned long long s_red[TB / 64][5];
+    __shared__ unsigned long long s_red[2][TB / 64][5];   // by item parity (no second barrier)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
     const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
-    // one item per block; XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the
-    // contiguous items [x*q, (x+1)*q), so a replica's items share an L2
-    const int64_t q = (W + 7) / 8, j = blockIdx.x >> 3;
-    const int64_t w = (blockIdx.x & 7) * q + j;
-    if (j >= q || w >= W) return;
+    // XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the contiguous items
+    // [x*q, (x+1)*q), so a replica's items share an L2.  LOOP = false: grid = the upper
+    // bound of items, one item per block (large sweeps; 64 VGPRs, 8 waves/SIMD).  LOOP =
+    // true: a small grid whose gridDim/8 blocks per XCD stride over the items (small
+    // sweeps, where a grid of mostly empty blocks would cost more than the work; the loop
+    // costs registers, which matters little there)
+    const int64_t q = (W + 7) / 8, x0 = (blockIdx.x & 7) * q, x1 = min(W, x0 + q);
+    auto item = [&](int64_t w, int par) {
     // (readfirstlane: values loaded from global memory are not known to be uniform, and a
     // vector r would move the per-replica arithmetic -- permutation keys, addresses -- to VALU)
     const int r = __builtin_amdgcn_readfirstlane(a.itemrep[(int64_t)bucket * a.wmax + w]);
@@ -507,14 +510,24 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) f4 += __shfl_xor(f4, off);
     if (lane == 0) {
-        s_red[wv][0] = f0; s_red[wv][1] = f1; s_red[wv][2] = f2; s_red[wv][3] = f3; s_red[wv][4] = f4;
+        s_red[par][wv][0] = f0; s_red[par][wv][1] = f1; s_red[par][wv][2] = f2; s_red[par][wv][3] = f3;
+        s_red[par][wv][4] = f4;
     }
     __syncthreads();
     if (threadIdx.x < 5 && rep_on) {
         unsigned long long sm = 0;
-        for (int k = 0; k < TB / 64; ++k) sm += s_red[k][threadIdx.x];
+        for (int k = 0; k < TB / 64; ++k) sm += s_red[par][k][threadIdx.x];
         // fields: s_red 0 dq -> 0, 1 unstable -> 1, 2 verts -> 3, 3 entries -> 4, 4 cands -> 5
         if (sm) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), sm);
+    }
+    };   // item
+    if constexpr (LOOP) {
+        int par = 0;
+#pragma unroll 1
+        for (int64_t w = x0 + (blockIdx.x >> 3); w < x1; w += (int64_t)(gridDim.x >> 3), par ^= 1) item(w, par);
+    } else {
+        const int64_t w = x0 + (blockIdx.x >> 3);
+        if (w < x1) item(w, 0);
     }
 }
 
@@ -978,12 +991,15 @@ __global__ __launch_bounds__(256) void k_list_offsets(int n_r, int64_t wmax, con
 // Every grid is fixed and every size is read on the device, so a sweep never waits on
 // the host.
 template <bool LOUV, typename TT>
-static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy) {
+static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy, int64_t small_grid) {
     if (any_heavy) FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     const int ev = timer_begin(c);
     // one item per block; grid = the bound wmax = n_r * ceil(S / LNT) (blocks past the
     // bucket's item count return at once)
-    k_decide_light<LOUV, TT><<<(unsigned)((a.wmax + 7) & ~int64_t(7)), TB, 0, c.stream>>>(a, k, sweep);
+    if (small_grid > 0)
+        k_decide_light<LOUV, TT, true><<<(unsigned)small_grid, TB, 0, c.stream>>>(a, k, sweep);
+    else
+        k_decide_light<LOUV, TT, false><<<(unsigned)((a.wmax + 7) & ~int64_t(7)), TB, 0, c.stream>>>(a, k, sweep);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
     k_apply<LOUV, TT><<<dim3((unsigned)c.apply_blocks, a.n_r), TB, 0, c.stream>>>(a, k);
@@ -1071,14 +1087,15 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
     const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
     int sweep = 0;
+    int64_t small_grid = 0;   // > 0: decide grid of the looping kernel, sized from sweep s-LAG's visits
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         FC_HIP(hipMemsetAsync(lcnt, 0, sizeof(int32_t) * (size_t)B * rcount, c.stream));
         k_list_build<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, B, list, lcnt);
         k_list_offsets<<<B, TB, 0, c.stream>>>(rcount, a.wmax, lcnt, blk_off, itemrep);
         for (int k = 0; k < B; ++k) {
-            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv);
-            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv);
-            else sub_round<true, int64_t>(c, a, k, sweep, hv);
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv, small_grid);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv, small_grid);
+            else sub_round<true, int64_t>(c, a, k, sweep, hv, small_grid);
         }
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
@@ -1105,6 +1122,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             if (ring[8 * chk] == 0) { ++sweep; break; }
             // small sweeps: hand every remaining sweep to the per-replica tail kernel
             const unsigned long long visits = *(unsigned long long*)(ring + 8 * chk + 6);
+            // items per bucket ~ visits / (B * LNT) + one partial item per replica; a 2x margin
+            // (sweeps shrink; the loop covers any excess)
+            const int64_t est = (int64_t)visits / ((int64_t)B * LNT) + rcount;
+            small_grid = (4 * est < a.wmax) ? std::max<int64_t>(64, ((2 * est + 7) / 8) * 8) : 0;
             if (c.tail_visits > 0 && (int64_t)visits <= c.tail_visits && B <= TAIL_MAXB && sweep + 1 < c.max_sweeps) {
                 int32_t* tbuf = ensure<int32_t>(c.tailbuf, (size_t)rcount * 3 * N);
                 int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
@@ -1230,7 +1251,8 @@ void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
         exclusive_scan(c, flag, rank, total + 1);
         k_relabel_out<<<nblk(total), TB, 0, c.stream>>>(N, total, out, first, rank);
     }
-    FC_HIP(hipMemcpyAsync(host, out, 4 * (size_t)total, hipMemcpyDeviceToHost, c.stream));
+    // hipMemcpyDefault: `host` may be host memory or a device buffer (distributed gather)
+    FC_HIP(hipMemcpyAsync(host, out, 4 * (size_t)total, hipMemcpyDefault, c.stream));
     sync(c);
 }
 __global__ void k_from_node_order(int64_t N, int64_t total, const int32_t* in, const int32_t* sigma, int32_t* lab) {

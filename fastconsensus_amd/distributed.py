@@ -23,6 +23,10 @@ from .core import FINAL_PASS_ITER
 LOUVAIN = 0
 
 
+def on_device(t):
+    return t.device.type == "cuda"
+
+
 def shard(n_p, rank, world):
     return n_p * rank // world, n_p * (rank + 1) // world
 
@@ -90,18 +94,19 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
     m = engine.m
     st["partition_edges"] += n_p * m
     st["m_final"] = m
-    local = None
     if mine > 0:
         engine.cd(algo, r0, mine, n_p, FINAL_PASS_ITER + it)         # final pass :383-392
-        local = engine.get_labels(mine, renumber=True)
-    if not gather:
-        return local, st
-    if world == 1:
-        return local, st
+    if not gather or world == 1:
+        return (engine.get_labels(mine, renumber=True) if mine > 0 else None), st
+    # final partitions: exported straight into the gather buffer (no host round trip), one
+    # all-gather, one download on rank 0
     cap = max(shard(n_p, g, world)[1] - shard(n_p, g, world)[0] for g in range(world))
     buf = torch.full((cap, n), -1, dtype=torch.int32, device=device)
     if mine > 0:
-        buf[:mine].copy_(torch.from_numpy(local))
+        if on_device(buf):
+            engine.get_labels(mine, renumber=True, dev_out=buf)
+        else:
+            buf[:mine].copy_(torch.from_numpy(engine.get_labels(mine, renumber=True)))
     bufs = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf)
     if rank != 0:

@@ -122,7 +122,8 @@ int fc_cd(fc_ctx* ctx, int algo, int replica_begin, int replica_count, int n_p_t
           int iteration);
 /* Replay: install host labelings [count][n] as the local replicas (begin = 0). */
 int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels);
-/* Download local labelings [count][n]; renumber != 0 -> ids 0..k-1 by first node. */
+/* Download local labelings [count][n] (in node order) into host memory or a device buffer of
+ * the context's GPU; renumber != 0 -> ids 0..k-1 by first node. */
 int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber);
 /* Per-edge partial over the local replicas into caller device buffer dev_out (int32[m]):
  * louvain -> largest global replica index whose labels split the edge, or -1
