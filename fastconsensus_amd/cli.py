@@ -9,7 +9,8 @@ import argparse
 import os
 import sys
 
-from .core import ALGORITHMS, OUT_OF_SCOPE, Engine, IdGraph, algo_id, labels_to_output
+from ._lib import FC_ALGO_LOUVAIN, FC_ALGO_LOUVAIN_NC
+from .core import ALGORITHMS, OUT_OF_SCOPE, RULES, Engine, IdGraph, algo_id, labels_to_output
 
 DEFAULT_TAU = {'louvain': 0.2, 'cnm': 0.7, 'infomap': 0.6, 'lpm': 0.8}   # :426
 
@@ -44,6 +45,8 @@ def build_parser():
                    help='choose from \'louvain\' , \'cnm\' , \'lpm\' , \'infomap\' ')
     p.add_argument('--seed', type=int, default=None, help=argparse.SUPPRESS)
     p.add_argument('--device', type=int, default=0, help=argparse.SUPPRESS)
+    # extension: the new_consensus.py fork's weight rule (:155-163), louvain only
+    p.add_argument('--rule', type=str, default='fast_consensus', choices=RULES, help=argparse.SUPPRESS)
     return p
 
 
@@ -84,6 +87,8 @@ def main(argv=None):
     if algo is None:
         output = None
     else:
+        if args.rule == 'new_consensus' and algo == FC_ALGO_LOUVAIN:
+            algo = FC_ALGO_LOUVAIN_NC
         with Engine(device=args.device, seed=args.seed) as eng:
             eng.load_graph(g.n, g.u, g.v)
             labels, _ = eng.run(algo, args.np, args.t, args.d)

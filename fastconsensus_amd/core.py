@@ -8,9 +8,12 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import FC_ALGO_LOUVAIN, FC_ALGO_LPM, FastConsensusError, Stats, check, ptr
+from ._lib import FC_ALGO_LOUVAIN, FC_ALGO_LOUVAIN_NC, FC_ALGO_LPM, FastConsensusError, Stats, check, ptr
 
 ALGORITHMS = {"louvain": FC_ALGO_LOUVAIN, "lpm": FC_ALGO_LPM}
+# consensus weight rules: fast_consensus.py (the named entry point) or the new_consensus.py
+# fork's plain count that keeps converged edges (:155-163); louvain only
+RULES = ("fast_consensus", "new_consensus")
 OUT_OF_SCOPE = ("infomap", "leiden", "cnm")
 FINAL_PASS_ITER = 0x40000000  # iteration salt of the final pass (matches capi.cpp fc_run)
 
@@ -245,18 +248,25 @@ def labels_to_output(algorithm, node_labels, labels):
 
 
 def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, seed=None, device=0,
-                   return_stats=False):
+                   return_stats=False, rule="fast_consensus"):
     """Drop-in for fast_consensus.py:129 ``fast_consensus(G, algorithm, n_p, thresh, delta)``.
 
     G: an undirected networkx Graph (weights are ignored: the reference resets them to 1,
     :135-136) or an ``IdGraph``.  Returns a list of n_p partitions -- dicts for louvain,
     sets of frozensets for lpm -- or None for an unknown algorithm (the reference's loop
     ``break``s and returns None, :380-381).  ``seed`` makes the run reproducible (the
-    reference is unseeded).
+    reference is unseeded).  ``rule="new_consensus"`` (louvain only) switches to the
+    new_consensus.py fork's weight rule (:155-163).
     """
     algo = algo_id(algorithm)
     if algo is None:
         return None
+    if rule not in RULES:
+        raise ValueError("rule must be one of %s" % (RULES,))
+    if rule == "new_consensus":
+        if algo != FC_ALGO_LOUVAIN:
+            raise ValueError("the new_consensus.py rule exists for louvain only")
+        algo = FC_ALGO_LOUVAIN_NC
     g = G if isinstance(G, IdGraph) else IdGraph.from_networkx(G)
     with Engine(device=device, seed=seed) as eng:
         eng.load_graph(g.n, g.u, g.v)

@@ -240,7 +240,7 @@ int fc_get_nextgraph(fc_ctx* ctx, int64_t* m_out, int32_t* u, int32_t* v, int32_
 int fc_cd(fc_ctx* ctx, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(algo == FC_ALGO_LOUVAIN || algo == FC_ALGO_LPM, FC_EINVAL, "algo must be louvain or lpm");
+    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM, FC_EINVAL, "algo must be louvain or lpm");
     cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
     FC_API_END
 }
@@ -280,7 +280,7 @@ int fc_consensus_apply(fc_ctx* ctx, int algo, int n_p, double tau, double delta,
     int64_t kept = 0, unc = 0;
     consensus_apply(c, algo, n_p, tau, (const int32_t*)dev_partial, &kept, &unc);
     // check_consensus_graph (:34): not converged iff count > delta * number_of_edges
-    if (converged) *converged = (algo == FC_ALGO_LOUVAIN) ? !((double)unc > delta * (double)kept) : 0;
+    if (converged) *converged = is_louvain(algo) ? !((double)unc > delta * (double)kept) : 0;
     if (kept_out) *kept_out = kept;
     if (unconv_out) *unconv_out = unc;
     FC_API_END
@@ -322,7 +322,7 @@ int fc_closure_apply(fc_ctx* ctx, int algo, int n_p, double delta, const void* d
                      int* converged, int64_t* m_out) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(algo != FC_ALGO_LOUVAIN || dev_counts || c.n_cand == 0, FC_EINVAL,
+    FC_REQUIRE(!is_louvain(algo) || dev_counts || c.n_cand == 0, FC_EINVAL,
                "louvain closure needs co-membership counts");
     closure_apply(c, algo, n_p, (const int32_t*)dev_counts, iteration);
     const int64_t unc = count_unconverged(c, c.g.ew.as<int32_t>(), c.g.m, n_p);
@@ -341,11 +341,11 @@ int fc_collect_timing(fc_ctx* ctx, fc_stats* st) {
 int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* labels_out, fc_stats* st) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(algo == FC_ALGO_LOUVAIN || algo == FC_ALGO_LPM, FC_EINVAL,
+    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM, FC_EINVAL,
                "algorithm must be louvain or lpm (infomap/leiden/cnm are out of scope)");
     FC_REQUIRE(n_p >= 1, FC_EINVAL, "n_p must be >= 1");
     FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
-    const bool louv = algo == FC_ALGO_LOUVAIN;
+    const bool louv = is_louvain(algo);
     graph_copy(c, c.g, c.g0);                                         // graph = G.copy() (:131)
     c.acc = fc_stats{};
     fc_stats& a = c.acc;

@@ -1009,7 +1009,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
     FC_REQUIRE(c.g.rowptr.p, FC_ESTATE, "no graph loaded");
     const int sl0 = timer_begin(c);
-    const bool louv = algo == FC_ALGO_LOUVAIN;
+    const bool louv = is_louvain(algo);
     const int64_t N = c.N;
     Graph& g = c.g;
     c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;

@@ -82,7 +82,7 @@ void consensus_partial(Ctx& c, int algo, int32_t* out) {
     FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings: run fc_cd or fc_set_labels first");
     if (!c.labT_valid) labels_transpose(c);
     const int sl = timer_begin(c);
-    if (algo == FC_ALGO_LOUVAIN)
+    if (algo == FC_ALGO_LOUVAIN)   // k_last; LPM and the new_consensus.py rule: co-membership count
         launch_pair_partial<true>(c, c.g.m, c.g.eu.as<int32_t>(), c.g.ev.as<int32_t>(), out);
     else
         launch_pair_partial<false>(c, c.g.m, c.g.eu.as<int32_t>(), c.g.ev.as<int32_t>(), out);
@@ -93,9 +93,10 @@ void consensus_partial(Ctx& c, int algo, int32_t* out) {
 // Closed form of the Louvain rule (fast_consensus.py:150-159), proven equal to the
 // literal loop in tests/test_oracle_golden.py: w in {0,n_p} -> 0; no split -> n_p;
 // else w + (n_p - 1 - k_last).  LPM (:273-280): the co-membership count.
+// new_consensus.py rule (:155-163, FC_ALGO_LOUVAIN_NC): w in {0,n_p} -> w, else the count.
 // keep iff !(w' < tau*n_p) in float64 (:165, :286).  Counts kept and "unconverged"
 // (w' not in {0, n_p}, check_consensus_graph :30-32) per block -> one atomic per block.
-__global__ __launch_bounds__(256) void k_consensus_apply(int louvain, int64_t m, int n_p, double cut,
+__global__ __launch_bounds__(256) void k_consensus_apply(int algo, int64_t m, int n_p, double cut,
                                                          const int32_t* __restrict__ ew,
                                                          const int32_t* __restrict__ part,
                                                          int32_t* __restrict__ wnew, int64_t* __restrict__ flag,
@@ -104,10 +105,13 @@ __global__ __launch_bounds__(256) void k_consensus_apply(int louvain, int64_t m,
     int keep = 0, unc = 0;
     if (e < m) {
         int nw;
-        if (louvain) {
+        if (algo == FC_ALGO_LOUVAIN) {
             const int w = ew[e];
             const int k = part[e];
             nw = (w == 0 || w == n_p) ? 0 : (k < 0 ? n_p : w + (n_p - 1 - k));
+        } else if (algo == FC_ALGO_LOUVAIN_NC) {
+            const int w = ew[e];
+            nw = (w == 0 || w == n_p) ? w : part[e];
         } else {
             nw = part[e];
         }
@@ -167,7 +171,7 @@ void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* parti
     unsigned long long* ctr = shards_begin(c, 2);
     const double cut = tau * (double)n_p;  // Python float64 product (fast_consensus.py:165)
     if (m > 0)
-        k_consensus_apply<<<nblk(m), TB, 0, c.stream>>>(algo == FC_ALGO_LOUVAIN, m, n_p, cut, g.ew.as<int32_t>(),
+        k_consensus_apply<<<nblk(m), TB, 0, c.stream>>>(algo, m, n_p, cut, g.ew.as<int32_t>(),
                                                          partial, wnew, flag, ctr);
     FC_HIP(hipMemsetAsync(flag + m, 0, sizeof(int64_t), c.stream));
     exclusive_scan(c, flag, pos, m + 1);
@@ -478,10 +482,10 @@ int64_t count_unconverged(Ctx& c, const int32_t* w, int64_t m, int n_p) {
 void closure_apply(Ctx& c, int algo, int n_p, const int32_t* counts, int iteration) {
     int sl = timer_begin(c);
     if (c.n_cand > 0)
-        k_closure_weights<<<nblk(c.n_cand), TB, 0, c.stream>>>(c.n_cand, algo == FC_ALGO_LOUVAIN, counts,
+        k_closure_weights<<<nblk(c.n_cand), TB, 0, c.stream>>>(c.n_cand, is_louvain(algo), counts,
                                                                c.cw2.as<int32_t>());
     int64_t nrep = 0;
-    if (algo == FC_ALGO_LOUVAIN) nrep = repair(c, iteration);  // lpm has no repair (:260-310)
+    if (is_louvain(algo)) nrep = repair(c, iteration);  // lpm has no repair (:260-310)
     timer_end(c, 2, sl);
     sl = timer_begin(c);
     graph_merge_next(c, c.n_cand + nrep);

@@ -12,6 +12,10 @@ namespace fc {
 
 void set_error(const std::string& msg);
 
+// Louvain community detection + louvain consensus loop (closure counts, isolate repair,
+// check #1): FC_ALGO_LOUVAIN and its new_consensus.py weight-rule variant.
+inline bool is_louvain(int algo) { return algo == FC_ALGO_LOUVAIN || algo == FC_ALGO_LOUVAIN_NC; }
+
 struct FcError {
     int code;
     std::string msg;

@@ -20,7 +20,7 @@ import torch.distributed as dist
 
 from .core import FINAL_PASS_ITER
 
-LOUVAIN = 0
+LOUVAIN, LPM, LOUVAIN_NC = 0, 1, 2
 
 
 def on_device(t):
@@ -36,7 +36,7 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     r0, r1 = shard(n_p, rank, world)
-    louv = algo == LOUVAIN
+    louv = algo in (LOUVAIN, LOUVAIN_NC)    # louvain loop: check #1, closure counts, repair
     on_gpu = str(device).startswith("cuda")
     if not on_gpu:
         return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv)
@@ -69,9 +69,9 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
             engine.cd(algo, r0, mine, n_p, it)                       # :148 / :270
             engine.consensus_partial(algo, part)                     # :150-159 / :273-280
         else:
-            part.fill_(-1 if louv else 0)
-        if world > 1:
-            dist.all_reduce(part, op=dist.ReduceOp.MAX if louv else dist.ReduceOp.SUM)
+            part.fill_(-1 if algo == LOUVAIN else 0)
+        if world > 1:   # louvain: k_last (MAX); lpm / new_consensus rule: counts (SUM)
+            dist.all_reduce(part, op=dist.ReduceOp.MAX if algo == LOUVAIN else dist.ReduceOp.SUM)
         st["partition_edges"] += n_p * m
         conv1, kept, unc = engine.consensus_apply(algo, n_p, tau, delta, part)   # :163-173
         if louv and conv1:

@@ -37,6 +37,9 @@ extern "C" {
 
 #define FC_ALGO_LOUVAIN 0 /* fast_consensus.py:141-202 (+ final pass :383-384) */
 #define FC_ALGO_LPM 1     /* fast_consensus.py:260-310 (+ final pass :391-392) */
+#define FC_ALGO_LOUVAIN_NC 2 /* louvain with new_consensus.py's weight rule (:155-163): an edge of
+                                weight w not in {0,n_p} gets the plain co-membership count,
+                                others keep w; everything else as FC_ALGO_LOUVAIN */
 
 typedef struct fc_ctx fc_ctx;
 
@@ -127,7 +130,8 @@ int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels);
 int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber);
 /* Per-edge partial over the local replicas into caller device buffer dev_out (int32[m]):
  * louvain -> largest global replica index whose labels split the edge, or -1
- * (reduce with MAX); lpm -> number of local replicas co-clustering it (reduce with SUM). */
+ * (reduce with MAX); lpm and louvain_nc -> number of local replicas co-clustering it
+ * (reduce with SUM). */
 int fc_consensus_partial(fc_ctx* ctx, int algo, void* dev_out);
 /* Apply the reduced partial: consensus weight rule (:150-159 / :273-280), threshold
  * (:163-168 / :284-288) and, for louvain, check #1 (:172).  kept_out/unconv_out: counts. */

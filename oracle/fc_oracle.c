@@ -50,7 +50,10 @@ static void shuffle_i32(i32* a, i64 n, u64* s) {
  *   nextgraph weight starts at 0 (:145-146); if graph weight not in (0, n_p) (:153):
  *   for each partition i: same community -> += 1 (:156-157), else -> = old weight (:159).
  * LPM branch, fast_consensus.py:273-280: count of partitions with u, v co-clustered.
- * labels are replica-major [n_p][N].  algo: 0 = louvain, 1 = lpm.
+ * algo 2: the new_consensus.py fork's louvain rule (new_consensus.py:155-163, literal):
+ *   nextgraph weight starts at 0 (:149-150); if graph weight not in (0, n_p) (:157):
+ *   += 1 per partition that co-clusters (:158-160); else (:161-163) -> = graph weight.
+ * labels are replica-major [n_p][N].  algo: 0 = louvain, 1 = lpm, 2 = louvain (new rule).
  */
 void orc_consensus(int algo, i64 m, const i32* eu, const i32* ev, const i32* w_in, int n_p,
                    i64 N, const i32* lab, i32* w_out) {
@@ -65,6 +68,14 @@ void orc_consensus(int algo, i64 m, const i32* eu, const i32* ev, const i32* w_i
                     if (lab[(i64)i * N + u] == lab[(i64)i * N + v]) nw += 1;
                     else nw = w;
                 }
+            }
+        } else if (algo == 2) {
+            const i32 w = w_in[e];
+            if (w != 0 && w != n_p) {
+                for (int i = 0; i < n_p; ++i)
+                    if (lab[(i64)i * N + u] == lab[(i64)i * N + v]) nw += 1;
+            } else {
+                nw = w;
             }
         } else {
             for (int i = 0; i < n_p; ++i) nw += (lab[(i64)i * N + u] == lab[(i64)i * N + v]);

@@ -24,7 +24,12 @@ _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
 _lib = None
 
-LOUVAIN, LPM = 0, 1
+LOUVAIN, LPM, LOUVAIN_NC = 0, 1, 2   # LOUVAIN_NC: louvain with new_consensus.py's rule (:155-163)
+
+
+def _cd_algo(algo):
+    """Community-detection algorithm of a loop variant (the new_consensus.py rule runs Louvain)."""
+    return LPM if algo == LPM else LOUVAIN
 AGE_ITER_SHIFT = 40          # closure/repair edges created in iteration b get ages >= (b+1) << 40
 AGE_REPAIR_OFFSET = 1 << 39
 
@@ -172,7 +177,8 @@ def closure_from_pairs(algo, g, pairs, labels, n_p):
     ou, ov, ow = (np.empty(max(P, 1), np.int32) for _ in range(3))
     of = np.empty(max(P, 1), np.int64)
     labels = _c(labels, np.int32)
-    k = lib().orc_closure_pairs(algo, g.m, g.u, g.v, P, pairs.reshape(-1), n_p, g.N, labels, ou, ov, ow, of)
+    k = lib().orc_closure_pairs(_cd_algo(algo), g.m, g.u, g.v, P, pairs.reshape(-1), n_p, g.N, labels, ou, ov, ow,
+                                of)
     return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), of[:k].copy()
 
 
@@ -201,7 +207,7 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)
-    lib().orc_cd_batch(algo, n_r, g.N, rowptr, col, cw, int(seed) & (2**64 - 1), lab, sw, int(nthreads))
+    lib().orc_cd_batch(_cd_algo(algo), n_r, g.N, rowptr, col, cw, int(seed) & (2**64 - 1), lab, sw, int(nthreads))
     return lab, sw
 
 
@@ -211,7 +217,7 @@ def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, 
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)
-    lib().orc_engine_cd(algo, g.N, rowptr, col, cw, n_r, rbase, iteration, int(seed) & (2**64 - 1), buckets,
+    lib().orc_engine_cd(_cd_algo(algo), g.N, rowptr, col, cw, n_r, rbase, iteration, int(seed) & (2**64 - 1), buckets,
                         max_sweeps, chunk, prune, lab, sw)
     return lab, sw
 
@@ -247,7 +253,7 @@ def iterate(algo, graph, labels, pairs, n_p, tau, delta, it):
     trace["keep"] = keep
     trace["kept"] = kept
     base = np.int64(it + 1) << AGE_ITER_SHIFT
-    if algo == LOUVAIN:
+    if algo != LPM:
         conv1, cnt1 = check(kept.w, n_p, delta)
         trace["check1"] = (conv1, cnt1)
         if conv1:
@@ -256,7 +262,7 @@ def iterate(algo, graph, labels, pairs, n_p, tau, delta, it):
     closure = EdgeGraph(graph.N, cu, cv, cw, base + cf)
     trace["closure"] = closure
     parts = [kept, closure]
-    if algo == LOUVAIN:
+    if algo != LPM:
         deg = kept.degrees() + closure.degrees()
         ru, rv, rw, rx = repair(graph, deg)
         rep = EdgeGraph(graph.N, ru, rv, rw, base + AGE_REPAIR_OFFSET + rx)

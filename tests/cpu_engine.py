@@ -67,13 +67,15 @@ class OracleEngine:
         p = part.numpy()[:g.m].astype(np.int64)
         if algo == 0:
             nw = np.where((g.w == 0) | (g.w == n_p), 0, np.where(p < 0, n_p, g.w + n_p - 1 - p))
+        elif algo == 2:                               # new_consensus.py:155-163
+            nw = np.where((g.w == 0) | (g.w == n_p), g.w, p)
         else:
             nw = p
         nw = nw.astype(np.int32)
         keep = orc.threshold(nw, tau, n_p)
         self.kept = orc.EdgeGraph(g.N, g.u[keep], g.v[keep], nw[keep], g.age[keep])
         conv, cnt = orc.check(self.kept.w, n_p, delta)
-        return (conv if algo == 0 else False), self.kept.m, cnt
+        return (conv if algo != 1 else False), self.kept.m, cnt
 
     def closure_sample(self, attempts, iteration):
         pairs = orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration)
@@ -90,11 +92,11 @@ class OracleEngine:
     def closure_apply(self, algo, n_p, delta, counts, iteration):
         cu, cv, cf = self.cand
         base = np.int64(iteration + 1) << orc.AGE_ITER_SHIFT
-        w = counts.numpy()[:len(cu)].astype(np.int32) if (algo == 0 and counts is not None) else \
+        w = counts.numpy()[:len(cu)].astype(np.int32) if (algo != 1 and counts is not None) else \
             np.zeros(len(cu), np.int32)
         closure = orc.EdgeGraph(self.g.N, cu, cv, w, base + cf)
         parts = [self.kept, closure]
-        if algo == 0:
+        if algo != 1:
             deg = self.kept.degrees() + closure.degrees()
             ru, rv, rw, rx = orc.repair(self.g, deg, self.sigma)
             parts.append(orc.EdgeGraph(self.g.N, ru, rv, rw, base + orc.AGE_REPAIR_OFFSET + rx))

@@ -22,8 +22,13 @@ at each iteration start, and every graph passed to ``check_consensus_graph``
 closure pairs through our implementation must reproduce every recorded graph
 bit-exactly (weights, keep masks, convergence decisions, closure/repair edges).
 
-Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz, *.json)
+The same harness runs the ``new_consensus.py`` fork (its weight rule, :155-163, is the
+``louvain_nc`` variant).
+
+Usage:  python tests/golden/make_golden.py [nc]   (writes tests/golden/*.npz, *.json;
+        ``nc``: only the new_consensus.py cases)
 """
+import contextlib
 import importlib.util
 import io
 import json
@@ -40,6 +45,7 @@ import networkx as nx
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = "/root/reference/fast_consensus.py"
+REF_NC = "/root/reference/new_consensus.py"   # fork with the plain-count weight rule (:155-163)
 KARATE = "/root/reference/examples/karate_club.txt"
 sys.dont_write_bytecode = True
 
@@ -183,11 +189,11 @@ class _RecordingRandom:
         return out
 
 
-def load_reference():
+def load_reference(path=REF):
     sys.modules["community"] = community_stub
     sys.modules["igraph"] = igraph_stub
     sys.modules["leidenalg"] = types.ModuleType("leidenalg")
-    spec = importlib.util.spec_from_file_location("fc_reference", REF)
+    spec = importlib.util.spec_from_file_location("fc_reference_%d" % len(path), path)
     fc = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fc)
     orig_check = fc.check_consensus_graph
@@ -205,7 +211,7 @@ def load_reference():
     return fc
 
 
-def run_case(fc, name, edgefile, algorithm, n_p, tau, delta, seed, max_iters=30):
+def run_case(fc, name, edgefile, algorithm, n_p, tau, delta, seed, max_iters=30, rule="fast_consensus"):
     G = nx.read_edgelist(edgefile, nodetype=int)
     nodes = list(G.nodes())
     REC.reset({v: i for i, v in enumerate(nodes)})
@@ -213,7 +219,8 @@ def run_case(fc, name, edgefile, algorithm, n_p, tau, delta, seed, max_iters=30)
     REC.max_calls = n_p * (max_iters + 1)
     random.seed(seed)
     np.random.seed(seed)
-    out = fc.fast_consensus(G, algorithm=algorithm, n_p=n_p, thresh=tau, delta=delta)
+    with contextlib.redirect_stdout(io.StringIO()):   # new_consensus.py prints progress
+        out = fc.fast_consensus(G, algorithm=algorithm, n_p=n_p, thresh=tau, delta=delta)
     n_cd = len(REC.cd_labels)
     assert n_cd % n_p == 0
     n_batches = n_cd // n_p
@@ -257,7 +264,9 @@ def run_case(fc, name, edgefile, algorithm, n_p, tau, delta, seed, max_iters=30)
         "n_cd_batches": n_batches, "check_results": check_meta,
         "n_checks": len(REC.checks),
         "stand_in": "networkx %s louvain_partitions level0 / asyn_lpa_communities" % nx.__version__,
-        "reference": "fast_consensus.py (ytabatabaee/fastconsensus @ 2025-02-25)",
+        "reference": "%s (ytabatabaee/fastconsensus @ 2025-02-25)" % (
+            "fast_consensus.py" if rule == "fast_consensus" else "new_consensus.py"),
+        "rule": rule,
     }
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
     with open(os.path.join(HERE, name + ".json"), "w") as f:
@@ -344,7 +353,18 @@ def make_lfr1k():
     return path
 
 
+def main_nc():
+    """Cases of the new_consensus.py rule only (existing fixtures untouched)."""
+    karate = os.path.join(HERE, "karate_club.txt")
+    lfr = os.path.join(HERE, "lfr1k_mu04.txt")
+    nc = load_reference(REF_NC)
+    run_case(nc, "karate_louvain_nc_np50", karate, "louvain", 50, 0.2, 0.1, seed=11, rule="new_consensus")
+    run_case(nc, "lfr1k_louvain_nc_np20", lfr, "louvain", 20, 0.2, 0.02, seed=13, rule="new_consensus")
+
+
 def main():
+    if sys.argv[1:] == ["nc"]:
+        return main_nc()
     shutil.copy(KARATE, os.path.join(HERE, "karate_club.txt"))
     karate = os.path.join(HERE, "karate_club.txt")
     lfr = make_lfr1k()
@@ -356,6 +376,7 @@ def main():
     run_cli_case("cli_karate_louvain", karate, ["--alg", "louvain", "-np", "10", "-t", "0.2", "-d", "0.1"], seed=5)
     run_cli_case("cli_karate_lpm", karate, ["--alg", "lpm", "-np", "5"], seed=6)
     run_arg_errors()
+    main_nc()
 
 
 if __name__ == "__main__":

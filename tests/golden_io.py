@@ -5,7 +5,8 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["karate_louvain_np50", "karate_lpm_np20", "lfr1k_louvain_np20", "lfr1k_lpm_np20"]
+CASES = ["karate_louvain_np50", "karate_lpm_np20", "lfr1k_louvain_np20", "lfr1k_lpm_np20",
+         "karate_louvain_nc_np50", "lfr1k_louvain_nc_np20"]   # nc: new_consensus.py's weight rule
 
 
 class Case:
@@ -15,7 +16,8 @@ class Case:
         z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
         self.z = {k: z[k] for k in z.files}
         self.name = name
-        self.algo = 0 if self.meta["algorithm"] == "louvain" else 1
+        # 0 louvain, 1 lpm, 2 louvain with the new_consensus.py rule (FC_ALGO_LOUVAIN_NC)
+        self.algo = 1 if self.meta["algorithm"] == "lpm" else (2 if self.meta.get("rule") == "new_consensus" else 0)
         self.n_p = self.meta["n_p"]
         self.tau = self.meta["tau"]
         self.delta = self.meta["delta"]

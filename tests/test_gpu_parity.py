@@ -54,7 +54,7 @@ def test_replay_golden_through_capi(fcmod, name):
         tr = otraces[it]
         np.testing.assert_array_equal(kw, tr["kept"].w)
         np.testing.assert_array_equal(kage, tr["kept"].age)
-        if case.algo == 0:
+        if case.algo != 1:
             assert as_dict(ku, kv, kw) == case.check_dict(c)
             assert conv1 == case.checks[c][1]
             c += 1
@@ -63,9 +63,9 @@ def test_replay_golden_through_capi(fcmod, name):
         ncand = eng.closure_set_pairs(case.pair_batches[it], it)
         assert ncand == tr["closure"].m
         cnt = dev_i32(ncand)
-        if ncand and case.algo == 0:
+        if ncand and case.algo != 1:
             eng.closure_partial(cnt)
-        conv2, m_new = eng.closure_apply(case.algo, case.n_p, case.delta, cnt if case.algo == 0 else None, it)
+        conv2, m_new = eng.closure_apply(case.algo, case.n_p, case.delta, cnt if case.algo != 1 else None, it)
         u, v, w, age = eng.get_graph()
         assert as_dict(u, v, w) == case.check_dict(c)
         g2 = ograph[it + 1]
@@ -328,7 +328,8 @@ def test_closure_sampler_properties(fcmod):
 @pytest.mark.parametrize("algo,n_p,tau,chunk,prune,relabel,tail",
                          [(0, 10, 0.2, 0, 0, 0, 0), (0, 12, 0.2, 16, 0, 1, 131072), (1, 4, 0.8, 0, 0, 0, 131072),
                           (0, 20, 0.2, 0, 0, 1, 0), (0, 10, 0.2, 0, 1, 1, 131072), (1, 6, 0.8, 16, 1, 1, 0),
-                          (1, 6, 0.8, 16, 1, 1, 131072), (0, 10, 0.2, 16, 1, 1, 0), (0, 10, 0.2, 16, 1, 1, 131072)])
+                          (1, 6, 0.8, 16, 1, 1, 131072), (0, 10, 0.2, 16, 1, 1, 0), (0, 10, 0.2, 16, 1, 1, 131072),
+                          (2, 10, 0.2, 16, 1, 1, 131072), (2, 12, 0.2, 0, 0, 0, 0)])
 def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel, tail):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
     loop (bucketed CD twin, consensus rule, Philox closure sampler, repair, ages): final
