@@ -105,6 +105,7 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) in production; gloo to rehearse N>1 on one GPU")
     ap.add_argument("--prune", type=int, default=-1, help="CD vertex pruning (engine option; -1 = default)")
     ap.add_argument("--relabel", type=int, default=-1, help="internal vertex numbering (engine option; -1 = default)")
+    ap.add_argument("--coarsen", type=int, default=-1, help="experimental coarse rounds, largest g (engine option)")
     ap.add_argument("--ids", default="generator", choices=["generator", "planted"],
                     help="experiment: renumber node ids by planted community before loading")
     args = ap.parse_args()
@@ -146,6 +147,8 @@ def main():
         eng.set_option("prune", args.prune)
     if args.relabel >= 0:
         eng.set_option("relabel", args.relabel)
+    if args.coarsen >= 0:
+        eng.set_option("coarsen", args.coarsen)
     t0 = time.time()
     eng.load_graph(n, u, v)
     torch.cuda.synchronize()

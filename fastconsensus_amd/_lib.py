@@ -14,12 +14,13 @@ LIB_PATH = os.environ.get("FC_LIB_PATH") or os.path.join(PKG, "lib", "libfastcon
 FC_ALGO_LOUVAIN = 0
 FC_ALGO_LPM = 1
 FC_ALGO_LOUVAIN_NC = 2   # louvain with new_consensus.py's weight rule (:155-163)
-OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6, "tail_visits": 7}
+OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6, "tail_visits": 7,
+           "coarsen": 8}
 ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 
 # Every symbol declared in include/fastconsensus_amd.h (checked by tests/test_capi_symbols.py)
 SYMBOLS = [
-    "fc_last_error", "fc_version", "fc_create", "fc_destroy", "fc_set_stream", "fc_set_timing",
+    "fc_last_error", "fc_version", "fc_create", "fc_destroy", "fc_set_stream", "fc_synchronize", "fc_set_timing",
     "fc_collect_timing", "fc_set_params", "fc_set_option", "fc_load_graph", "fc_graph_info", "fc_get_node_map", "fc_reset_graph", "fc_get_graph", "fc_get_nextgraph", "fc_run",
     "fc_cd", "fc_set_labels", "fc_get_labels", "fc_consensus_partial", "fc_consensus_apply",
     "fc_closure_sample", "fc_closure_set_pairs", "fc_closure_partial", "fc_closure_apply",
@@ -70,6 +71,7 @@ def load():
     L.fc_destroy.argtypes = [vp]
     L.fc_destroy.restype = None
     L.fc_set_stream.argtypes = [vp, vp]
+    L.fc_synchronize.argtypes = [vp]
     L.fc_set_timing.argtypes = [vp, c_int]
     L.fc_collect_timing.argtypes = [vp, P(Stats)]
     L.fc_set_params.argtypes = [vp, c_int, c_int, c_int]

@@ -65,6 +65,22 @@ class Engine:
 
     def set_stream(self, stream_handle):
         check(self._L.fc_set_stream(self._ctx, stream_handle))
+        self._shared_stream = stream_handle is not None
+
+    def _dev(self, t):
+        """Address of a caller device buffer.  Unless the engine runs on the caller's stream
+        (set_stream), the work queued on that buffer by torch (e.g. the zero fill of
+        torch.zeros) is drained first: the engine's own stream is not ordered after it."""
+        if t is not None and not getattr(self, "_shared_stream", False) and hasattr(t, "is_cuda") and t.is_cuda:
+            import torch
+            torch.cuda.current_stream(t.device).synchronize()
+        return ptr(t)
+
+    def _written(self):
+        """After a step that wrote a caller device buffer: unless the engine runs on the
+        caller's stream, wait for it, so that torch may read the buffer on its own stream."""
+        if not getattr(self, "_shared_stream", False):
+            check(self._L.fc_synchronize(self._ctx))
 
     def set_timing(self, on=True):
         check(self._L.fc_set_timing(self._ctx, 1 if on else 0))
@@ -148,19 +164,20 @@ class Engine:
         tensor `dev_out` (int32, >= count*n elements) when given."""
         if dev_out is not None:
             assert dev_out.dtype == torch_int32() and dev_out.numel() >= count * self.n
-            check(self._L.fc_get_labels(self._ctx, ptr(dev_out), 1 if renumber else 0))
+            check(self._L.fc_get_labels(self._ctx, self._dev(dev_out), 1 if renumber else 0))
             return dev_out
         out = np.empty((count, self.n), np.int32)
         check(self._L.fc_get_labels(self._ctx, ptr(out), 1 if renumber else 0))
         return out
 
     def consensus_partial(self, algo, dev_out):
-        check(self._L.fc_consensus_partial(self._ctx, int(algo), ptr(dev_out)))
+        check(self._L.fc_consensus_partial(self._ctx, int(algo), self._dev(dev_out)))
+        self._written()
 
     def consensus_apply(self, algo, n_p, tau, delta, dev_partial):
         conv, kept, unc = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
         check(self._L.fc_consensus_apply(self._ctx, int(algo), int(n_p), float(tau), float(delta),
-                                         ptr(dev_partial), ctypes.byref(conv), ctypes.byref(kept),
+                                         self._dev(dev_partial), ctypes.byref(conv), ctypes.byref(kept),
                                          ctypes.byref(unc)))
         return bool(conv.value), kept.value, unc.value
 
@@ -176,11 +193,12 @@ class Engine:
         return nc.value
 
     def closure_partial(self, dev_out):
-        check(self._L.fc_closure_partial(self._ctx, ptr(dev_out)))
+        check(self._L.fc_closure_partial(self._ctx, self._dev(dev_out)))
+        self._written()
 
     def closure_apply(self, algo, n_p, delta, dev_counts, iteration):
         conv, m = ctypes.c_int(), ctypes.c_int64()
-        check(self._L.fc_closure_apply(self._ctx, int(algo), int(n_p), float(delta), ptr(dev_counts),
+        check(self._L.fc_closure_apply(self._ctx, int(algo), int(n_p), float(delta), self._dev(dev_counts),
                                        int(iteration), ctypes.byref(conv), ctypes.byref(m)))
         return bool(conv.value), m.value
 

@@ -149,6 +149,13 @@ int fc_set_stream(fc_ctx* ctx, void* s) {
     FC_API_END
 }
 
+int fc_synchronize(fc_ctx* ctx) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_HIP(hipStreamSynchronize(c.stream));
+    FC_API_END
+}
+
 int fc_set_timing(fc_ctx* ctx, int enable) {
     FC_CTX(ctx)
     FC_API_BEGIN
@@ -178,6 +185,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
             break;
         case FC_OPT_PRUNE: c.prune = value != 0; break;
         case FC_OPT_RELABEL: c.relabel = value != 0; break;
+        case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }

@@ -86,7 +86,12 @@ struct CDArgs {
                                  // [3n_r..4n_r) transition sweep: decide writes the nlab rows it gathers,
                                  // moves push (every vertex is visited), push mode from the next sweep
     int prune;
-    const int32_t* list;         // [B][n_r][S] vertices to visit (bucket order), or nullptr = every position
+    const int32_t* list;         // [n_r][PN] vertices to visit, grouped by round (offsets loff)
+    const int32_t* loff;         // [n_r][B+1] round offsets into a replica's list
+    int B;                       // buckets per sweep
+    int coarsen;                 // FC_OPT_COARSEN: 0, or the largest g (filtered sweeps in rounds of g buckets)
+    int64_t hcap;                // heavy-row slots per replica and round (heavy vertices in the graph)
+    int64_t dstride;             // decision slots per replica (PN: a coarse round may exceed S)
     const int32_t* lcnt;         // [B][n_r] list lengths
     const int32_t* blk_off;      // [B][n_r+1] light-kernel item offsets per replica
     const int32_t* itemrep;      // [B][wmax] replica of each light-kernel item
@@ -108,6 +113,14 @@ __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, in
 // Replica r's sweep visits every position (no pruning filter yet): its "list" is implicit,
 // entry di of bucket k = position k*S + di.
 __device__ __forceinline__ bool rep_full(const CDArgs& a, int r) { return !(a.prune && a.track[a.n_r + r]); }
+// Rounds of a filtered sweep of V vertices: g consecutive buckets per round, g the largest
+// power of two <= B with V*g <= N (oracle/fc_oracle.c tw_coarse restates it).
+__device__ __forceinline__ int coarse_factor(int64_t N, int64_t V, int B, int gmax) {
+    int g = 1;
+    while (2 * g <= B && 2 * g <= gmax && V * 2 * (int64_t)g <= N) g *= 2;
+    return g;
+}
+
 
 
 __device__ __forceinline__ unsigned long long* red_slot(const CDArgs& a, int r, int f) {
@@ -458,19 +471,16 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     return out;
 }
 
-template <bool LOUV, typename TT, bool LOOP>
+template <bool LOUV, typename TT>
 __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
     __shared__ WaveShared s_ws[TB / 64];
     __shared__ unsigned long long s_red[2][TB / 64][5];   // by item parity (no second barrier)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
     const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
-    // XCD x (blocks b with b % 8 == x, round-robin dispatch) takes the contiguous items
-    // [x*q, (x+1)*q), so a replica's items share an L2.  LOOP = false: grid = the upper
-    // bound of items, one item per block (large sweeps; 64 VGPRs, 8 waves/SIMD).  LOOP =
-    // true: a small grid whose gridDim/8 blocks per XCD stride over the items (small
-    // sweeps, where a grid of mostly empty blocks would cost more than the work; the loop
-    // costs registers, which matters little there)
+    // One item per block (the host sizes the grid to the largest round of the sweep); XCD x
+    // (blocks b with b % 8 == x, round-robin dispatch) takes the contiguous items
+    // [x*q, (x+1)*q), so a replica's items share an L2.
     const int64_t q = (W + 7) / 8, x0 = (blockIdx.x & 7) * q, x1 = min(W, x0 + q);
     auto item = [&](int64_t w, int par) {
     // (readfirstlane: values loaded from global memory are not known to be uniform, and a
@@ -484,13 +494,13 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     if (in_range) {
         if (rep_full(a, r)) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
                                            bucket * a.S + di);
-        else v = a.list[seg * a.S + di];   // lists hold vertex ids
+        else v = a.list[(int64_t)r * a.PN + a.loff[(int64_t)r * (a.B + 1) + bucket] + di];   // vertex ids
     }
     const bool rep_on = a.active[r] != 0;
     const bool valid = rep_on && in_range && v >= 0;
     const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, valid, v, s_ws[wv]);
     if (rep_on && in_range) {
-        a.dec[(int64_t)r * a.S + di] = make_int2(v >= 0 ? vis.dcs : -1, v);   // heavy: rewritten later
+        a.dec[(int64_t)r * a.dstride + di] = make_int2(v >= 0 ? vis.dcs : -1, v);   // heavy: rewritten later
         if (vis.heavy) {
             const int hq = atomicAdd(a.heavy_cnt, 1);
             a.heavy[3 * hq] = r;
@@ -521,14 +531,8 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         if (sm) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), sm);
     }
     };   // item
-    if constexpr (LOOP) {
-        int par = 0;
-#pragma unroll 1
-        for (int64_t w = x0 + (blockIdx.x >> 3); w < x1; w += (int64_t)(gridDim.x >> 3), par ^= 1) item(w, par);
-    } else {
-        const int64_t w = x0 + (blockIdx.x >> 3);
-        if (w < x1) item(w, 0);
-    }
+    const int64_t w = x0 + (blockIdx.x >> 3);
+    if (w < x1) item(w, 0);
 }
 
 // A high-degree vertex decided by a whole 256-thread block (every thread calls it).  Table
@@ -629,7 +633,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         const int32_t dcs = heavy_visit<LOUV, TT, TB>(a, r, sweep, v, sh, a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots,
                                                   &dq, &unst);
         if (threadIdx.x == 0) {
-            a.dec[(int64_t)r * a.S + di] = make_int2(dcs, v);
+            a.dec[(int64_t)r * a.dstride + di] = make_int2(dcs, v);
             if (dq) atomicAdd(red_slot(a, r, 0), dq);
             if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
         }
@@ -664,7 +668,7 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
     if (!a.active[r]) return;
     const int64_t seg = (int64_t)bucket * a.n_r + r;
     const int64_t len = a.lcnt[seg];
-    const int2* decr = a.dec + (int64_t)r * a.S;
+    const int2* decr = a.dec + (int64_t)r * a.dstride;
     const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
     int moved = 0;
     if (!push && !trk) {
@@ -770,8 +774,9 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
 static constexpr int TAIL_MAXB = 256;
 static constexpr int TAIL_TB = 1024;     // threads per replica workgroup in k_cd_tail
 template <bool LOUV, typename TT, int NTH>
-__global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_sweeps, int B, int32_t* tbuf,
+__global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_sweeps, int32_t* tbuf,
                                                  int32_t* tmark, unsigned long long* tail_acc, int32_t* n_active_out) {
+    const int B = a.B;
     __shared__ WaveShared s_ws[NTH / 64];
     __shared__ HeavyShared<NTH> sh;
     __shared__ int s_off[TAIL_MAXB + 1], s_cur[TAIL_MAXB];
@@ -785,16 +790,17 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
     int32_t* wl2 = wl + a.N;
     int32_t* bl = wl2 + a.N;
     int32_t* mark = tmark + (int64_t)r * a.N;
-    const uint8_t* aff = a.aff + (int64_t)r * a.N;
-    int2* decr = a.dec + (int64_t)r * a.S;
-    int32_t* hv = a.heavy + (int64_t)r * a.S;
+    uint8_t* aff = a.aff + (int64_t)r * a.N;
+    int2* decr = a.dec + (int64_t)r * a.dstride;
+    int32_t* hv = a.heavy + (int64_t)r * a.hcap;
     int32_t* scratch = a.heavy_scratch ? a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots : nullptr;
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    if (!rep_full(a, r)) {                    // initial worklist: the flagged vertices
+    if (!rep_full(a, r)) {                    // initial worklist: the flagged vertices (flags cleared)
         for (int64_t v0 = 0; v0 < a.N; v0 += NTH) {
             const int64_t v = v0 + threadIdx.x;
             const bool f = v < a.N && aff[v];
+            if (f) aff[v] = 0;
             const unsigned long long b = __ballot(f);
             int base = 0;
             if ((threadIdx.x & 63) == 0 && b) base = atomicAdd(&s_n, __popcll(b));
@@ -830,8 +836,11 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             }
             __syncthreads();
         }
-        for (int k = 0; k < B; ++k) {
-            const int64_t nk = full ? min(a.S, a.PN - (int64_t)k * a.S) : (int64_t)(s_off[k + 1] - s_off[k]);
+        // rounds: one bucket each, or g consecutive buckets of a filtered sweep (k_list_plan)
+        const int g = (!full && a.coarsen) ? coarse_factor(a.N, (int64_t)n, B, a.coarsen) : 1;
+        for (int k = 0; k < B; k += g) {
+            const int k1 = min(B, k + g);
+            const int64_t nk = full ? min(a.S, a.PN - (int64_t)k * a.S) : (int64_t)(s_off[k1] - s_off[k]);
             if (threadIdx.x == 0) s_nheavy = 0;
             __syncthreads();
             for (int64_t base = wv * WNT; base < nk; base += WNT * (NTH / 64)) {   // wave-uniform (waves are independent)
@@ -922,27 +931,94 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
 }
 
 // Visit lists of one sweep, per replica: every vertex (sweeps before tracking starts, or
-// pruning off), or those flagged affected by the previous sweep's moves -- bucketed by the
-// vertex's position in this sweep's random order (inverse permutation).  The order inside
-// a bucket is immaterial: a bucket's decisions all read the state the earlier buckets
-// left, and its moves commute (distinct vertices, integer atomics), so entries land in
-// any order.  Flags are read and cleared here.  Cost: one pass over aff plus work per
-// listed vertex (no per-position scan).  Dynamic LDS: 2 * B ints.
-static constexpr int LB_PER = 16;        // vertices per thread in k_list_build
-__global__ __launch_bounds__(256) void k_list_build(CDArgs a, int sweep, int B, int32_t* list, int32_t* lcnt) {
+// pruning off; the list stays implicit: entry di of bucket k is position k*S + di), or
+// those flagged affected by the previous sweep's moves -- bucketed by the vertex's position
+// in this sweep's random order (inverse permutation).  A filtered sweep of V vertices runs
+// its buckets in ROUNDS of g consecutive buckets, g the largest power of two <= B with
+// V*g <= N (k_list_plan), so a round holds about as many decisions as a bucket of a full
+// sweep -- not 32 latency-bound launches of a few hundred visits each.  The order inside a
+// round is immaterial: its decisions all read the state the earlier rounds left, and its
+// moves commute (distinct vertices, integer atomics), so entries land in any order.
+// Pass 1 counts the flagged vertices per bucket, the plan sizes the rounds, pass 2 fills the
+// per-replica lists [n_r][PN] and clears the flags.  Dynamic LDS: 2 * B ints.
+static constexpr int LB_PER = 16;        // vertices per thread in k_list_count / k_list_fill
+__device__ __forceinline__ uint32_t vertex_bucket(const CDArgs& a, const Perm& P, uint32_t v) {
+    const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
+    return pos / (uint32_t)a.S;
+}
+__global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t* cntfine) {
     extern __shared__ int s_lb[];
+    const int r = blockIdx.y, B = a.B;
+    if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
+    for (int k = threadIdx.x; k < B; k += TB) s_lb[k] = 0;
+    __syncthreads();
+    const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
+    const uint8_t* aff = a.aff + (int64_t)r * a.N;
+    const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < LB_PER; ++i) {
+        const int64_t v = v0 + (int64_t)i * TB;
+        if (v < a.N && aff[v]) atomicAdd(&s_lb[vertex_bucket(a, P, (uint32_t)v)], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < B; k += TB)
+        if (s_lb[k]) atomicAdd(&cntfine[(int64_t)r * B + k], s_lb[k]);
+}
+// Rounds per replica: lcnt[k][r] (entries of round k), loff[r][k] (offsets into the
+// replica's list), fill cursors, coarsening g; info[0] = max rounds, info[2..3] = visits.
+__global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int32_t* cursor, int32_t* gco,
+                            int32_t* lcnt, int32_t* info) {
+    const int B = a.B;
+    for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
+        int32_t* lo = loff + (int64_t)r * (B + 1);
+        if (!a.active[r]) {
+            for (int k = 0; k < B; ++k) lcnt[(int64_t)k * a.n_r + r] = 0;
+            gco[r] = 1;
+            continue;
+        }
+        if (rep_full(a, r)) {
+            int64_t tot = 0;
+            for (int k = 0; k < B; ++k) {
+                const int32_t c = (int32_t)max((int64_t)0, min(a.S, a.PN - (int64_t)k * a.S));
+                lcnt[(int64_t)k * a.n_r + r] = c;
+                tot += c;
+            }
+            gco[r] = 1;
+            atomicMax(info, B);
+            atomicAdd((unsigned long long*)(info + 2), (unsigned long long)tot);
+            continue;
+        }
+        const int32_t* cf = cntfine + (int64_t)r * B;
+        int64_t V = 0;
+        for (int k = 0; k < B; ++k) V += cf[k];
+        const int g = a.coarsen ? coarse_factor(a.N, V, B, a.coarsen) : 1;
+        const int rounds = (B + g - 1) / g;
+        int32_t acc = 0;
+        for (int k = 0; k < B; ++k) {
+            int32_t c = 0;
+            if (k < rounds)
+                for (int f = k * g; f < min(B, (k + 1) * g); ++f) c += cf[f];
+            lo[k] = acc;
+            cursor[(int64_t)r * B + k] = acc;
+            lcnt[(int64_t)k * a.n_r + r] = c;
+            acc += c;
+        }
+        lo[B] = acc;
+        gco[r] = g;
+        atomicMax(info, rounds);
+        atomicAdd((unsigned long long*)(info + 2), (unsigned long long)V);
+    }
+}
+__global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const int32_t* gco, int32_t* cursor,
+                                                   int32_t* list) {
+    extern __shared__ int s_lb[];
+    const int r = blockIdx.y, B = a.B;
     int* s_cnt = s_lb;
     int* s_base = s_lb + B;
-    const int r = blockIdx.y;
-    if (!a.active[r]) return;
+    if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
     for (int k = threadIdx.x; k < B; k += TB) s_cnt[k] = 0;
     __syncthreads();
-    if (rep_full(a, r)) {     // every position: implicit list (no flag can be set before tracking starts)
-        if (blockIdx.x == 0)
-            for (int k = threadIdx.x; k < B; k += TB)
-                lcnt[(int64_t)k * a.n_r + r] = (int32_t)min(a.S, a.PN - (int64_t)k * a.S);
-        return;
-    }
+    const int g = gco[r];
     const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
     uint8_t* aff = a.aff + (int64_t)r * a.N;
     int bk[LB_PER], loc[LB_PER];
@@ -951,27 +1027,24 @@ __global__ __launch_bounds__(256) void k_list_build(CDArgs a, int sweep, int B, 
     for (int i = 0; i < LB_PER; ++i) {
         const int64_t v = v0 + (int64_t)i * TB;
         bk[i] = -1;
-        if (v >= a.N) continue;
-        if (!aff[v]) continue;    // filter: vertices whose neighbour moved last sweep
+        if (v >= a.N || !aff[v]) continue;   // filter: vertices whose neighbour moved last sweep
         aff[v] = 0;
-        uint32_t pos;
-        if (a.chunk) pos = perm_invert(P, (uint32_t)v / CHUNK) * CHUNK + (uint32_t)v % CHUNK;
-        else pos = perm_invert(P, (uint32_t)v);
-        bk[i] = (int)(pos / (uint32_t)a.S);
+        bk[i] = (int)vertex_bucket(a, P, (uint32_t)v) / g;
         loc[i] = atomicAdd(&s_cnt[bk[i]], 1);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < B; k += TB)
-        s_base[k] = s_cnt[k] ? atomicAdd(&lcnt[(int64_t)k * a.n_r + r], s_cnt[k]) : 0;
+        s_base[k] = s_cnt[k] ? atomicAdd(&cursor[(int64_t)r * B + k], s_cnt[k]) : 0;
     __syncthreads();
+    int32_t* lr = list + (int64_t)r * a.PN;
 #pragma unroll
     for (int i = 0; i < LB_PER; ++i)
-        if (bk[i] >= 0) list[((int64_t)bk[i] * a.n_r + r) * a.S + s_base[bk[i]] + loc[i]] = (int32_t)(v0 + (int64_t)i * TB);
+        if (bk[i] >= 0) lr[s_base[bk[i]] + loc[i]] = (int32_t)(v0 + (int64_t)i * TB);
 }
 // Per bucket: light-decide item offsets per replica (items of LNT list entries) and the
 // replica of every item.
 __global__ __launch_bounds__(256) void k_list_offsets(int n_r, int64_t wmax, const int32_t* lcnt, int32_t* blk_off,
-                                                      int32_t* itemrep) {
+                                                      int32_t* itemrep, int32_t* info) {
     const int k = blockIdx.x;
     int32_t* bo = blk_off + (int64_t)k * (n_r + 1);
     if (threadIdx.x == 0) {
@@ -981,6 +1054,7 @@ __global__ __launch_bounds__(256) void k_list_offsets(int n_r, int64_t wmax, con
             acc += (lcnt[(int64_t)k * n_r + r] + LNT - 1) / LNT;
         }
         bo[n_r] = acc;
+        atomicMax(info + 1, acc);    // items of the largest round (the host sizes the decide grid)
     }
     __syncthreads();
     for (int r = 0; r < n_r; ++r)
@@ -991,18 +1065,31 @@ __global__ __launch_bounds__(256) void k_list_offsets(int n_r, int64_t wmax, con
 // Every grid is fixed and every size is read on the device, so a sweep never waits on
 // the host.
 template <bool LOUV, typename TT>
-static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy, int64_t small_grid) {
+static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy, int64_t grid) {
     if (any_heavy) FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     const int ev = timer_begin(c);
     // one item per block; grid = the bound wmax = n_r * ceil(S / LNT) (blocks past the
     // bucket's item count return at once)
-    if (small_grid > 0)
-        k_decide_light<LOUV, TT, true><<<(unsigned)small_grid, TB, 0, c.stream>>>(a, k, sweep);
-    else
-        k_decide_light<LOUV, TT, false><<<(unsigned)((a.wmax + 7) & ~int64_t(7)), TB, 0, c.stream>>>(a, k, sweep);
+    k_decide_light<LOUV, TT><<<(unsigned)grid, TB, 0, c.stream>>>(a, k, sweep);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
     k_apply<LOUV, TT><<<dim3((unsigned)c.apply_blocks, a.n_r), TB, 0, c.stream>>>(a, k);
+}
+
+__global__ void k_count_heavy(int64_t n, const int64_t* rowptr, int64_t thr, unsigned long long* out) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool h = v < n && rowptr[v + 1] - rowptr[v] > thr;
+    const unsigned long long b = __ballot(h);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+}
+// Vertices whose row exceeds thr entries (heavy rows of the working graph).
+static int64_t count_heavy(Ctx& c, int64_t thr) {
+    unsigned long long* d = (unsigned long long*)ensure<int64_t>(c.counters, 4);
+    FC_HIP(hipMemsetAsync(d, 0, 8, c.stream));
+    k_count_heavy<<<nblk(c.N), TB, 0, c.stream>>>(c.N, c.g.rowptr.as<int64_t>(), thr, d);
+    FC_HIP(hipMemcpyAsync(c.hpin, d, 8, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    return c.hpin[0];
 }
 
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
@@ -1024,7 +1111,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // tot in int32 whenever every community total fits (all <= 2M < 2^31): half the gathers
     const bool tot32 = g.M2 <= 0x7fffffffll;
     void* tot = louv ? (void*)ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
-    int2* dec = ensure<int2>(c.dec, (size_t)rcount * S);
+    const int64_t PN = CH ? NC * CH : N;
+    int2* dec = ensure<int2>(c.dec, (size_t)rcount * PN);   // a coarse round may hold up to PN decisions
     const int64_t m2 = 2 * g.m;
     int32_t* nlab = ensure<int32_t>(c.nlab, (size_t)rcount * (m2 > 0 ? m2 : 1));
     // per-replica state: active i32 [n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active
@@ -1035,15 +1123,29 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int32_t* n_active = (int32_t*)(sacc + 4 * (size_t)rcount);   // see k_sweep_end
     unsigned long long* tail_acc = (unsigned long long*)(n_active + 8);   // [n_r][4] k_cd_tail visits
     const size_t zero_bytes = (char*)(tail_acc + 4 * (size_t)rcount) - (char*)red;
-    int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * S + 3);
+    // heavy rows (degree > LIGHT_MAX_DEG): at most one entry per heavy vertex and replica per round
+    int64_t n_heavy = 0;
+    if (g.max_deg > LIGHT_MAX_DEG) n_heavy = count_heavy(c, LIGHT_MAX_DEG);
+    int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * (size_t)std::max<int64_t>(n_heavy, 1) + 3);
     uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
     FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));
     int32_t* track = ensure<int32_t>(c.track, 4 * (size_t)rcount);
     FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
-    int32_t* list = ensure<int32_t>(c.vlist, (size_t)B * rcount * S);
-    int32_t* lcnt = ensure<int32_t>(c.vcnt, (size_t)B * rcount + (size_t)B * (rcount + 1));
+    int32_t* list = ensure<int32_t>(c.vlist, (size_t)rcount * PN);
+    // lcnt [B][n_r] | blk_off [B][n_r+1] | cntfine [n_r][B] | loff [n_r][B+1] | cursor [n_r][B] | gco [n_r] | info [8]
+    const size_t plan_ints = (size_t)B * rcount + (size_t)B * (rcount + 1) + (size_t)rcount * B +
+                             (size_t)rcount * (B + 1) + (size_t)rcount * B + rcount + 1 + 8;
+    int32_t* lcnt = ensure<int32_t>(c.vcnt, plan_ints);
     int32_t* blk_off = lcnt + (size_t)B * rcount;
-    const int64_t wmax = (int64_t)rcount * ((S + LNT - 1) / LNT);
+    int32_t* cntfine = blk_off + (size_t)B * (rcount + 1);
+    int32_t* loff = cntfine + (size_t)rcount * B;
+    int32_t* cursor = loff + (size_t)rcount * (B + 1);
+    int32_t* gco = cursor + (size_t)rcount * B;
+    // [0] max rounds, [1] max items per round, [2..3] u64 visits (8-byte aligned: 64-bit atomics)
+    int32_t* info = gco + rcount;
+    if ((uintptr_t)info & 7) ++info;
+    // items per round: a coarse round of a replica holds at most PN entries
+    const int64_t wmax = (int64_t)rcount * ((PN + LNT - 1) / LNT + 1);
     int32_t* itemrep = ensure<int32_t>(c.itemrep, (size_t)B * wmax);
     int32_t* heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
     int64_t heavy_slots = 1;
@@ -1065,80 +1167,68 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                "edge weights too large for exact int64 modularity gains");
 
     CDArgs a;
-    a.N = N; a.S = S; a.PN = CH ? ((N + CH - 1) / CH) * CH : N; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
+    a.N = N; a.S = S; a.PN = PN; a.B = B; a.dstride = PN; a.coarsen = c.coarsen; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
-    a.aff = aff; a.list = list; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
-    a.itemrep = itemrep; a.wmax = wmax;
+    a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
+    a.itemrep = itemrep; a.wmax = wmax; a.hcap = std::max<int64_t>(n_heavy, 1);
 
-    // The host enqueues sweeps ahead and reads the active count of sweep s - LAG (pinned
-    // ring c.hpin[8..15], one event per slot): no per-sweep round trip.  Sweeps enqueued
-    // after every replica stopped find no active replica and do nothing.
-    const int LAG = c.trace ? 0 : 2;
-    if (c.sweep_ev.empty()) {
-        c.sweep_ev.resize(8);
-        for (auto& e : c.sweep_ev) FC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    int32_t* ring = (int32_t*)(c.hpin + 8);   // 8 slots x 32 B: n_active[0..7] of a sweep
+    // One host round trip per sweep, after the visit lists are planned: it returns the number
+    // of rounds (coarse buckets) and the largest round's decide items, so every launch is
+    // sized exactly, plus the active count left by the previous sweep.
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
     const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
+    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..3] | n_active[0]
     int sweep = 0;
-    int64_t small_grid = 0;   // > 0: decide grid of the looping kernel, sized from sweep s-LAG's visits
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
-        FC_HIP(hipMemsetAsync(lcnt, 0, sizeof(int32_t) * (size_t)B * rcount, c.stream));
-        k_list_build<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, B, list, lcnt);
-        k_list_offsets<<<B, TB, 0, c.stream>>>(rcount, a.wmax, lcnt, blk_off, itemrep);
-        for (int k = 0; k < B; ++k) {
-            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv, small_grid);
-            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv, small_grid);
-            else sub_round<true, int64_t>(c, a, k, sweep, hv, small_grid);
+        FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
+        FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
+        k_list_count<<<dim3(lb_grid, rcount), TB, sizeof(int) * B, c.stream>>>(a, sweep, cntfine);
+        k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, info);
+        FC_HIP(hipMemcpyAsync(hinfo, info, 16, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hinfo + 4, n_active, 4, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        const int rounds = hinfo[0];
+        const unsigned long long visits = *(unsigned long long*)(hinfo + 2);
+        if (rounds == 0 || (sweep > 0 && hinfo[4] == 0)) break;   // every replica has stopped
+        // small sweeps: hand every remaining sweep to the per-replica tail kernel (it takes the
+        // planned flags as its first worklist)
+        if (c.tail_visits > 0 && (int64_t)visits <= c.tail_visits && B <= TAIL_MAXB) {
+            int32_t* tbuf = ensure<int32_t>(c.tailbuf, (size_t)rcount * 3 * N);
+            int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
+            FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));
+            if (c.trace) fprintf(stderr, "[fc] cd it=%d tail kernel from sweep %d\n", iteration, sweep);
+            if (!louv)
+                k_cd_tail<false, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep, c.max_sweeps, tbuf, tmark, tail_acc, n_active);
+            else if (tot32)
+                k_cd_tail<true, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep, c.max_sweeps, tbuf, tmark, tail_acc, n_active);
+            else
+                k_cd_tail<true, int64_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep, c.max_sweeps, tbuf, tmark, tail_acc, n_active);
+            break;
+        }
+        k_list_fill<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, gco, cursor, list);
+        k_list_offsets<<<rounds, TB, 0, c.stream>>>(rcount, a.wmax, lcnt, blk_off, itemrep, info);
+        FC_HIP(hipMemcpyAsync(hinfo + 1, info + 1, 4, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        const int64_t grid = ((int64_t)std::max(hinfo[1], 1) + 7) & ~int64_t(7);
+        for (int k = 0; k < rounds; ++k) {
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv, grid);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv, grid);
+            else sub_round<true, int64_t>(c, a, k, sweep, hv, grid);
         }
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
-        const int slot = sweep & 7;
-        FC_HIP(hipMemcpyAsync(ring + 8 * slot, n_active, 32, hipMemcpyDeviceToHost, c.stream));
-        FC_HIP(hipEventRecord(c.sweep_ev[slot], c.stream));
         if (c.trace) {
             sync(c);
-            std::vector<unsigned long long> sa(4 * (size_t)rcount);
-            FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
-            sync(c);
-            unsigned long long vv = 0;
-            for (int r = 0; r < rcount; ++r) vv += sa[4 * r];
             static auto t_last = std::chrono::steady_clock::now();
             const auto t_now = std::chrono::steady_clock::now();
-            fprintf(stderr, "[fc] cd it=%d sweep=%d active_after=%d cum_vertex_visits=%llu dt_us=%.0f\n",
-                    iteration, sweep, ring[8 * slot], vv,
-                    1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
+            fprintf(stderr, "[fc] cd it=%d sweep=%d rounds=%d visits=%llu dt_us=%.0f\n", iteration, sweep, rounds,
+                    visits, 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
             t_last = t_now;
-        }
-        if (sweep >= LAG) {
-            const int chk = (sweep - LAG) & 7;
-            FC_HIP(hipEventSynchronize(c.sweep_ev[chk]));
-            if (ring[8 * chk] == 0) { ++sweep; break; }
-            // small sweeps: hand every remaining sweep to the per-replica tail kernel
-            const unsigned long long visits = *(unsigned long long*)(ring + 8 * chk + 6);
-            // items per bucket ~ visits / (B * LNT) + one partial item per replica; a 2x margin
-            // (sweeps shrink; the loop covers any excess)
-            const int64_t est = (int64_t)visits / ((int64_t)B * LNT) + rcount;
-            small_grid = (4 * est < a.wmax) ? std::max<int64_t>(64, ((2 * est + 7) / 8) * 8) : 0;
-            if (c.tail_visits > 0 && (int64_t)visits <= c.tail_visits && B <= TAIL_MAXB && sweep + 1 < c.max_sweeps) {
-                int32_t* tbuf = ensure<int32_t>(c.tailbuf, (size_t)rcount * 3 * N);
-                int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
-                FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));
-                if (c.trace) fprintf(stderr, "[fc] cd it=%d tail kernel from sweep %d\n", iteration, sweep + 1);
-                if (!louv)
-                    k_cd_tail<false, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
-                else if (tot32)
-                    k_cd_tail<true, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
-                else
-                    k_cd_tail<true, int64_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep + 1, c.max_sweeps, B, tbuf, tmark, tail_acc, n_active);
-                break;
-            }
         }
     }
     // replica-sweeps and light-kernel traffic counters for the roofline model

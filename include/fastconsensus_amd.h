@@ -71,6 +71,9 @@ void fc_destroy(fc_ctx* ctx);
 /* Run all work on an external stream (e.g. torch.cuda.current_stream().cuda_stream).
  * NULL restores the context's own stream. */
 int fc_set_stream(fc_ctx* ctx, void* hip_stream);
+/* Wait for the context's queued work (device buffers written by the step API are then
+ * safe to read from another stream). */
+int fc_synchronize(fc_ctx* ctx);
 /* 0/1: record HIP events around kernels and fill the *_ms fields of fc_stats. */
 int fc_set_timing(fc_ctx* ctx, int enable);
 /* Fill *stats with everything accumulated since the last call: the *_ms fields and
@@ -90,6 +93,10 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_TAIL_VISITS 7 /* once a sweep visits <= this many vertices (all replicas), the
                                 remaining sweeps run in one workgroup per replica (default
                                 1048576; 0 = off).  Same results either way.                   */
+#define FC_OPT_COARSEN 8    /* 0 (default): one bucket per round.  gmax > 0: a filtered sweep of V
+                                vertices runs its buckets in rounds of g (largest power of two <= gmax,
+                                <= buckets, with V*g <= n).  Experimental: coarse rounds decide more
+                                neighbouring vertices simultaneously and can need many more sweeps. */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

@@ -497,9 +497,25 @@ static inline int tw_better(long long s1, uint32_t h1, i32 c1, long long s2, uin
 }
 
 /* One replica.  algo 0 = louvain local moving, 1 = lpa.  Returns sweeps executed. */
+/* Bucket of list entry q (lists are concatenated per bucket, offsets loff). */
+static int bucket_of_entry(const i64* loff, int k0, int k1, i64 q) {
+    int k = k0;
+    while (k + 1 < k1 && loff[k + 1] <= q) ++k;
+    return k;
+}
+
+/* Coarsening of a filtered sweep (engine cd.hip k_list_offsets): its V listed vertices are
+ * decided in rounds of g consecutive buckets, g the largest power of two <= B with V*g <= N,
+ * so a round holds about as many decisions as one bucket of a full sweep (N/B); g <= gmax. */
+static int tw_coarse(i64 N, i64 V, int B, int gmax) {
+    int g = 1;
+    while (2 * g <= B && 2 * g <= gmax && V * 2 * (i64)g <= N) g *= 2;
+    return g;
+}
+
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
                       u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
-                      i32* lab) {
+                      int coarsen, i32* lab) {
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
@@ -511,7 +527,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     const i64 PN = chunk ? NC * chunk : N;
     const int B = (int)(buckets < NC ? buckets : NC);
     const i64 S = chunk ? ((NC + B - 1) / B) * chunk : (N + B - 1) / B;
-    i32* dec = (i32*)malloc(sizeof(i32) * (size_t)(S + 1));
+    i32* dec = (i32*)malloc(sizeof(i32) * (size_t)(PN + 1));
     u8* aff = (u8*)calloc((size_t)N, 1);
     i64* lists = (i64*)malloc(sizeof(i64) * (size_t)(PN + 1));   /* per-bucket visit lists */
     i64* loff = (i64*)malloc(sizeof(i64) * (size_t)(B + 1));
@@ -542,15 +558,20 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
             }
             loff[B] = n;
         }
-        for (int k = 0; k < B; ++k) {
+        /* rounds: one bucket each, or g consecutive buckets of a filtered sweep */
+        const int g = (listed && prune_now && coarsen) ? tw_coarse(N, loff[B], B, coarsen) : 1;
+        for (int k = 0; k < B; k += g) {
+            const int k1 = k + g < B ? k + g : B;
             i64 blen = PN - (i64)k * S;
             if (blen > S) blen = S;
             if (blen <= 0) continue;
-            const i64 ne = listed ? loff[k + 1] - loff[k] : blen;
+            const i64 ne = listed ? loff[k1] - loff[k] : blen;   /* g > 1 only when listed */
             for (i64 e = 0; e < ne; ++e) {
                 const i64 i = listed ? lists[loff[k] + e] : e;
                 dec[e] = -1;
-                const i64 p = (i64)k * S + i;
+                /* position: listed entries of round [k, k1) carry their own bucket */
+                const int kb = listed ? bucket_of_entry(loff, k, k1, loff[k] + e) : k;
+                const i64 p = (i64)kb * S + i;
                 const i64 vv = chunk ? (i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk
                                      : (i64)tw_perm_apply(&P, (uint32_t)p);
                 if (vv >= N) continue;
@@ -591,7 +612,8 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
             for (i64 e = 0; e < ne; ++e) {
                 if (dec[e] < 0) continue;
                 const i64 i = listed ? lists[loff[k] + e] : e;
-                const i64 p = (i64)k * S + i;
+                const int kb = listed ? bucket_of_entry(loff, k, k1, loff[k] + e) : k;
+                const i64 p = (i64)kb * S + i;
                 const i32 v = chunk ? (i32)((i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk)
                                     : (i32)tw_perm_apply(&P, (uint32_t)p);
                 const i32 old = lab[v], nw = dec[e];
@@ -616,8 +638,8 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
 /* Replicas [rbase, rbase+n_r) of the engine's bucketed CD on a symmetric CSR.
  * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
 void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
-                   int iteration, u64 seed, int buckets, int max_sweeps, int chunk, int prune, i32* lab,
-                   int* sweeps) {
+                   int iteration, u64 seed, int buckets, int max_sweeps, int chunk, int prune, int coarsen,
+                   i32* lab, int* sweeps) {
     i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
     i64 M2 = 0;
     for (i64 v = 0; v < N; ++v) {
@@ -629,7 +651,7 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
-                            buckets, max_sweeps, chunk, prune, lab + (i64)r * N);
+                            buckets, max_sweeps, chunk, prune, coarsen, lab + (i64)r * N);
         if (sweeps) sweeps[r] = sw;
     }
     free(kdeg);

@@ -160,22 +160,25 @@ def _lfr1k_graph():
 TAILS = [0, 1 << 40]
 
 
+@pytest.mark.parametrize("coarsen", [0, 4])
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("buckets,chunk,prune", [(32, 0, 0), (5, 0, 0), (32, 16, 0), (7, 16, 0), (32, 0, 1),
                                                  (5, 16, 1)])
-def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail):
+def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen):
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=99)
     eng.set_params(buckets=buckets)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
     eng.set_option("tail_visits", tail)
+    eng.set_option("coarsen", coarsen)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 4)
     got = eng.get_labels(n_r)
-    exp, sw = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune)
+    exp, sw = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune,
+                    coarsen=coarsen)
     np.testing.assert_array_equal(got, exp)
     # sharding invariance: replicas 2..4 alone give the same labelings
     eng.cd(algo, 2, 3, n_r, 4)
