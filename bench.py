@@ -106,10 +106,14 @@ def main():
     ap.add_argument("--prune", type=int, default=-1, help="CD vertex pruning (engine option; -1 = default)")
     ap.add_argument("--relabel", type=int, default=-1, help="internal vertex numbering (engine option; -1 = default)")
     ap.add_argument("--coarsen", type=int, default=-1, help="experimental coarse rounds, largest g (engine option)")
+    ap.add_argument("--n-p", type=int, default=0, help="experiment: override the config's n_p")
     ap.add_argument("--ids", default="generator", choices=["generator", "planted"],
                     help="experiment: renumber node ids by planted community before loading")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.n_p > 0:
+        cfg["n_p"] = args.n_p
+        cfg["desc"] += " (n_p overridden: %d)" % args.n_p
 
     import torch
     import torch.distributed as dist

@@ -965,7 +965,8 @@ __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t
         if (s_lb[k]) atomicAdd(&cntfine[(int64_t)r * B + k], s_lb[k]);
 }
 // Rounds per replica: lcnt[k][r] (entries of round k), loff[r][k] (offsets into the
-// replica's list), fill cursors, coarsening g; info[0] = max rounds, info[2..3] = visits.
+// replica's list), fill cursors, coarsening g; info[0] = max rounds, info[2..3] = visits,
+// info[4] = the largest replica's visits.
 __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int32_t* cursor, int32_t* gco,
                             int32_t* lcnt, int32_t* info) {
     const int B = a.B;
@@ -986,6 +987,7 @@ __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int
             gco[r] = 1;
             atomicMax(info, B);
             atomicAdd((unsigned long long*)(info + 2), (unsigned long long)tot);
+            atomicMax(info + 4, (int)min(tot, (int64_t)INT_MAX));
             continue;
         }
         const int32_t* cf = cntfine + (int64_t)r * B;
@@ -1007,6 +1009,7 @@ __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int
         gco[r] = g;
         atomicMax(info, rounds);
         atomicAdd((unsigned long long*)(info + 2), (unsigned long long)V);
+        atomicMax(info + 4, (int)V);
     }
 }
 __global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const int32_t* gco, int32_t* cursor,
@@ -1182,22 +1185,22 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // sized exactly, plus the active count left by the previous sweep.
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
     const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
-    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..3] | n_active[0]
+    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..4] | n_active[0] at [6]
     int sweep = 0;
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
         FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
         k_list_count<<<dim3(lb_grid, rcount), TB, sizeof(int) * B, c.stream>>>(a, sweep, cntfine);
         k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, info);
-        FC_HIP(hipMemcpyAsync(hinfo, info, 16, hipMemcpyDeviceToHost, c.stream));
-        FC_HIP(hipMemcpyAsync(hinfo + 4, n_active, 4, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hinfo, info, 20, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hinfo + 6, n_active, 4, hipMemcpyDeviceToHost, c.stream));
         sync(c);
         const int rounds = hinfo[0];
         const unsigned long long visits = *(unsigned long long*)(hinfo + 2);
-        if (rounds == 0 || (sweep > 0 && hinfo[4] == 0)) break;   // every replica has stopped
-        // small sweeps: hand every remaining sweep to the per-replica tail kernel (it takes the
-        // planned flags as its first worklist)
-        if (c.tail_visits > 0 && (int64_t)visits <= c.tail_visits && B <= TAIL_MAXB) {
+        if (rounds == 0 || (sweep > 0 && hinfo[6] == 0)) break;   // every replica has stopped
+        // small sweeps (every replica visits <= tail_visits vertices): hand every remaining
+        // sweep to the per-replica tail kernel (it takes the flags as its first worklist)
+        if (c.tail_visits > 0 && (int64_t)hinfo[4] <= c.tail_visits && B <= TAIL_MAXB) {
             int32_t* tbuf = ensure<int32_t>(c.tailbuf, (size_t)rcount * 3 * N);
             int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
             FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));

@@ -129,7 +129,7 @@ struct Ctx {
     std::vector<hipEvent_t> sweep_ev;   // per-sweep completion ring (cd_run)
     DevBuf itemrep;                 // CD: replica of each light-decide item, per bucket
     DevBuf tailbuf, tailmark;       // CD tail kernel: worklists [n_r][3N], epoch marks [n_r][N]
-    int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 1048576;  // 0 = off
+    int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 16384;  // per replica; 0 = off
     int coarsen = 0;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     bool trace = getenv("FC_TRACE") && *getenv("FC_TRACE") && *getenv("FC_TRACE") != '0';  // per-sweep stderr

@@ -90,9 +90,9 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 before fc_load_graph); results are reported in node order     */
 #define FC_OPT_PRUNE 5       /* 1 (default): once a sweep moves < n/4 vertices, later sweeps visit only vertices with a moved
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
-#define FC_OPT_TAIL_VISITS 7 /* once a sweep visits <= this many vertices (all replicas), the
-                                remaining sweeps run in one workgroup per replica (default
-                                1048576; 0 = off).  Same results either way.                   */
+#define FC_OPT_TAIL_VISITS 7 /* once no replica visits more than this many vertices in a sweep,
+                                the remaining sweeps run in one workgroup per replica (default
+                                16384; 0 = off).  Same results either way.                      */
 #define FC_OPT_COARSEN 8    /* 0 (default): one bucket per round.  gmax > 0: a filtered sweep of V
                                 vertices runs its buckets in rounds of g (largest power of two <= gmax,
                                 <= buckets, with V*g <= n).  Experimental: coarse rounds decide more
