@@ -47,6 +47,7 @@ static constexpr int HEAVY_GRID = 256;
 static constexpr double DQ_SCALE = 1099511627776.0;  // 2^40 fixed point for predicted dQ
 static constexpr int NSH = 16;          // counter shards per replica
 static constexpr int RF = 8;            // fields: 0 dq, 1 unstable, 2 moves, 3 verts, 4 entries, 5 cands
+static constexpr int RR_FULL = 1, RR_PUSH = 2, RR_TRANS = 4;   // round-record flags
 
 
 static inline unsigned nblk(int64_t n, int tb = TB) {
@@ -93,9 +94,9 @@ struct CDArgs {
     int64_t hcap;                // heavy-row slots per replica and round (heavy vertices in the graph)
     int64_t dstride;             // decision slots per replica (PN: a coarse round may exceed S)
     const int32_t* lcnt;         // [B][n_r] list lengths
-    const int32_t* blk_off;      // [B][n_r+1] light-kernel item offsets per replica
-    const int32_t* itemrep;      // [B][wmax] replica of each light-kernel item
-    int64_t wmax;                // items per bucket, upper bound: n_r * ceil(S / LNT)
+    // [B][n_r] per round and replica (k_list_plan): x first position (implicit list) or list
+    // offset, y entries, z flags RR_*; one scalar load gives a decide block all it needs
+    const int4* rrec;
     int32_t* heavy;              // (r, dec index, position) triples
     int32_t* heavy_cnt;
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
@@ -189,19 +190,8 @@ __device__ __forceinline__ int32_t decide_final(const CDArgs& a, int r, int32_t 
     }
 }
 
-// One LT-lane tile per vertex (LT = 8: 32 vertices per block, so twice the visits of a
-// 16-lane tile are in flight per CU; the visit is a chain of dependent gathers, so that
-// is what sets the rate).  The vertex's own label, degree and own-community total are
-// fetched first, alongside the row; then every lane issues ALL of its (<= PER) neighbour
-// gathers before it inserts them into the tile's LDS hash table; the lane that creates a
-// slot owns it and evaluates that candidate community (its Sigma gather batched likewise).
-//
-// Work: the bucket's visit lists of all replicas, cut into items of NT consecutive list
-// entries of one replica (item offsets per replica in blk_off, built on the device).  The
-// grid is fixed; block b takes a contiguous run of items (XCD-contiguous block order, so a
-// replica's items stay on few XCDs), so no host round trip sizes the launch.
-// One vertex visit (LT lanes; every thread of the block calls it: it holds two block
-// barriers).  Louvain: move iff the best gain is > 0; LPA: the most frequent label.
+// Result of one vertex visit (decide_wave, heavy_visit).  Louvain: move iff the best gain
+// is > 0; LPA: the most frequent label.
 struct Visit {
     int32_t dcs;               // target community, or -1
     unsigned long long dq;     // predicted modularity gain (fixed point, Louvain)
@@ -230,6 +220,8 @@ struct WaveShared {
     int32_t val[WNT * HCAP];
     long long best2[WNT];        // best exact score among lower-val candidates (rare path)
     long long tmin[WNT];         // min Sigma among the max-val candidates
+    unsigned long long tb[WNT];  // int32 Sigma: best max-val candidate, (Sigma << 32) | ~tie hash (min wins)
+    long long b1[WNT];           // int32 Sigma: score of that candidate
     unsigned long long k2[WNT];
     long long kv[WNT];
     int32_t vm[WNT], own[WNT], kown[WNT];
@@ -256,12 +248,11 @@ __device__ __forceinline__ void wave_sync() {
 // Returns vertex t's visit in lane t (< 8); ncand is per lane (sum it over the wave).
 template <bool LOUV, typename TT>
 __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int sweep, bool valid, int32_t v,
-                                             WaveShared& ws) {
+                                             bool push, bool trans, WaveShared& ws) {
     const int lane = threadIdx.x & 63;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
     const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-    const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
 #ifdef FC_PHASE_PROF
     const bool _samp = (blockIdx.x & 63) == 0;
     unsigned long long _tp = __builtin_amdgcn_s_memtime();
@@ -296,7 +287,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
 #pragma unroll
         for (int s = lane; s < WNT * HCAP / 4; s += 64) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
         if (lane < WNT) {
-            ws.best2[lane] = LLONG_MIN; ws.tmin[lane] = LLONG_MAX; ws.k2[lane] = 0; ws.vm[lane] = INT_MIN; ws.kown[lane] = 0;
+            ws.best2[lane] = LLONG_MIN; ws.tmin[lane] = LLONG_MAX; ws.tb[lane] = ~0ull; ws.k2[lane] = 0; ws.vm[lane] = INT_MIN; ws.kown[lane] = 0;
             ws.own[lane] = work ? own : -1;
             ws.kv[lane] = kv;
             ws.tvh[lane] = hash32(stream_key(a.seed, rg, a.iter, sweep, 2) ^ (uint32_t)v);
@@ -392,6 +383,14 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         return max(b1, ws.best2[t]);
     };
     TT tg[8];                                    // gathered Sigma (-1: not evaluated)
+    // int32 Sigma (Louvain): among the max-val candidates score = vm*2M - k_v*Sigma, so the
+    // best one and its tie key come from ONE packed atomicMin per candidate,
+    // (Sigma << 32) | ~hash (smallest Sigma, then largest hash; Sigma taken as 0 when k_v = 0,
+    // where they all tie); the hash is a bijection of the id, so no id tie remains and the
+    // winner's id is recovered by inverting it.  The separate tie pass runs only when a
+    // lower-val candidate may still reach the best score (rare).
+    constexpr bool PK = LOUV && sizeof(TT) == 4;
+    bool slow = !PK;                             // wave-uniform: generic tie pass (k2)
     if (LOUV) {
         // among the max-val candidates the score is vm*2M - k_v*Sigma: the smallest Sigma wins
 #pragma unroll
@@ -401,19 +400,39 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
             if (ws.val[sl] == ws.vm[t]) tg[it] = totr[ws.key[sl]];
         }
+        if constexpr (PK) {
 #pragma unroll
-        for (int it = 0; it < 8; ++it)
-            if (tg[it] >= 0) { ++ncand; atomicMin(&ws.tmin[rec[it] >> 8], (long long)tg[it]); }
-        wave_sync();
+            for (int it = 0; it < 8; ++it) {
+                if (tg[it] < 0) continue;
+                ++ncand;
+                const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+                const uint32_t h = hash32(ws.tvh[t] ^ (uint32_t)ws.key[sl]);
+                const uint32_t sg = ws.kv[t] ? (uint32_t)tg[it] : 0u;
+                atomicMin(&ws.tb[t], ((unsigned long long)sg << 32) | (uint32_t)~h);
+            }
+            wave_sync();
+            if (lane < WNT && ws.vm[lane] != INT_MIN) {
+                ws.tmin[lane] = (long long)(ws.tb[lane] >> 32);
+                ws.b1[lane] = score(ws.vm[lane], ws.tmin[lane], ws.kv[lane]);
+            }
+            wave_sync();
+        } else {
+#pragma unroll
+            for (int it = 0; it < 8; ++it)
+                if (tg[it] >= 0) { ++ncand; atomicMin(&ws.tmin[rec[it] >> 8], (long long)tg[it]); }
+            wave_sync();
+        }
         // a lower val whose bound val*2M still reaches that score (rare: k_v*Sigma >= 2M)
         bool need = false;
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
             if (rec[it] < 0 || tg[it] >= 0) continue;
             const int t = rec[it] >> 8;
-            need |= (long long)ws.val[t * HCAP + (rec[it] & 255)] * a.M2 >= score(ws.vm[t], ws.tmin[t], ws.kv[t]);
+            const long long b1 = PK ? ws.b1[t] : score(ws.vm[t], ws.tmin[t], ws.kv[t]);
+            need |= (long long)ws.val[t * HCAP + (rec[it] & 255)] * a.M2 >= b1;
         }
         if (__any(need)) {                       // wave-uniform
+            slow = true;
 #pragma unroll
             for (int it = 0; it < 8; ++it) {
                 if (rec[it] < 0 || tg[it] >= 0) continue;
@@ -435,16 +454,18 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     }
     PST(6);
     // tie key among the candidates at the best score: larger hash, then smaller id
+    if (slow) {                                  // wave-uniform
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        if (tg[it] < 0) continue;
-        const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
-        const int32_t key = ws.key[sl], val = ws.val[sl];
-        const long long sc = LOUV ? score(val, tg[it], ws.kv[t]) : (long long)val;
-        if (sc != best_of(t)) continue;
-        atomicMax(&ws.k2[t], ((unsigned long long)hash32(ws.tvh[t] ^ (uint32_t)key) << 32) | (uint32_t)~key);
+        for (int it = 0; it < 8; ++it) {
+            if (tg[it] < 0) continue;
+            const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+            const int32_t key = ws.key[sl], val = ws.val[sl];
+            const long long sc = LOUV ? score(val, tg[it], ws.kv[t]) : (long long)val;
+            if (sc != best_of(t)) continue;
+            atomicMax(&ws.k2[t], ((unsigned long long)hash32(ws.tvh[t] ^ (uint32_t)key) << 32) | (uint32_t)~key);
+        }
+        wave_sync();
     }
-    wave_sync();
     PST(7);
     // ---- the decision, lanes 0..7
     Visit out;
@@ -452,7 +473,8 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     if (work && ws.vm[lane] != INT_MIN) {        // some candidate besides the own community (Louvain)
         const long long best_s = best_of(lane);
         {
-            const int32_t best_c = (int32_t)~(uint32_t)ws.k2[lane];
+            const int32_t best_c = slow ? (int32_t)~(uint32_t)ws.k2[lane]
+                                        : (int32_t)(hash32_inv(~(uint32_t)ws.tb[lane]) ^ ws.tvh[lane]);
             const TT kown = (TT)ws.kown[lane];
             if (LOUV) {
                 const long long G = best_s - (long long)kown * a.M2 + kv * ((long long)tot_own - kv);
@@ -472,34 +494,37 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
 }
 
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep) {
+__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep, int X) {
     __shared__ WaveShared s_ws[TB / 64];
     __shared__ unsigned long long s_red[2][TB / 64][5];   // by item parity (no second barrier)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int32_t* bo = a.blk_off + (int64_t)bucket * (a.n_r + 1);
-    const int64_t W = __builtin_amdgcn_readfirstlane(bo[a.n_r]);
-    // One item per block (the host sizes the grid to the largest round of the sweep); XCD x
-    // (blocks b with b % 8 == x, round-robin dispatch) takes the contiguous items
-    // [x*q, (x+1)*q), so a replica's items share an L2.
-    const int64_t q = (W + 7) / 8, x0 = (blockIdx.x & 7) * q, x1 = min(W, x0 + q);
-    auto item = [&](int64_t w, int par) {
-    // (readfirstlane: values loaded from global memory are not known to be uniform, and a
-    // vector r would move the per-replica arithmetic -- permutation keys, addresses -- to VALU)
-    const int r = __builtin_amdgcn_readfirstlane(a.itemrep[(int64_t)bucket * a.wmax + w]);
-    const int64_t seg = ((int64_t)bucket * a.n_r + r);
-    const int64_t di = (w - __builtin_amdgcn_readfirstlane(bo[r])) * LNT + wv * WNT + lane;   // decision slot (lane < 8)
-    const bool in_range = lane < WNT && di < __builtin_amdgcn_readfirstlane(a.lcnt[seg]);
+    // One item (LNT list entries of one replica) per block.  Every replica owns X item slots
+    // (X = the sweep's largest per-replica round, from the host's one read per sweep); slots
+    // past a replica's entries return at once.  XCD x (blocks b with b % 8 == x, round-robin
+    // dispatch) takes the contiguous slots [x*q, (x+1)*q), so a replica's items share an L2.
+    const uint32_t W = (uint32_t)a.n_r * (uint32_t)X, q = (W + 7) / 8;
+    const uint32_t w = (blockIdx.x & 7) * q + (blockIdx.x >> 3);
+    if ((blockIdx.x >> 3) >= q || w >= W) return;                       // block-uniform
+    const int r = (int)(w / (uint32_t)X);
+    const int i = (int)(w - (uint32_t)r * (uint32_t)X);
+    const int4 rr = a.rrec[(int64_t)bucket * a.n_r + r];                // one scalar load
+    const int cnt = rr.y - i * LNT;
+    if (cnt <= 0) return;                                                // block-uniform
+    auto item = [&](int par) {
+    const int slot = wv * WNT + lane;
+    const int64_t di = (int64_t)i * LNT + slot;                          // decision slot (lane < 8)
+    const bool in_range = lane < WNT && slot < cnt;
     const int rg = a.rbase + r;
     int32_t v = -1;
     if (in_range) {
-        if (rep_full(a, r)) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
-                                           bucket * a.S + di);
-        else v = a.list[(int64_t)r * a.PN + a.loff[(int64_t)r * (a.B + 1) + bucket] + di];   // vertex ids
+        if (rr.z & RR_FULL) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
+                                           (int64_t)rr.x + di);
+        else v = a.list[(int64_t)r * a.PN + rr.x + di];                  // vertex ids
     }
-    const bool rep_on = a.active[r] != 0;
-    const bool valid = rep_on && in_range && v >= 0;
-    const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, valid, v, s_ws[wv]);
-    if (rep_on && in_range) {
+    const bool valid = in_range && v >= 0;
+    const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, valid, v, (rr.z & RR_PUSH) != 0, (rr.z & RR_TRANS) != 0,
+                                            s_ws[wv]);
+    if (in_range) {
         a.dec[(int64_t)r * a.dstride + di] = make_int2(v >= 0 ? vis.dcs : -1, v);   // heavy: rewritten later
         if (vis.heavy) {
             const int hq = atomicAdd(a.heavy_cnt, 1);
@@ -524,15 +549,14 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
         s_red[par][wv][4] = f4;
     }
     __syncthreads();
-    if (threadIdx.x < 5 && rep_on) {
+    if (threadIdx.x < 5) {
         unsigned long long sm = 0;
         for (int k = 0; k < TB / 64; ++k) sm += s_red[par][k][threadIdx.x];
         // fields: s_red 0 dq -> 0, 1 unstable -> 1, 2 verts -> 3, 3 entries -> 4, 4 cands -> 5
         if (sm) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), sm);
     }
     };   // item
-    const int64_t w = x0 + (blockIdx.x >> 3);
-    if (w < x1) item(w, 0);
+    item(0);
 }
 
 // A high-degree vertex decided by a whole 256-thread block (every thread calls it).  Table
@@ -812,6 +836,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
     for (int sweep = sweep0; sweep < max_sweeps; ++sweep) {
         const bool full = rep_full(a, r);
         const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
+        const bool dpush = a.track[2 * a.n_r + r] != 0, dtrans = a.track[3 * a.n_r + r] != 0;
         const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
         const int32_t stamp = sweep + 1;
         for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
@@ -848,7 +873,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 const bool in = lane < WNT && idx < nk;
                 int32_t v = -1;
                 if (in) v = full ? pos_vertex(a, P, (int64_t)k * a.S + idx) : bl[s_off[k] + idx];
-                const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, in && v >= 0, v, s_ws[wv]);
+                const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, in && v >= 0, v, dpush, dtrans, s_ws[wv]);
                 unsigned nc = (unsigned)vis.ncand;
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) nc += __shfl_xor(nc, off);
@@ -968,22 +993,30 @@ __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t
 // replica's list), fill cursors, coarsening g; info[0] = max rounds, info[2..3] = visits,
 // info[4] = the largest replica's visits.
 __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int32_t* cursor, int32_t* gco,
-                            int32_t* lcnt, int32_t* info) {
+                            int32_t* lcnt, int4* rrec, int32_t* info) {
     const int B = a.B;
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         int32_t* lo = loff + (int64_t)r * (B + 1);
         if (!a.active[r]) {
-            for (int k = 0; k < B; ++k) lcnt[(int64_t)k * a.n_r + r] = 0;
+            for (int k = 0; k < B; ++k) {
+                lcnt[(int64_t)k * a.n_r + r] = 0;
+                rrec[(int64_t)k * a.n_r + r] = make_int4(0, 0, 0, 0);
+            }
             gco[r] = 1;
             continue;
         }
+        const int fl = (a.track[2 * a.n_r + r] ? RR_PUSH : 0) | (a.track[3 * a.n_r + r] ? RR_TRANS : 0);
+        int32_t cmax = 0;                        // largest round: decide item slots per replica
         if (rep_full(a, r)) {
             int64_t tot = 0;
             for (int k = 0; k < B; ++k) {
                 const int32_t c = (int32_t)max((int64_t)0, min(a.S, a.PN - (int64_t)k * a.S));
                 lcnt[(int64_t)k * a.n_r + r] = c;
+                rrec[(int64_t)k * a.n_r + r] = make_int4((int32_t)((int64_t)k * a.S), c, fl | RR_FULL, 0);
+                cmax = max(cmax, c);
                 tot += c;
             }
+            atomicMax(info + 1, (cmax + LNT - 1) / LNT);
             gco[r] = 1;
             atomicMax(info, B);
             atomicAdd((unsigned long long*)(info + 2), (unsigned long long)tot);
@@ -1003,10 +1036,13 @@ __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int
             lo[k] = acc;
             cursor[(int64_t)r * B + k] = acc;
             lcnt[(int64_t)k * a.n_r + r] = c;
+            rrec[(int64_t)k * a.n_r + r] = make_int4(acc, c, fl, 0);
+            cmax = max(cmax, c);
             acc += c;
         }
         lo[B] = acc;
         gco[r] = g;
+        atomicMax(info + 1, (cmax + LNT - 1) / LNT);
         atomicMax(info, rounds);
         atomicAdd((unsigned long long*)(info + 2), (unsigned long long)V);
         atomicMax(info + 4, (int)V);
@@ -1044,36 +1080,16 @@ __global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const in
     for (int i = 0; i < LB_PER; ++i)
         if (bk[i] >= 0) lr[s_base[bk[i]] + loc[i]] = (int32_t)(v0 + (int64_t)i * TB);
 }
-// Per bucket: light-decide item offsets per replica (items of LNT list entries) and the
-// replica of every item.
-__global__ __launch_bounds__(256) void k_list_offsets(int n_r, int64_t wmax, const int32_t* lcnt, int32_t* blk_off,
-                                                      int32_t* itemrep, int32_t* info) {
-    const int k = blockIdx.x;
-    int32_t* bo = blk_off + (int64_t)k * (n_r + 1);
-    if (threadIdx.x == 0) {
-        int32_t acc = 0;
-        for (int r = 0; r < n_r; ++r) {
-            bo[r] = acc;
-            acc += (lcnt[(int64_t)k * n_r + r] + LNT - 1) / LNT;
-        }
-        bo[n_r] = acc;
-        atomicMax(info + 1, acc);    // items of the largest round (the host sizes the decide grid)
-    }
-    __syncthreads();
-    for (int r = 0; r < n_r; ++r)
-        for (int32_t w = bo[r] + threadIdx.x; w < bo[r + 1]; w += blockDim.x) itemrep[(int64_t)k * wmax + w] = r;
-}
-
 // One bucket: decide (light + heavy rows) against the state left by earlier buckets, apply.
 // Every grid is fixed and every size is read on the device, so a sweep never waits on
 // the host.
 template <bool LOUV, typename TT>
-static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy, int64_t grid) {
+static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy, int X) {
     if (any_heavy) FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     const int ev = timer_begin(c);
-    // one item per block; grid = the bound wmax = n_r * ceil(S / LNT) (blocks past the
-    // bucket's item count return at once)
-    k_decide_light<LOUV, TT><<<(unsigned)grid, TB, 0, c.stream>>>(a, k, sweep);
+    // one item per block: X item slots per replica, rounded up to whole XCD groups of 8
+    const int64_t grid = (((int64_t)a.n_r * X + 7) / 8) * 8;
+    k_decide_light<LOUV, TT><<<(unsigned)grid, TB, 0, c.stream>>>(a, k, sweep, X);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
     k_apply<LOUV, TT><<<dim3((unsigned)c.apply_blocks, a.n_r), TB, 0, c.stream>>>(a, k);
@@ -1135,21 +1151,19 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int32_t* track = ensure<int32_t>(c.track, 4 * (size_t)rcount);
     FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
     int32_t* list = ensure<int32_t>(c.vlist, (size_t)rcount * PN);
-    // lcnt [B][n_r] | blk_off [B][n_r+1] | cntfine [n_r][B] | loff [n_r][B+1] | cursor [n_r][B] | gco [n_r] | info [8]
-    const size_t plan_ints = (size_t)B * rcount + (size_t)B * (rcount + 1) + (size_t)rcount * B +
+    // rrec int4 [B][n_r] | lcnt [B][n_r] | cntfine [n_r][B] | loff [n_r][B+1] | cursor [n_r][B] | gco [n_r] | info [8]
+    const size_t plan_ints = 4 * (size_t)B * rcount + (size_t)B * rcount + (size_t)rcount * B +
                              (size_t)rcount * (B + 1) + (size_t)rcount * B + rcount + 1 + 8;
-    int32_t* lcnt = ensure<int32_t>(c.vcnt, plan_ints);
-    int32_t* blk_off = lcnt + (size_t)B * rcount;
-    int32_t* cntfine = blk_off + (size_t)B * (rcount + 1);
+    int4* rrec = (int4*)ensure<int32_t>(c.vcnt, plan_ints);
+    int32_t* lcnt = (int32_t*)(rrec + (size_t)B * rcount);
+    int32_t* cntfine = lcnt + (size_t)B * rcount;
     int32_t* loff = cntfine + (size_t)rcount * B;
     int32_t* cursor = loff + (size_t)rcount * (B + 1);
     int32_t* gco = cursor + (size_t)rcount * B;
-    // [0] max rounds, [1] max items per round, [2..3] u64 visits (8-byte aligned: 64-bit atomics)
+    // [0] max rounds, [1] decide item slots per replica (its largest round), [2..3] u64 visits
+    // (8-byte aligned: 64-bit atomics), [4] the largest replica's visits
     int32_t* info = gco + rcount;
     if ((uintptr_t)info & 7) ++info;
-    // items per round: a coarse round of a replica holds at most PN entries
-    const int64_t wmax = (int64_t)rcount * ((PN + LNT - 1) / LNT + 1);
-    int32_t* itemrep = ensure<int32_t>(c.itemrep, (size_t)B * wmax);
     int32_t* heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
     int64_t heavy_slots = 1;
     while (heavy_slots < 2 * (int64_t)g.max_deg) heavy_slots <<= 1;
@@ -1177,12 +1191,12 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
-    a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.blk_off = blk_off; a.track = track; a.prune = c.prune;
-    a.itemrep = itemrep; a.wmax = wmax; a.hcap = std::max<int64_t>(n_heavy, 1);
+    a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
+    a.hcap = std::max<int64_t>(n_heavy, 1);
 
     // One host round trip per sweep, after the visit lists are planned: it returns the number
-    // of rounds (coarse buckets) and the largest round's decide items, so every launch is
-    // sized exactly, plus the active count left by the previous sweep.
+    // of rounds (coarse buckets) and the largest per-replica round (decide item slots), so
+    // every launch is sized exactly, plus the active count left by the previous sweep.
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
     const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
     int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..4] | n_active[0] at [6]
@@ -1191,7 +1205,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
         FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
         k_list_count<<<dim3(lb_grid, rcount), TB, sizeof(int) * B, c.stream>>>(a, sweep, cntfine);
-        k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, info);
+        k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, rrec, info);
         FC_HIP(hipMemcpyAsync(hinfo, info, 20, hipMemcpyDeviceToHost, c.stream));
         FC_HIP(hipMemcpyAsync(hinfo + 6, n_active, 4, hipMemcpyDeviceToHost, c.stream));
         sync(c);
@@ -1214,14 +1228,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             break;
         }
         k_list_fill<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, gco, cursor, list);
-        k_list_offsets<<<rounds, TB, 0, c.stream>>>(rcount, a.wmax, lcnt, blk_off, itemrep, info);
-        FC_HIP(hipMemcpyAsync(hinfo + 1, info + 1, 4, hipMemcpyDeviceToHost, c.stream));
-        sync(c);
-        const int64_t grid = ((int64_t)std::max(hinfo[1], 1) + 7) & ~int64_t(7);
+        const int X = std::max(hinfo[1], 1);
         for (int k = 0; k < rounds; ++k) {
-            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv, grid);
-            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv, grid);
-            else sub_round<true, int64_t>(c, a, k, sweep, hv, grid);
+            if (!louv) sub_round<false, int32_t>(c, a, k, sweep, hv, X);
+            else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv, X);
+            else sub_round<true, int64_t>(c, a, k, sweep, hv, X);
         }
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);

@@ -127,7 +127,6 @@ struct Ctx {
     int relabel = 1;                // FC_OPT_RELABEL (applies at the next fc_load_graph)
     int64_t apply_blocks = getenv("FC_APPLY_BLOCKS") ? atoll(getenv("FC_APPLY_BLOCKS")) : 32;   // per replica
     std::vector<hipEvent_t> sweep_ev;   // per-sweep completion ring (cd_run)
-    DevBuf itemrep;                 // CD: replica of each light-decide item, per bucket
     DevBuf tailbuf, tailmark;       // CD tail kernel: worklists [n_r][3N], epoch marks [n_r][N]
     int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 16384;  // per replica; 0 = off
     int coarsen = 0;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)

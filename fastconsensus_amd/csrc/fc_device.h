@@ -15,6 +15,13 @@ FC_HD uint32_t hash32(uint32_t x) {
     x ^= x >> 16;
     return x;
 }
+// hash32 is a bijection; its inverse recovers x from hash32(x)
+FC_HD uint32_t hash32_inv(uint32_t x) {
+    x ^= x >> 16; x *= 0x7ed1b41du;
+    x ^= (x >> 13) ^ (x >> 26); x *= 0xa5cb9243u;
+    x ^= x >> 16;
+    return x;
+}
 FC_HD uint32_t hash2(uint32_t a, uint32_t b) { return hash32(a ^ hash32(b + 0x9e3779b9u)); }
 FC_HD uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
