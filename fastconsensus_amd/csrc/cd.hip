@@ -348,6 +348,10 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
                 hq[u] = (hq[u] + 1) & (HCAP - 1);
                 pv[u] = atomicCAS(&ws.key[tq[u] * HCAP + hq[u]], -1, kq[u]);
             }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (kq[u] < 0) continue;
             atomicAdd(&ws.val[tq[u] * HCAP + hq[u]], wq[u]);
             if (pv[u] == -1) rec[c * 4 + u] = (tq[u] << 8) | (int)hq[u];
         }
@@ -1092,7 +1096,12 @@ static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy,
     k_decide_light<LOUV, TT><<<(unsigned)grid, TB, 0, c.stream>>>(a, k, sweep, X);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
-    k_apply<LOUV, TT><<<dim3((unsigned)c.apply_blocks, a.n_r), TB, 0, c.stream>>>(a, k);
+    // apply: FC_APPLY_BLOCKS blocks per replica, more when few replicas share the GPU (a
+    // push/tracking move is a dependent row walk, so the chip needs ~2K resident blocks), but
+    // no more than the round's decisions fill (16-lane tiles)
+    const int64_t ab = std::min<int64_t>(std::max<int64_t>(c.apply_blocks, (2048 + a.n_r - 1) / a.n_r),
+                                         std::max<int64_t>(1, ((int64_t)X * LNT + TILES - 1) / TILES));
+    k_apply<LOUV, TT><<<dim3((unsigned)ab, a.n_r), TB, 0, c.stream>>>(a, k);
 }
 
 __global__ void k_count_heavy(int64_t n, const int64_t* rowptr, int64_t thr, unsigned long long* out) {
