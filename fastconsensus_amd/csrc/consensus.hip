@@ -206,6 +206,13 @@ void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* parti
 __device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int32_t* col, int32_t a,
                                                 int32_t b) {
     int64_t lo = rowptr[a], hi = rowptr[a + 1];
+    if (hi - lo <= 16) {   // short row: 16 independent loads (one round trip), not a dependent search
+        bool f = false;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (lo + q < hi) f |= col[lo + q] == b;
+        return f;
+    }
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
         const int32_t x = col[mid];
@@ -337,11 +344,12 @@ __global__ void k_deg_next(int64_t n, const int64_t* krowptr, int64_t* deg) {
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x < n) deg[x] = krowptr[x + 1] - krowptr[x];
 }
+// Only deg == 0 matters (isolates): a closure edge marks both ends with a plain store.
 __global__ void k_deg_add(int64_t k, const int32_t* cu, const int32_t* cv, int64_t* deg) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k) return;
-    atomicAdd((unsigned long long*)&deg[cu[i]], 1ull);
-    atomicAdd((unsigned long long*)&deg[cv[i]], 1ull);
+    deg[cu[i]] = 1;
+    deg[cv[i]] = 1;
 }
 // Indexed by NODE ORDER t (x = sigma[t]): nx.isolates visits nodes in node order.
 __global__ void k_iso_flags(int64_t n, const int32_t* sigma, const int64_t* deg, const int64_t* rowptr,

@@ -2,6 +2,8 @@
 // weight reset, fast_consensus.py:131-136, :434), deterministic CSR build, and the
 // merge that turns nextgraph into graph (fast_consensus.py:198, :307).
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_merge.hpp>
+#include <rocprim/iterator/discard_iterator.hpp>
 
 #include "fc_ctx.h"
 #include "fc_device.h"
@@ -241,11 +243,16 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
 }
 
 // ------------------------------------------------------------------ CSR build
-__global__ void k_count_uv(int64_t m, const int32_t* eu, const int32_t* ev, int64_t* cu, int64_t* cv) {
-    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= m) return;
-    atomicAdd((unsigned long long*)&cu[eu[e]], 1ull);
-    atomicAdd((unsigned long long*)&cv[ev[e]], 1ull);
+// start[x] = first index i with key[i] >= x, x in [0, n], for sorted keys in [0, n): the
+// exclusive prefix count of each node's edges, written once per node with no atomics
+// (index i writes the nodes in (key[i-1], key[i]]).
+template <class K>
+__global__ void k_bounds(int64_t m, const K* key, int64_t n, int64_t* start) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > m) return;
+    const int64_t lo = i == 0 ? -1 : (int64_t)key[i - 1];
+    const int64_t hi = i == m ? n : (int64_t)key[i];
+    for (int64_t x = lo + 1; x <= hi; ++x) start[x] = i;
 }
 __global__ void k_rowptr(int64_t n, int64_t m, const int64_t* us, const int64_t* vs, int64_t* rowptr) {
     int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,13 +277,13 @@ __global__ void k_fill_upper(int64_t m, const int32_t* eu, const int32_t* ev, co
     col[p] = ev[e]; cw[p] = ew[e]; ceid[p] = (int32_t)e;
     posu[e] = (int32_t)p;
 }
-__global__ void k_fill_lower(int64_t m, const int32_t* perm, const int32_t* eu, const int32_t* ev,
+__global__ void k_fill_lower(int64_t m, const int32_t* perm, const uint32_t* vsorted, const int32_t* eu,
                              const int32_t* ew, const int64_t* rowptr, const int64_t* vstart, int32_t* col,
                              int32_t* cw, int32_t* ceid, int32_t* posv) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= m) return;
     int32_t e = perm[f];
-    int32_t v = ev[e];
+    int32_t v = (int32_t)vsorted[f];          // = ev[e], read in order
     int64_t p = rowptr[v] + (f - vstart[v]);
     col[p] = eu[e]; cw[p] = ew[e]; ceid[p] = e;
     posv[e] = (int32_t)p;
@@ -319,35 +326,33 @@ __global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int6
 
 void graph_build_csr(Ctx& c, Graph& g) {
     const int64_t n = c.N, m = g.m;
-    int64_t* cu = ensure<int64_t>(c.nodetmp, n + 1);
-    int64_t* cv = ensure<int64_t>(c.nodetmp2, n + 1);
     int64_t* us = ensure<int64_t>(c.nodetmp3, 2 * (n + 1));
     int64_t* vs = us + (n + 1);
-    FC_HIP(hipMemsetAsync(cu, 0, sizeof(int64_t) * (n + 1), c.stream));
-    FC_HIP(hipMemsetAsync(cv, 0, sizeof(int64_t) * (n + 1), c.stream));
-    if (m > 0) k_count_uv<<<nblk(m), TB, 0, c.stream>>>(m, g.eu.as<int32_t>(), g.ev.as<int32_t>(), cu, cv);
-    exclusive_scan(c, cu, us, n + 1);
-    exclusive_scan(c, cv, vs, n + 1);
     int64_t* rowptr = ensure<int64_t>(g.rowptr, n + 1);
-    k_rowptr<<<nblk(n + 1), TB, 0, c.stream>>>(n, m, us, vs, rowptr);
     int64_t m2 = 2 * m > 0 ? 2 * m : 1;
     int32_t* col = ensure<int32_t>(g.col, m2);
     int32_t* cw = ensure<int32_t>(g.cw, m2);
     int32_t* ceid = ensure<int32_t>(g.ceid, m2);
-    if (m > 0) {
-        uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, m);
-        uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, m);
-        int32_t* i1 = (int32_t*)ensure<int64_t>(c.midx, m);
-        int32_t* i2 = (int32_t*)ensure<int64_t>(c.midx2, m);
+    uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, m > 0 ? m : 1);
+    uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, m > 0 ? m : 1);
+    int32_t* i1 = (int32_t*)ensure<int64_t>(c.midx, m > 0 ? m : 1);
+    int32_t* i2 = (int32_t*)ensure<int64_t>(c.midx2, m > 0 ? m : 1);
+    if (m > 0) {   // edges by v (stable: each v's run stays in u order)
         k_iota_ev<<<nblk(m), TB, 0, c.stream>>>(m, g.ev.as<int32_t>(), k1, i1);
         sort_pairs(c, (const uint32_t*)k1, k2, (const int32_t*)i1, i2, m, c.key_bits);
+    }
+    // row starts of the upper (u) and lower (v) halves: eu is sorted, k2 holds the sorted ev
+    k_bounds<int32_t><<<nblk(m + 1), TB, 0, c.stream>>>(m, g.eu.as<int32_t>(), n, us);
+    k_bounds<uint32_t><<<nblk(m + 1), TB, 0, c.stream>>>(m, k2, n, vs);
+    k_rowptr<<<nblk(n + 1), TB, 0, c.stream>>>(n, m, us, vs, rowptr);
+    if (m > 0) {
         int32_t* posu = (int32_t*)k1;   // sort inputs are dead once the sort is enqueued
         int32_t* posv = i1;
         int32_t* rev = ensure<int32_t>(g.crev, m2);
         k_fill_upper<<<nblk(m), TB, 0, c.stream>>>(m, g.eu.as<int32_t>(), g.ev.as<int32_t>(), g.ew.as<int32_t>(),
                                                     rowptr, us, vs, col, cw, ceid, posu);
-        k_fill_lower<<<nblk(m), TB, 0, c.stream>>>(m, i2, g.eu.as<int32_t>(), g.ev.as<int32_t>(),
-                                                    g.ew.as<int32_t>(), rowptr, vs, col, cw, ceid, posv);
+        k_fill_lower<<<nblk(m), TB, 0, c.stream>>>(m, i2, k2, g.eu.as<int32_t>(), g.ew.as<int32_t>(), rowptr, vs,
+                                                    col, cw, ceid, posv);
         k_fill_rev<<<nblk(m), TB, 0, c.stream>>>(m, posu, posv, rev);
     }
     int64_t* kdeg = ensure<int64_t>(g.kdeg, n);
@@ -382,7 +387,10 @@ __global__ void k_merge_gather(int64_t n, int64_t n0, const int64_t* idx, const 
     else { s -= n0; eu[i] = bu[s]; ev[i] = bv[s]; ew[i] = bw[s]; eage[i] = bage[s]; }
 }
 
-// kept (c.ku..) ++ added (c.cu.., n_cand closure + n_rep repair) -> c.g, then CSR.
+// kept (c.ku.., sorted) ++ added (c.cu.., n_cand closure + n_rep repair) -> c.g, then CSR.
+// The three lists are disjoint (closure pairs are non-edges of the kept graph, repair pairs
+// touch nodes isolated in both), so the canonical order is unique: only the added list is
+// radix-sorted, then merged with the kept list (merge path).
 void graph_merge_next(Ctx& c, int64_t n_added) {
     const int64_t n0 = c.kept_m, total = c.kept_m + n_added;
     int64_t cap = total > 0 ? total : 1;
@@ -390,14 +398,30 @@ void graph_merge_next(Ctx& c, int64_t n_added) {
     uint64_t* k2 = ensure<uint64_t>(c.mkey2, cap);
     int64_t* i1 = ensure<int64_t>(c.midx, cap);
     int64_t* i2 = ensure<int64_t>(c.midx2, cap);
+    int64_t* im = ensure<int64_t>(c.cval, cap);
     Graph& g = c.g;
     ensure<int32_t>(g.eu, cap); ensure<int32_t>(g.ev, cap); ensure<int32_t>(g.ew, cap); ensure<int64_t>(g.eage, cap);
     if (total > 0) {
         k_merge_keys<<<nblk(total), TB, 0, c.stream>>>(n0, n_added, c.ku.as<int32_t>(), c.kv.as<int32_t>(),
                                                         c.cu.as<int32_t>(), c.cv.as<int32_t>(), c.key_bits, k1, i1);
-        sort_pairs(c, k1, k2, i1, i2, total, 2 * c.key_bits);
+        const int64_t* src = i1;
+        if (n_added > 0) {
+            sort_pairs(c, k1 + n0, k2 + n0, i1 + n0, i2 + n0, n_added, 2 * c.key_bits);
+            if (n0 > 0) {
+                size_t tmp = 0;
+                auto disc = rocprim::make_discard_iterator();
+                FC_HIP(rocprim::merge(nullptr, tmp, k1, k2 + n0, disc, i1, i2 + n0, im, (size_t)n0, (size_t)n_added,
+                                      rocprim::less<uint64_t>(), c.stream));
+                c.sort_tmp.ensure(tmp);
+                FC_HIP(rocprim::merge(c.sort_tmp.p, tmp, k1, k2 + n0, disc, i1, i2 + n0, im, (size_t)n0,
+                                      (size_t)n_added, rocprim::less<uint64_t>(), c.stream));
+                src = im;
+            } else {
+                src = i2;
+            }
+        }
         k_merge_gather<<<nblk(total), TB, 0, c.stream>>>(
-            total, n0, i2, c.ku.as<int32_t>(), c.kv.as<int32_t>(), c.kw.as<int32_t>(), c.kage.as<int64_t>(),
+            total, n0, src, c.ku.as<int32_t>(), c.kv.as<int32_t>(), c.kw.as<int32_t>(), c.kage.as<int64_t>(),
             c.cu.as<int32_t>(), c.cv.as<int32_t>(), c.cw2.as<int32_t>(), c.cage.as<int64_t>(), g.eu.as<int32_t>(),
             g.ev.as<int32_t>(), g.ew.as<int32_t>(), g.eage.as<int64_t>());
     }
