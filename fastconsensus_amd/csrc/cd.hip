@@ -798,7 +798,7 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab,
 //   * the worklist is bucketed by inverse permutation (counting sort in LDS);
 //   * per bucket: light decisions (8-lane tiles, 32 per pass), heavy rows (whole block),
 //     barrier, moves applied, barrier.
-// The initial worklist is the aff flags left by the last multi-kernel sweep.
+// The first sweep's visit list is the one k_list_fill built for it (bucketed, flags cleared).
 static constexpr int TAIL_MAXB = 256;
 static constexpr int TAIL_TB = 1024;     // threads per replica workgroup in k_cd_tail
 template <bool LOUV, typename TT, int NTH>
@@ -822,21 +822,11 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
     int2* decr = a.dec + (int64_t)r * a.dstride;
     int32_t* hv = a.heavy + (int64_t)r * a.hcap;
     int32_t* scratch = a.heavy_scratch ? a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots : nullptr;
-    if (threadIdx.x == 0) s_n = 0;
+    (void)aff;
+    const int32_t* lo0 = a.loff + (int64_t)r * (B + 1);
+    if (threadIdx.x == 0) s_n = lo0[B];       // the first sweep's list (k_list_fill), when filtered
     __syncthreads();
-    if (!rep_full(a, r)) {                    // initial worklist: the flagged vertices (flags cleared)
-        for (int64_t v0 = 0; v0 < a.N; v0 += NTH) {
-            const int64_t v = v0 + threadIdx.x;
-            const bool f = v < a.N && aff[v];
-            if (f) aff[v] = 0;
-            const unsigned long long b = __ballot(f);
-            int base = 0;
-            if ((threadIdx.x & 63) == 0 && b) base = atomicAdd(&s_n, __popcll(b));
-            base = __shfl(base, 0);
-            if (f) wl[base + __popcll(b & ((1ull << (threadIdx.x & 63)) - 1ull))] = (int32_t)v;
-        }
-    }
-    __syncthreads();
+    bool first = true;
     for (int sweep = sweep0; sweep < max_sweeps; ++sweep) {
         const bool full = rep_full(a, r);
         const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
@@ -848,7 +838,13 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; }
         __syncthreads();
         const int n = s_n;
-        if (!full) {                          // bucket the worklist (order inside a bucket is immaterial)
+        const int32_t* blp = bl;
+        if (!full && first) {                 // rounds as k_list_plan laid them out: round j = buckets [j*g, (j+1)*g)
+            const int g0 = a.coarsen ? coarse_factor(a.N, (int64_t)n, B, a.coarsen) : 1;
+            for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = lo0[(k + g0 - 1) / g0];
+            blp = a.list + (int64_t)r * a.PN;
+            __syncthreads();
+        } else if (!full) {                   // bucket the worklist (order inside a bucket is immaterial)
             for (int i = threadIdx.x; i < n; i += NTH) {
                 const uint32_t v = (uint32_t)wl[i];
                 const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
@@ -876,7 +872,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 const int64_t idx = base + lane;
                 const bool in = lane < WNT && idx < nk;
                 int32_t v = -1;
-                if (in) v = full ? pos_vertex(a, P, (int64_t)k * a.S + idx) : bl[s_off[k] + idx];
+                if (in) v = full ? pos_vertex(a, P, (int64_t)k * a.S + idx) : blp[s_off[k] + idx];
                 const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, in && v >= 0, v, dpush, dtrans, s_ws[wv]);
                 unsigned nc = (unsigned)vis.ncand;
 #pragma unroll
@@ -955,6 +951,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         }
         __syncthreads();
         if (s_stop) break;
+        first = false;
         int32_t* t = wl; wl = wl2; wl2 = t;
     }
 }
@@ -1228,6 +1225,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
             FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));
             if (c.trace) fprintf(stderr, "[fc] cd it=%d tail kernel from sweep %d\n", iteration, sweep);
+            k_list_fill<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, gco, cursor, list);
             if (!louv)
                 k_cd_tail<false, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep, c.max_sweeps, tbuf, tmark, tail_acc, n_active);
             else if (tot32)
