@@ -131,7 +131,7 @@ void fc_destroy(fc_ctx* ctx) {
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
                       &c.hit, &c.mkey, &c.mkey2, &c.midx, &c.midx2, &c.sort_tmp, &c.nodetmp, &c.nodetmp2,
-                      &c.nodetmp3, &c.part, &c.ccount, &c.tailbuf, &c.tailmark, &c.sigma, &c.npos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
+                      &c.nodetmp3, &c.part, &c.ccount, &c.tailbuf, &c.tailmark, &c.sigma, &c.npos, &c.spos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
                       &c.st_lab};
     for (auto* b : bufs) b->release();
     for (auto e : c.timer.pool) (void)hipEventDestroy(e);
@@ -185,6 +185,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
             break;
         case FC_OPT_PRUNE: c.prune = value != 0; break;
         case FC_OPT_RELABEL: c.relabel = value != 0; break;
+        case FC_OPT_STORE: c.store_order = value != 0; break;
         case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};

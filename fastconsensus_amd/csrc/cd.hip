@@ -29,6 +29,8 @@
 namespace fc {
 
 template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
+template <class K, class V>
+void sort_pairs_public(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit);
 
 static constexpr int TB = 256;
 // Sweep order: vertices, or chunks of CHUNK consecutive vertices (chunk = 0 or CHUNK,
@@ -67,6 +69,8 @@ struct CDArgs {
     uint64_t seed;
     const int64_t* rowptr;
     const int32_t* col;
+    const int32_t* colp;         // storage slot of col[j] (label gathers: lab rows are in slot order)
+    const int32_t* spos;         // storage slot of vertex v in every lab row (Ctx::spos)
     const int32_t* cw;
     const int64_t* kdeg;
     int64_t M2;
@@ -265,7 +269,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     if (vl) {
         rb = a.rowptr[v];
         d = a.rowptr[v + 1] - rb;
-        own = labr[v];
+        own = labr[a.spos[v]];
         if (LOUV) kv = a.kdeg[v];
     }
     PST(0);
@@ -316,7 +320,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             for (int s = 1; s < WNT; ++s) t += (e >= o[s]) ? 1 : 0;
             jq[u] = __shfl(jb, t) + e;
             const bool ok = e < E;
-            kq[u] = ok ? (push ? nlr[jq[u]] : a.col[jq[u]]) : -1;
+            kq[u] = ok ? (push ? nlr[jq[u]] : a.colp[jq[u]]) : -1;   // pull: a label slot
             wq[u] = ok ? (LOUV ? a.cw[jq[u]] : 1) : 0;
             tq[u] = t;
         }
@@ -598,12 +602,12 @@ __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, Hea
     const int32_t* nlr = a.nlab + (int64_t)r * a.m2;
     const bool push = a.track[2 * a.n_r + r] != 0, trans = a.track[3 * a.n_r + r] != 0;
     for (int64_t j = rb + threadIdx.x; j < rb + d; j += NTH) {
-        const int32_t lj = push ? nlr[j] : labr[a.col[j]];
+        const int32_t lj = push ? nlr[j] : labr[a.colp[j]];
         if (trans) a.nlab[(int64_t)r * a.m2 + j] = lj;   // transition sweep (see decide_wave)
         tbl_insert(keys, vals, slots - 1, lj, LOUV ? a.cw[j] : 1);
     }
     __syncthreads();
-    const int32_t own = labr[v];
+    const int32_t own = labr[a.spos[v]];
     const int64_t kv = a.kdeg[v];
     const TT* totr = (const TT*)a.tot + (int64_t)r * a.N;
     long long best_s = LLONG_MIN, kown = 0;
@@ -675,7 +679,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
 // adjacency entries (nlab) and, while tracking, flags the neighbours for the next sweep.
 template <bool LOUV, typename TT>
 __device__ __forceinline__ void apply_move(const CDArgs& a, int r, int32_t d, int32_t v) {
-    int32_t* l = a.lab + (int64_t)r * a.N + v;
+    int32_t* l = a.lab + (int64_t)r * a.N + a.spos[v];
     const int32_t old = *l;
     *l = d;
     if (LOUV) {
@@ -779,11 +783,12 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
 }
 
 template <typename TT>
-__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, int32_t* lab, TT* tot, int louv) {
+__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, const int32_t* spos, int32_t* lab, TT* tot,
+                          int louv) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
     if (v >= n) return;
-    lab[(int64_t)r * n + v] = (int32_t)v;
+    lab[(int64_t)r * n + spos[v]] = (int32_t)v;
     if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
 }
 
@@ -1184,14 +1189,16 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     }
     FC_HIP(hipMemsetAsync(red, 0, zero_bytes, c.stream));
     dim3 ig(nblk(N), rcount);
-    if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, (int32_t*)tot, louv ? 1 : 0);
-    else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), lab, (int64_t*)tot, louv ? 1 : 0);
+    const int32_t* spos = c.spos.as<int32_t>();
+    if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), spos, lab, (int32_t*)tot, louv ? 1 : 0);
+    else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), spos, lab, (int64_t*)tot, louv ? 1 : 0);
     FC_REQUIRE(!louv || (double)g.max_kdeg * (double)g.M2 < 4.0e18, FC_ELIMIT,
                "edge weights too large for exact int64 modularity gains");
 
     CDArgs a;
     a.N = N; a.S = S; a.PN = PN; a.B = B; a.dstride = PN; a.coarsen = c.coarsen; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
+    a.colp = g.colp.as<int32_t>(); a.spos = spos;
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
@@ -1257,6 +1264,9 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     FC_HIP(hipMemcpyAsync(sa.data(), sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
     sync(c);
     const unsigned long long rep_sweeps = sa[4 * (size_t)rcount + 2];   // n_active[4..5]
+    if (c.trace)
+        fprintf(stderr, "[fc] cd it=%d done: %d multi-kernel sweeps, %.2f sweeps per replica\n", iteration, sweep,
+                (double)rep_sweeps / rcount);
     c.acc.cd_sweeps += (int64_t)rep_sweeps;
     c.prof.cd_sweeps += (int64_t)rep_sweeps;
     c.hpin[0] = c.hpin[1] = c.hpin[2] = 0;
@@ -1291,7 +1301,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
 
 // ------------------------------------------------------------------ transpose / renumber
 // lab [n_r][N] -> labT [N][ldT]  (64x64 tiles through LDS, both sides coalesced)
-__global__ __launch_bounds__(256) void k_transpose(int64_t N, int n_r, int ldT, const int32_t* lab, int32_t* labT) {
+__global__ __launch_bounds__(256) void k_transpose(int64_t N, int n_r, int ldT, const int32_t* lab, const int32_t* spos,
+                                                  int32_t* labT) {
     __shared__ int32_t t[64][65];
     const int64_t v0 = (int64_t)blockIdx.x * 64;
     const int r0 = blockIdx.y * 64;
@@ -1299,7 +1310,7 @@ __global__ __launch_bounds__(256) void k_transpose(int64_t N, int n_r, int ldT, 
     for (int rr = ty; rr < 64; rr += 4) {
         const int r = r0 + rr;
         const int64_t v = v0 + tx;
-        if (r < n_r && v < N) t[rr][tx] = lab[(int64_t)r * N + v];
+        if (r < n_r && v < N) t[rr][tx] = lab[(int64_t)r * N + spos[v]];
     }
     __syncthreads();
     for (int vv = ty; vv < 64; vv += 4) {
@@ -1313,7 +1324,7 @@ void labels_transpose(Ctx& c) {
     c.ldT = (c.n_r + 3) & ~3;
     int32_t* labT = ensure<int32_t>(c.labT, (size_t)c.N * c.ldT);
     dim3 grid(nblk(c.N, 64), (c.n_r + 63) / 64);
-    k_transpose<<<grid, TB, 0, c.stream>>>(c.N, c.n_r, c.ldT, c.lab.as<int32_t>(), labT);
+    k_transpose<<<grid, TB, 0, c.stream>>>(c.N, c.n_r, c.ldT, c.lab.as<int32_t>(), c.spos.as<int32_t>(), labT);
     c.labT_valid = true;
 }
 
@@ -1322,19 +1333,19 @@ __global__ void k_first_init(int64_t total, int32_t* first) {
     if (i < total) first[i] = 0x7fffffff;
 }
 // first[r][c] = earliest NODE position of community c
-__global__ void k_first_min(int64_t N, const int32_t* lab, const int32_t* npos, int32_t* first) {
+__global__ void k_first_min(int64_t N, const int32_t* lab, const int32_t* spos, const int32_t* npos, int32_t* first) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
-    if (v < N) atomicMin(&first[(int64_t)r * N + lab[(int64_t)r * N + v]], npos[v]);
+    if (v < N) atomicMin(&first[(int64_t)r * N + lab[(int64_t)r * N + spos[v]]], npos[v]);
 }
 // over node order t: out[r][t] = raw label of node t; flag = t opens its community
-__global__ void k_node_order(int64_t N, int64_t total, const int32_t* lab, const int32_t* sigma,
+__global__ void k_node_order(int64_t N, int64_t total, const int32_t* lab, const int32_t* sigma, const int32_t* spos,
                              const int32_t* first, int32_t* out, int32_t* flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > total) return;
     if (i == total) { if (flag) flag[i] = 0; return; }
     const int64_t r = i / N, t = i % N;
-    const int32_t c = lab[r * N + sigma[t]];
+    const int32_t c = lab[r * N + spos[sigma[t]]];
     out[i] = c;
     if (flag) flag[i] = first[r * N + c] == (int32_t)t ? 1 : 0;
 }
@@ -1354,10 +1365,11 @@ void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
     int32_t* rank = renumber ? ensure<int32_t>(c.hit, total + 1) : nullptr;
     if (renumber) {
         k_first_init<<<nblk(total), TB, 0, c.stream>>>(total, first);
-        k_first_min<<<dim3(nblk(N), c.n_r), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), c.npos.as<int32_t>(), first);
+        k_first_min<<<dim3(nblk(N), c.n_r), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), c.spos.as<int32_t>(),
+                                                               c.npos.as<int32_t>(), first);
     }
-    k_node_order<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), c.sigma.as<int32_t>(), first,
-                                                       out, flag);
+    k_node_order<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), c.sigma.as<int32_t>(),
+                                                       c.spos.as<int32_t>(), first, out, flag);
     if (renumber) {
         exclusive_scan(c, flag, rank, total + 1);
         k_relabel_out<<<nblk(total), TB, 0, c.stream>>>(N, total, out, first, rank);
@@ -1366,11 +1378,12 @@ void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
     FC_HIP(hipMemcpyAsync(host, out, 4 * (size_t)total, hipMemcpyDefault, c.stream));
     sync(c);
 }
-__global__ void k_from_node_order(int64_t N, int64_t total, const int32_t* in, const int32_t* sigma, int32_t* lab) {
+__global__ void k_from_node_order(int64_t N, int64_t total, const int32_t* in, const int32_t* sigma,
+                                  const int32_t* spos, int32_t* lab) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int64_t r = i / N, t = i % N;
-    lab[r * N + sigma[t]] = in[i];   // label values only matter through equality
+    lab[r * N + spos[sigma[t]]] = in[i];   // label values only matter through equality
 }
 // Host labelings in node order -> local replicas (replay).
 void labels_from_host(Ctx& c, int count, const int32_t* host) {
@@ -1378,8 +1391,37 @@ void labels_from_host(Ctx& c, int count, const int32_t* host) {
     int32_t* in = ensure<int32_t>(c.st_lab, total + 1);
     FC_HIP(hipMemcpyAsync(in, host, 4 * (size_t)total, hipMemcpyHostToDevice, c.stream));
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)total);
-    k_from_node_order<<<nblk(total), TB, 0, c.stream>>>(N, total, in, c.sigma.as<int32_t>(), lab);
+    k_from_node_order<<<nblk(total), TB, 0, c.stream>>>(N, total, in, c.sigma.as<int32_t>(), c.spos.as<int32_t>(), lab);
     sync(c);
 }
 
+// ------------------------------------------------------------------ label storage order
+// Ctx::spos: every replica's label row is stored in COMMUNITY order, so the neighbour-label
+// gathers of a sweep (lab[colp[j]]) land on few lines.  The order comes from one Louvain
+// replica run on the input graph at load (the same engine, any seed: only locality
+// matters); vertices sorted by (community, id).  Storage only -- label VALUES, visit order
+// and every decision are unchanged, so results are identical with or without it.
+__global__ void k_store_keys(int64_t N, const int32_t* lab, uint32_t* key, int32_t* idx) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= N) return;
+    key[v] = (uint32_t)lab[v];   // spos is the identity while this runs
+    idx[v] = (int32_t)v;
+}
+__global__ void k_store_slots(int64_t N, const int32_t* order, int32_t* spos) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < N) spos[order[i]] = (int32_t)i;
+}
+void store_order(Ctx& c) {
+    const int64_t N = c.N;
+    cd_run(c, FC_ALGO_LOUVAIN, 0, 1, 1, 0x3fffffff);
+    uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, N);
+    uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, N);
+    int32_t* i1 = (int32_t*)ensure<int64_t>(c.midx, N);
+    int32_t* i2 = (int32_t*)ensure<int64_t>(c.midx2, N);
+    k_store_keys<<<nblk(N), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), k1, i1);
+    sort_pairs_public(c, (const uint32_t*)k1, k2, (const int32_t*)i1, i2, N, c.key_bits);
+    k_store_slots<<<nblk(N), TB, 0, c.stream>>>(N, i2, c.spos.as<int32_t>());
+    c.n_r = 0;
+    sync(c);
+}
 }  // namespace fc

@@ -64,12 +64,13 @@ struct Graph {
     DevBuf eu, ev, ew, eage;        // int32, int32, int32, int64  [m]
     DevBuf rowptr, col, cw, ceid;   // int64 [N+1], int32 [2m] x3
     DevBuf crev;                    // int32 [2m]: index of the reverse entry (v->u for u->v)
+    DevBuf colp;                    // int32 [2m]: storage slot (Ctx::spos) of col[j]: label gathers
     DevBuf kdeg;                    // int64 [N] weighted degree
     int64_t M2 = 0;                 // sum of kdeg = 2 * total weight
     int32_t max_deg = 0;
     int64_t max_kdeg = 0;
     void release() {
-        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &crev, &kdeg};
+        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &crev, &colp, &kdeg};
         for (auto* x : b) x->release();
     }
 };
@@ -129,6 +130,8 @@ struct Ctx {
     std::vector<hipEvent_t> sweep_ev;   // per-sweep completion ring (cd_run)
     DevBuf tailbuf, tailmark;       // CD tail kernel: worklists [n_r][3N], epoch marks [n_r][N]
     int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 16384;  // per replica; 0 = off
+    int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
+    DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
     int coarsen = 0;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     bool trace = getenv("FC_TRACE") && *getenv("FC_TRACE") && *getenv("FC_TRACE") != '0';  // per-sweep stderr
@@ -145,6 +148,8 @@ void graph_merge_next(Ctx& c, int64_t n_added);
 void graph_copy(Ctx& c, Graph& dst, const Graph& src);
 // cd.cpp
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
+void store_order(Ctx& c);             // Ctx::spos from a one-replica Louvain run (FC_OPT_STORE)
+void graph_slots(Ctx& c, Graph& g);   // g.colp = spos[g.col]
 void labels_transpose(Ctx& c);
 void labels_to_host(Ctx& c, int32_t* out, bool renumber);   // node order [n_r][N]
 void labels_from_host(Ctx& c, int count, const int32_t* in);

@@ -43,6 +43,8 @@ void sort_pairs_public(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int
 }
 template void sort_pairs_public<uint64_t, int64_t>(Ctx&, const uint64_t*, uint64_t*, const int64_t*, int64_t*,
                                                    int64_t, int);
+template void sort_pairs_public<uint32_t, int32_t>(Ctx&, const uint32_t*, uint32_t*, const int32_t*, int32_t*,
+                                                   int64_t, int);
 template void sort_pairs_public<uint64_t, int32_t>(Ctx&, const uint64_t*, uint64_t*, const int32_t*, int32_t*,
                                                    int64_t, int);
 
@@ -140,6 +142,13 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
     std::vector<int32_t> h_npos(n);
     for (int64_t i = 0; i < n; ++i) h_npos[c.h_sigma[i]] = (int32_t)i;
     ensure<int32_t>(c.sigma, n); ensure<int32_t>(c.npos, n);
+    {   // label storage slots: identity until store_order() below
+        std::vector<int32_t> id(n);
+        for (int64_t i = 0; i < n; ++i) id[i] = (int32_t)i;
+        ensure<int32_t>(c.spos, n);
+        FC_HIP(hipMemcpyAsync(c.spos.p, id.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
+        sync(c);
+    }
     FC_HIP(hipMemcpyAsync(c.sigma.p, c.h_sigma.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
     FC_HIP(hipMemcpyAsync(c.npos.p, h_npos.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
     std::vector<int32_t> mu_(m), mv_(m);
@@ -181,6 +190,10 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
                                                     g.ew.as<int32_t>(), g.eage.as<int64_t>());
     c.m_original = mu;   // L = G.number_of_edges() (fast_consensus.py:132, :144)
     graph_build_csr(c, g);
+    if (c.store_order && g.M2 > 0) {
+        store_order(c);
+        graph_slots(c, g);
+    }
     graph_copy(c, c.g0, g);
     c.labT_valid = false;
     sync(c);   // the mapped host edge arrays die here
@@ -237,6 +250,7 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
     cp(dst.rowptr, src.rowptr, 8 * (n + 1));
     cp(dst.col, src.col, 8 * m); cp(dst.cw, src.cw, 8 * m); cp(dst.ceid, src.ceid, 8 * m);
     cp(dst.crev, src.crev, 8 * m);
+    cp(dst.colp, src.colp, 8 * m);
     cp(dst.kdeg, src.kdeg, 8 * n);
     dst.m = src.m; dst.M2 = src.M2; dst.max_deg = src.max_deg; dst.max_kdeg = src.max_kdeg;
     c.labT_valid = false;
@@ -324,6 +338,16 @@ __global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int6
     }
 }
 
+__global__ void k_slots(int64_t m2, const int32_t* col, const int32_t* spos, int32_t* colp) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m2) colp[j] = spos[col[j]];
+}
+void graph_slots(Ctx& c, Graph& g) {
+    const int64_t m2 = 2 * g.m;
+    int32_t* colp = ensure<int32_t>(g.colp, m2 > 0 ? m2 : 1);
+    if (m2 > 0) k_slots<<<nblk(m2), TB, 0, c.stream>>>(m2, g.col.as<int32_t>(), c.spos.as<int32_t>(), colp);
+}
+
 void graph_build_csr(Ctx& c, Graph& g) {
     const int64_t n = c.N, m = g.m;
     int64_t* us = ensure<int64_t>(c.nodetmp3, 2 * (n + 1));
@@ -363,6 +387,7 @@ void graph_build_csr(Ctx& c, Graph& g) {
     g.M2 = h[0];
     g.max_deg = (int32_t)h[1];
     g.max_kdeg = h[2];
+    graph_slots(c, g);
 }
 
 // ------------------------------------------------------------------ merge

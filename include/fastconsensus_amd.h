@@ -97,6 +97,11 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 vertices runs its buckets in rounds of g (largest power of two <= gmax,
                                 <= buckets, with V*g <= n).  Experimental: coarse rounds decide more
                                 neighbouring vertices simultaneously and can need many more sweeps. */
+#define FC_OPT_STORE 9       /* label storage order (set it before fc_load_graph).  1 (default): the
+                                replicas' label rows are stored in community order (a one-replica
+                                Louvain run at load orders the vertices), so the neighbour-label
+                                gathers of a sweep hit nearby lines; 0: internal-id order.  Storage
+                                only: results are identical either way.                         */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

@@ -367,6 +367,26 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     eng.close()
 
 
+@pytest.mark.parametrize("algo", [0, 1, 2])
+def test_label_storage_order_is_storage_only(fcmod, algo):
+    """FC_OPT_STORE (label rows in community order, from a Louvain run at load) changes
+    where labels live, never a decision: identical partitions and final graph with it off."""
+    case, _ = _lfr1k_graph()
+    e = case.edges_file
+    out = []
+    for store in (0, 1):
+        eng = fcmod.Engine(seed=5)
+        eng.set_option("store", store)
+        eng.load_graph(case.N, e[:, 0], e[:, 1])
+        labels, st = eng.run(algo, 10, 0.2 if algo != 1 else 0.8, 0.02)
+        out.append((labels, st["iterations"], eng.get_graph()))
+        eng.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+    for a, b in zip(out[0][2], out[1][2]):
+        np.testing.assert_array_equal(a, b)
+
+
 # ------------------------------------------------------------------------- full BASELINE sizes
 @pytest.fixture(scope="module")
 def lfr1m():
