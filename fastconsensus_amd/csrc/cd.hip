@@ -840,7 +840,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         const int32_t stamp = sweep + 1;
         for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
         if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
-        if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; }
+        if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; s_nheavy = 0; }
         __syncthreads();
         const int n = s_n;
         const int32_t* blp = bl;
@@ -871,8 +871,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         for (int k = 0; k < B; k += g) {
             const int k1 = min(B, k + g);
             const int64_t nk = full ? min(a.S, a.PN - (int64_t)k * a.S) : (int64_t)(s_off[k1] - s_off[k]);
-            if (threadIdx.x == 0) s_nheavy = 0;
-            __syncthreads();
+            // (s_nheavy was zeroed before the previous bucket's last barrier, or before the sweep's)
             for (int64_t base = wv * WNT; base < nk; base += WNT * (NTH / 64)) {   // wave-uniform (waves are independent)
                 const int64_t idx = base + lane;
                 const bool in = lane < WNT && idx < nk;
@@ -896,7 +895,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             }
             __syncthreads();
             const int nh = s_nheavy;
-            for (int h = 0; h < nh; ++h) {    // block-uniform
+            for (int h = 0; h < nh; ++h) {    // block-uniform (heavy_visit holds block barriers)
                 const int32_t idx = hv[h];
                 const int32_t v = decr[idx].y;
                 unsigned long long dq = 0;
@@ -908,7 +907,8 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                     if (unst) atomicAdd(&s_acc[1], 1ull);
                 }
             }
-            __syncthreads();
+            if (nh) __syncthreads();          // block-uniform: heavy decisions land before the moves
+            if (threadIdx.x == 0) s_nheavy = 0;   // read above; next bucket's decide appends after the barrier below
             // apply the bucket's moves; while tracking, neighbours join the next worklist
             int moved = 0;
             if (!push && !trk) {
