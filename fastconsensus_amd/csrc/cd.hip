@@ -79,7 +79,8 @@ struct CDArgs {
     const int32_t* rev;          // reverse adjacency entry of j
     int64_t m2;                  // 2m (adjacency entries)
     void* tot;                   // int32 [n_r][N] when 2M < 2^31, else int64
-    int2* dec;                   // [n_r][S] (target community or -1, vertex)
+    int4* dec;                   // [n_r][dstride] (target community or -1, vertex, own label, k_v when 2M < 2^31):
+                                 // the move needs no random read of the old label or the degree
     int32_t* active;
     // Sharded per-replica counters [n_r][NSH][RF]: one hot address per replica would
     // serialise every block's atomic (~12 ns each, MI355X_MICROARCH.md "fanin").
@@ -202,6 +203,7 @@ struct Visit {
     int unst;                  // LPA: own label not dominant
     int ncand;                 // Sigma gathers (Louvain) / candidates (LPA)
     int64_t d;                 // degree
+    int32_t own, kvw;          // own label and k_v (int32 when 2M < 2^31) for the decision record
     bool work, heavy;
 };
 #ifdef FC_PHASE_PROF
@@ -478,6 +480,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     // ---- the decision, lanes 0..7
     Visit out;
     out.dcs = -1; out.dq = 0; out.unst = 0; out.ncand = ncand; out.d = d; out.work = work; out.heavy = heavy;
+    out.own = own; out.kvw = (int32_t)kv;
     if (work && ws.vm[lane] != INT_MIN) {        // some candidate besides the own community (Louvain)
         const long long best_s = best_of(lane);
         {
@@ -533,7 +536,7 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, valid, v, (rr.z & RR_PUSH) != 0, (rr.z & RR_TRANS) != 0,
                                             s_ws[wv]);
     if (in_range) {
-        a.dec[(int64_t)r * a.dstride + di] = make_int2(v >= 0 ? vis.dcs : -1, v);   // heavy: rewritten later
+        a.dec[(int64_t)r * a.dstride + di] = make_int4(v >= 0 ? vis.dcs : -1, v, vis.own, vis.kvw);   // heavy: .x later
         if (vis.heavy) {
             const int hq = atomicAdd(a.heavy_cnt, 1);
             a.heavy[3 * hq] = r;
@@ -665,7 +668,7 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         const int32_t dcs = heavy_visit<LOUV, TT, TB>(a, r, sweep, v, sh, a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots,
                                                   &dq, &unst);
         if (threadIdx.x == 0) {
-            a.dec[(int64_t)r * a.dstride + di] = make_int2(dcs, v);
+            a.dec[(int64_t)r * a.dstride + di].x = dcs;   // the light kernel wrote v, own, k_v
             if (dq) atomicAdd(red_slot(a, r, 0), dq);
             if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
         }
@@ -678,13 +681,12 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
 // updates the label and the totals, the tile scatters the new label into the reverse
 // adjacency entries (nlab) and, while tracking, flags the neighbours for the next sweep.
 template <bool LOUV, typename TT>
-__device__ __forceinline__ void apply_move(const CDArgs& a, int r, int32_t d, int32_t v) {
-    int32_t* l = a.lab + (int64_t)r * a.N + a.spos[v];
-    const int32_t old = *l;
-    *l = d;
+__device__ __forceinline__ void apply_move(const CDArgs& a, int r, const int4& dv) {
+    const int32_t d = dv.x, v = dv.y, old = dv.z;
+    a.lab[(int64_t)r * a.N + a.spos[v]] = d;
     if (LOUV) {
         TT* tot = (TT*)a.tot + (int64_t)r * a.N;
-        const TT kv = (TT)a.kdeg[v];
+        const TT kv = sizeof(TT) == 4 ? (TT)dv.w : (TT)a.kdeg[v];
         if constexpr (sizeof(TT) == 8) {
             atomicAdd((unsigned long long*)&tot[old], (unsigned long long)(-(long long)kv));
             atomicAdd((unsigned long long*)&tot[d], (unsigned long long)kv);
@@ -700,23 +702,23 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
     if (!a.active[r]) return;
     const int64_t seg = (int64_t)bucket * a.n_r + r;
     const int64_t len = a.lcnt[seg];
-    const int2* decr = a.dec + (int64_t)r * a.dstride;
+    const int4* decr = a.dec + (int64_t)r * a.dstride;
     const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
     int moved = 0;
     if (!push && !trk) {
         for (int64_t di = (int64_t)blockIdx.x * TB + threadIdx.x; di < len; di += (int64_t)gridDim.x * TB) {
-            const int2 dv = decr[di];
-            if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv.x, dv.y); ++moved; }
+            const int4 dv = decr[di];
+            if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
         }
     } else {
         const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
         int32_t* nlr = a.nlab + (int64_t)r * a.m2;
         uint8_t* aff = a.aff + (int64_t)r * a.N;
         for (int64_t di = (int64_t)blockIdx.x * TILES + tile; di < len; di += (int64_t)gridDim.x * TILES) {
-            const int2 dv = decr[di];
+            const int4 dv = decr[di];
             const int32_t d = dv.x, v = dv.y;
             if (d < 0) continue;
-            if (lane == 0) { apply_move<LOUV, TT>(a, r, d, v); ++moved; }
+            if (lane == 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
             const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
             if (push && trk) {
                 for (int64_t j = rb + lane; j < re; j += TILE) {
@@ -824,7 +826,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
     int32_t* bl = wl2 + a.N;
     int32_t* mark = tmark + (int64_t)r * a.N;
     uint8_t* aff = a.aff + (int64_t)r * a.N;
-    int2* decr = a.dec + (int64_t)r * a.dstride;
+    int4* decr = a.dec + (int64_t)r * a.dstride;
     int32_t* hv = a.heavy + (int64_t)r * a.hcap;
     int32_t* scratch = a.heavy_scratch ? a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots : nullptr;
     (void)aff;
@@ -883,7 +885,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 for (int off = 32; off > 0; off >>= 1) nc += __shfl_xor(nc, off);
                 if (lane == 0 && nc) atomicAdd(&s_acc[5], (unsigned long long)nc);
                 if (in) {
-                    decr[idx] = make_int2(v >= 0 ? vis.dcs : -1, v);
+                    decr[idx] = make_int4(v >= 0 ? vis.dcs : -1, v, vis.own, vis.kvw);
                     if (vis.heavy) hv[atomicAdd(&s_nheavy, 1)] = (int32_t)idx;
                     if (vis.dq) atomicAdd(&s_acc[0], vis.dq);
                     if (vis.unst) atomicAdd(&s_acc[1], 1ull);
@@ -902,7 +904,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 int unst = 0;
                 const int32_t dcs = heavy_visit<LOUV, TT, NTH>(a, r, sweep, v, sh, scratch, &dq, &unst);
                 if (threadIdx.x == 0) {
-                    decr[idx] = make_int2(dcs, v);
+                    decr[idx].x = dcs;
                     if (dq) atomicAdd(&s_acc[0], dq);
                     if (unst) atomicAdd(&s_acc[1], 1ull);
                 }
@@ -913,17 +915,17 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             int moved = 0;
             if (!push && !trk) {
                 for (int64_t di = threadIdx.x; di < nk; di += NTH) {
-                    const int2 dv = decr[di];
-                    if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv.x, dv.y); ++moved; }
+                    const int4 dv = decr[di];
+                    if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
                 }
             } else {
                 const int t16 = threadIdx.x / TILE, l16 = threadIdx.x % TILE;
                 int32_t* nlr = a.nlab + (int64_t)r * a.m2;
                 for (int64_t di = t16; di < nk; di += NTH / TILE) {
-                    const int2 dv = decr[di];
+                    const int4 dv = decr[di];
                     const int32_t d = dv.x, v = dv.y;
                     if (d < 0) continue;
-                    if (l16 == 0) { apply_move<LOUV, TT>(a, r, d, v); ++moved; }
+                    if (l16 == 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
                     const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
                     for (int64_t j = rb + l16; j < re; j += TILE) {
                         if (push) nlr[a.rev[j]] = d;
@@ -1142,7 +1144,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const bool tot32 = g.M2 <= 0x7fffffffll;
     void* tot = louv ? (void*)ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
     const int64_t PN = CH ? NC * CH : N;
-    int2* dec = ensure<int2>(c.dec, (size_t)rcount * PN);   // a coarse round may hold up to PN decisions
+    int4* dec = ensure<int4>(c.dec, (size_t)rcount * PN);   // a coarse round may hold up to PN decisions
     const int64_t m2 = 2 * g.m;
     int32_t* nlab = ensure<int32_t>(c.nlab, (size_t)rcount * (m2 > 0 ? m2 : 1));
     // per-replica state: active i32 [n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active
