@@ -1141,7 +1141,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
     // tot in int32 whenever every community total fits (all <= 2M < 2^31): half the gathers
-    const bool tot32 = g.M2 <= 0x7fffffffll;
+    const bool tot32 = g.M2 <= 0x7fffffffll && !c.order_pass;
     void* tot = louv ? (void*)ensure<int64_t>(c.tot, (size_t)rcount * N) : nullptr;
     const int64_t PN = CH ? NC * CH : N;
     int4* dec = ensure<int4>(c.dec, (size_t)rcount * PN);   // a coarse round may hold up to PN decisions
@@ -1415,6 +1415,13 @@ __global__ void k_store_slots(int64_t N, const int32_t* order, int32_t* spos) {
 }
 void store_order(Ctx& c) {
     const int64_t N = c.N;
+    // int64 totals: the pass runs the k_decide_light<true, long> instance, so kernel
+    // statistics of the int32 instance cover the consensus runs alone
+    struct Pass {
+        Ctx& c;
+        explicit Pass(Ctx& x) : c(x) { c.order_pass = true; }
+        ~Pass() { c.order_pass = false; }
+    } pass(c);
     cd_run(c, FC_ALGO_LOUVAIN, 0, 1, 1, 0x3fffffff);
     uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, N);
     uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, N);

@@ -130,6 +130,7 @@ struct Ctx {
     std::vector<hipEvent_t> sweep_ev;   // per-sweep completion ring (cd_run)
     DevBuf tailbuf, tailmark;       // CD tail kernel: worklists [n_r][3N], epoch marks [n_r][N]
     int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 16384;  // per replica; 0 = off
+    bool order_pass = false;        // store_order()'s CD run (int64 totals, see there)
     int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
     DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
     int coarsen = 0;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)

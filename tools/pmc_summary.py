@@ -28,8 +28,9 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
         for r in rows(os.path.join(prof_dir, name, "**", "*counter_collection.csv")):
             kern = r.get("Kernel_Name", "?")
             short = kern.split("(")[0].split("<")[0].strip()
-            if "k_decide_light" in kern:
-                short = "k_decide_light<%s>" % ("louvain" if "true" in kern.split(">")[0] else "lpa")
+            if "k_decide_light" in kern:   # per instance: <true, int> is the consensus runs' Louvain kernel
+                targs = kern.split("<", 1)[1].split(">")[0].replace(" ", "")
+                short = "k_decide_light<%s>" % {"true,int": "louvain", "false,int": "lpa"}.get(targs, targs)
             counters[short][r.get("Counter_Name", "?")].append(float(r.get("Counter_Value", "nan")))
     per = {}
     for kern, cs in counters.items():
