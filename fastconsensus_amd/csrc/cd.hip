@@ -71,6 +71,7 @@ struct CDArgs {
     const int32_t* col;
     const int32_t* colp;         // storage slot of col[j] (label gathers: lab rows are in slot order)
     const int32_t* spos;         // storage slot of vertex v in every lab row (Ctx::spos)
+    const int4* vrec;            // per vertex: row start (uint32), degree, k_v (int32 totals only), slot
     const int32_t* cw;
     const int64_t* kdeg;
     int64_t M2;
@@ -269,10 +270,11 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     int32_t own = -1;
     TT tot_own = 0;
     if (vl) {
-        rb = a.rowptr[v];
-        d = a.rowptr[v + 1] - rb;
-        own = labr[a.spos[v]];
-        if (LOUV) kv = a.kdeg[v];
+        const int4 vr = a.vrec[v];               // one 16-byte load: row, degree, k_v, slot
+        rb = (int64_t)(uint32_t)vr.x;
+        d = vr.y;
+        own = labr[vr.w];
+        if (LOUV) kv = sizeof(TT) == 4 ? (int64_t)vr.z : a.kdeg[v];
     }
     PST(0);
     const bool heavy = vl && d > LIGHT_MAX_DEG;
@@ -681,9 +683,9 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
 // updates the label and the totals, the tile scatters the new label into the reverse
 // adjacency entries (nlab) and, while tracking, flags the neighbours for the next sweep.
 template <bool LOUV, typename TT>
-__device__ __forceinline__ void apply_move(const CDArgs& a, int r, const int4& dv) {
+__device__ __forceinline__ void apply_move(const CDArgs& a, int r, const int4& dv, int32_t slot) {
     const int32_t d = dv.x, v = dv.y, old = dv.z;
-    a.lab[(int64_t)r * a.N + a.spos[v]] = d;
+    a.lab[(int64_t)r * a.N + slot] = d;
     if (LOUV) {
         TT* tot = (TT*)a.tot + (int64_t)r * a.N;
         const TT kv = sizeof(TT) == 4 ? (TT)dv.w : (TT)a.kdeg[v];
@@ -708,7 +710,7 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
     if (!push && !trk) {
         for (int64_t di = (int64_t)blockIdx.x * TB + threadIdx.x; di < len; di += (int64_t)gridDim.x * TB) {
             const int4 dv = decr[di];
-            if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
+            if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]); ++moved; }
         }
     } else {
         const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
@@ -718,8 +720,9 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
             const int4 dv = decr[di];
             const int32_t d = dv.x, v = dv.y;
             if (d < 0) continue;
-            if (lane == 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
-            const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
+            const int4 vr = a.vrec[v];
+            if (lane == 0) { apply_move<LOUV, TT>(a, r, dv, vr.w); ++moved; }
+            const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
             if (push && trk) {
                 for (int64_t j = rb + lane; j < re; j += TILE) {
                     nlr[a.rev[j]] = d;     // neighbours now see v's new community
@@ -916,7 +919,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             if (!push && !trk) {
                 for (int64_t di = threadIdx.x; di < nk; di += NTH) {
                     const int4 dv = decr[di];
-                    if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
+                    if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]); ++moved; }
                 }
             } else {
                 const int t16 = threadIdx.x / TILE, l16 = threadIdx.x % TILE;
@@ -925,8 +928,9 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                     const int4 dv = decr[di];
                     const int32_t d = dv.x, v = dv.y;
                     if (d < 0) continue;
-                    if (l16 == 0) { apply_move<LOUV, TT>(a, r, dv); ++moved; }
-                    const int64_t rb = a.rowptr[v], re = a.rowptr[v + 1];
+                    const int4 vr = a.vrec[v];
+                    if (l16 == 0) { apply_move<LOUV, TT>(a, r, dv, vr.w); ++moved; }
+                    const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
                     for (int64_t j = rb + l16; j < re; j += TILE) {
                         if (push) nlr[a.rev[j]] = d;
                         if (trk) {
@@ -1200,7 +1204,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     CDArgs a;
     a.N = N; a.S = S; a.PN = PN; a.B = B; a.dstride = PN; a.coarsen = c.coarsen; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
-    a.colp = g.colp.as<int32_t>(); a.spos = spos;
+    a.colp = g.colp.as<int32_t>(); a.spos = spos; a.vrec = g.vrec.as<int4>();
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;

@@ -65,12 +65,13 @@ struct Graph {
     DevBuf rowptr, col, cw, ceid;   // int64 [N+1], int32 [2m] x3
     DevBuf crev;                    // int32 [2m]: index of the reverse entry (v->u for u->v)
     DevBuf colp;                    // int32 [2m]: storage slot (Ctx::spos) of col[j]: label gathers
+    DevBuf vrec;                    // int4 [N]: row start (m < 2^31), degree, k_v (valid when 2M < 2^31), slot
     DevBuf kdeg;                    // int64 [N] weighted degree
     int64_t M2 = 0;                 // sum of kdeg = 2 * total weight
     int32_t max_deg = 0;
     int64_t max_kdeg = 0;
     void release() {
-        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &crev, &colp, &kdeg};
+        DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &crev, &colp, &vrec, &kdeg};
         for (auto* x : b) x->release();
     }
 };

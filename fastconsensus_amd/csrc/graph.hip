@@ -251,6 +251,7 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
     cp(dst.col, src.col, 8 * m); cp(dst.cw, src.cw, 8 * m); cp(dst.ceid, src.ceid, 8 * m);
     cp(dst.crev, src.crev, 8 * m);
     cp(dst.colp, src.colp, 8 * m);
+    cp(dst.vrec, src.vrec, 16 * n);
     cp(dst.kdeg, src.kdeg, 8 * n);
     dst.m = src.m; dst.M2 = src.M2; dst.max_deg = src.max_deg; dst.max_kdeg = src.max_kdeg;
     c.labT_valid = false;
@@ -342,10 +343,20 @@ __global__ void k_slots(int64_t m2, const int32_t* col, const int32_t* spos, int
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j < m2) colp[j] = spos[col[j]];
 }
+// One 16-byte record per vertex for the CD kernels: row start, degree, k_v, storage slot --
+// one load where a list-order visit would touch three random lines (rowptr, kdeg, spos).
+__global__ void k_vrec(int64_t n, const int64_t* rowptr, const int64_t* kdeg, const int32_t* spos, int4* vrec) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const int64_t rb = rowptr[v];
+    vrec[v] = make_int4((int32_t)(uint32_t)rb, (int32_t)(rowptr[v + 1] - rb), (int32_t)kdeg[v], spos[v]);
+}
 void graph_slots(Ctx& c, Graph& g) {
-    const int64_t m2 = 2 * g.m;
+    const int64_t m2 = 2 * g.m, n = c.N;
     int32_t* colp = ensure<int32_t>(g.colp, m2 > 0 ? m2 : 1);
     if (m2 > 0) k_slots<<<nblk(m2), TB, 0, c.stream>>>(m2, g.col.as<int32_t>(), c.spos.as<int32_t>(), colp);
+    int4* vrec = ensure<int4>(g.vrec, n);
+    k_vrec<<<nblk(n), TB, 0, c.stream>>>(n, g.rowptr.as<int64_t>(), g.kdeg.as<int64_t>(), c.spos.as<int32_t>(), vrec);
 }
 
 void graph_build_csr(Ctx& c, Graph& g) {
