@@ -143,9 +143,19 @@ class Engine:
         return u, v, w, age
 
     # -- one-shot driver ------------------------------------------------------------------
-    def run(self, algo, n_p, tau, delta):
+    def run(self, algo, n_p, tau, delta, out=None):
+        """Whole fast_consensus run; returns ([n_p][n] int32 labelings, stats).  `out`: an
+        optional C-contiguous int32 host array of that shape to write into (a caller that runs
+        repeatedly keeps one: a fresh 256 MB array costs ~20 ms of OS page zeroing on first
+        touch, more than the PCIe download itself)."""
         n = self.n
-        labels = np.empty((n_p, n), np.int32)
+        if out is None:
+            labels = np.empty((n_p, n), np.int32)
+        else:
+            if not (isinstance(out, np.ndarray) and out.dtype == np.int32 and out.shape == (n_p, n)
+                    and out.flags.c_contiguous):
+                raise ValueError("out must be a C-contiguous int32 array of shape (n_p, n)")
+            labels = out
         st = Stats()
         check(self._L.fc_run(self._ctx, int(algo), int(n_p), float(tau), float(delta), ptr(labels),
                              ctypes.byref(st)))
@@ -167,6 +177,12 @@ class Engine:
             check(self._L.fc_get_labels(self._ctx, self._dev(dev_out), 1 if renumber else 0))
             return dev_out
         out = np.empty((count, self.n), np.int32)
+        check(self._L.fc_get_labels(self._ctx, ptr(out), 1 if renumber else 0))
+        return out
+
+    def get_labels_into(self, out, renumber=False):
+        """Like get_labels(out.shape[0], ...) into a caller-owned C-contiguous int32 host array."""
+        assert out.dtype == np.int32 and out.ndim == 2 and out.shape[1] == self.n and out.flags.c_contiguous
         check(self._L.fc_get_labels(self._ctx, ptr(out), 1 if renumber else 0))
         return out
 

@@ -361,13 +361,9 @@ __global__ void k_iso_flags(int64_t n, const int32_t* sigma, const int64_t* deg,
     // isolated in nextgraph and has a neighbour in graph (else the reference raises)
     flag[t] = (deg[x] == 0 && rowptr[x + 1] > rowptr[x]) ? 1 : 0;
 }
-// Target of isolated node x: its neighbour in the OLD graph with the minimum old weight;
-// ties -> first in networkx adjacency order = earlier neighbours ascending, then later
-// neighbours by creation age (proof: DESIGN.md; pinned by tests/golden adj snapshots).
-__global__ void k_iso_target(int64_t n, const int32_t* sigma, const int32_t* npos, const int64_t* flag,
-                             const int64_t* pos, const int64_t* rowptr, const int32_t* col, const int32_t* cw,
-                             const int32_t* ceid, const int64_t* eage, int32_t* iso, int64_t* isoidx,
-                             int32_t* target, int32_t* tw) {
+// Isolate bookkeeping in node order t: isoidx[x] = its index among the isolates (or -1).
+__global__ void k_iso_index(int64_t n, const int32_t* sigma, const int64_t* flag, const int64_t* pos, int32_t* iso,
+                            int64_t* isoidx) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     const int32_t x = sigma[t];
@@ -375,16 +371,39 @@ __global__ void k_iso_target(int64_t n, const int32_t* sigma, const int32_t* npo
     const int64_t i = pos[t];
     isoidx[x] = i;
     iso[i] = x;
-    int32_t bw = 0x7fffffff, by = -1;
-    int64_t bs = 0x7fffffffffffffffll;
-    for (int64_t j = rowptr[x]; j < rowptr[x + 1]; ++j) {
-        const int32_t y = col[j], w = cw[j];
-        const int32_t py = npos[y];
-        const int64_t sec = (py < (int32_t)t) ? (int64_t)py : ((int64_t)1 << 62) + eage[ceid[j]];
-        if (w < bw || (w == bw && sec < bs)) { bw = w; bs = sec; by = y; }
+}
+// Target of isolated node x: its neighbour in the OLD graph with the minimum old weight;
+// ties -> first in networkx adjacency order = earlier neighbours ascending, then later
+// neighbours by creation age (proof: DESIGN.md; pinned by tests/golden adj snapshots).
+// One wave per isolate: lanes stride the row, then a lexicographic (w, sec, j) min over the
+// wave -- a row walk of a hub in the old graph was one thread's serial dependent loads.
+__global__ __launch_bounds__(256) void k_iso_target(int64_t k, const int32_t* npos, const int32_t* iso,
+                                                    const int64_t* rowptr, const int32_t* col, const int32_t* cw,
+                                                    const int32_t* ceid, const int64_t* eage, int32_t* target,
+                                                    int32_t* tw) {
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (i >= k) return;                       // wave-uniform
+    const int32_t x = iso[i];
+    const int32_t t = npos[x];
+    int32_t bw = 0x7fffffff;
+    int64_t bs = 0x7fffffffffffffffll, bj = 0x7fffffffffffffffll;
+    for (int64_t j = rowptr[x] + lane; j < rowptr[x + 1]; j += 64) {
+        const int32_t w = cw[j];
+        const int32_t py = npos[col[j]];
+        const int64_t sec = (py < t) ? (int64_t)py : ((int64_t)1 << 62) + eage[ceid[j]];
+        if (w < bw || (w == bw && (sec < bs || (sec == bs && j < bj)))) { bw = w; bs = sec; bj = j; }
     }
-    target[i] = by;
-    tw[i] = bw;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const int32_t ow = __shfl_xor(bw, off);
+        const int64_t os = __shfl_xor(bs, off), oj = __shfl_xor(bj, off);
+        if (ow < bw || (ow == bw && (os < bs || (os == bs && oj < bj)))) { bw = ow; bs = os; bj = oj; }
+    }
+    if (lane == 0) {
+        target[i] = bj != 0x7fffffffffffffffll ? col[bj] : -1;
+        tw[i] = bw;
+    }
 }
 // Sequential live-isolates semantics (nx.isolates is a lazy generator): x is skipped iff
 // an earlier repaired node chose x.  Resolved by Jacobi sweeps over the DAG x' -> T(x').
@@ -439,9 +458,10 @@ static int64_t repair(Ctx& c, int iteration) {
     int64_t* isoidx = ensure<int64_t>(c.isoflag, n);
     int32_t* target = ensure<int32_t>(c.target, k);
     int32_t* tw = ensure<int32_t>(c.tw, k);
-    k_iso_target<<<nblk(n), TB, 0, c.stream>>>(n, sigma, npos, fl, ps, g.rowptr.as<int64_t>(), g.col.as<int32_t>(),
-                                                g.cw.as<int32_t>(), g.ceid.as<int32_t>(), g.eage.as<int64_t>(), iso,
-                                                isoidx, target, tw);
+    k_iso_index<<<nblk(n), TB, 0, c.stream>>>(n, sigma, fl, ps, iso, isoidx);
+    k_iso_target<<<nblk(k * 64), TB, 0, c.stream>>>(k, npos, iso, g.rowptr.as<int64_t>(), g.col.as<int32_t>(),
+                                                     g.cw.as<int32_t>(), g.ceid.as<int32_t>(), g.eage.as<int64_t>(),
+                                                     target, tw);
     int32_t* active = ensure<int32_t>(c.active, k);
     int32_t* hit = ensure<int32_t>(c.hit, k + 1);
     int32_t* changed = hit + k;

@@ -6,6 +6,8 @@ rule depends on replica order, fast_consensus.py:154-159).  Every rank keeps an 
 copy of the graph; the only data-path exchanges are
   * per-edge partials: Louvain k_last (all-reduce MAX) / LPM co-membership counts (SUM);
   * per-candidate closure co-membership counts (SUM, louvain only);
+both travel as uint8 when n_p <= 255 (k_last + 1 and counts are in [0, n_p]): a quarter
+of the int32 bytes on every xGMI ring hop;
 after which threshold, check, closure (same counter-based RNG on every rank), repair and
 the graph rebuild run replicated and deterministically -- no graph broadcast.  The final
 partitions are all-gathered to rank 0.  The loop mirrors fc_run (capi.cpp) step for step,
@@ -31,15 +33,33 @@ def shard(n_p, rank, world):
     return n_p * rank // world, n_p * (rank + 1) // world
 
 
-def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True):
-    """Returns (labels [n_p][N] on rank 0 (None elsewhere), stats dict)."""
+def _all_reduce_small(t, op, n_p, world, shift):
+    """In-place all-reduce of int32 values in [-shift, n_p - shift] (MAX, or SUM of per-rank
+    counts whose total is <= n_p); as uint8 when n_p <= 255.  Exact: MAX commutes with the
+    +shift, and every partial SUM is a count of replicas, <= n_p."""
+    if world <= 1:
+        return t
+    if n_p > 255:
+        dist.all_reduce(t, op=op)
+        return t
+    b = (t + shift).to(torch.uint8)
+    dist.all_reduce(b, op=op)
+    t.copy_(b)
+    if shift:
+        t.sub_(shift)
+    return t
+
+
+def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True, out=None):
+    """Returns (labels [n_p][N] on rank 0 (None elsewhere), stats dict).  `out`: optional
+    C-contiguous int32 host array [n_p][N] that rank 0 downloads into (see Engine.run)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     r0, r1 = shard(n_p, rank, world)
     louv = algo in (LOUVAIN, LOUVAIN_NC)    # louvain loop: check #1, closure counts, repair
     on_gpu = str(device).startswith("cuda")
     if not on_gpu:
-        return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv)
+        return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out)
     # engine kernels and torch/RCCL ops on ONE explicit stream: no cross-stream races
     # (torch's default stream is the legacy null stream, which the engine cannot adopt)
     stream = torch.cuda.Stream(device=device)
@@ -47,13 +67,13 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     engine.set_stream(stream.cuda_stream)
     try:
         with torch.cuda.stream(stream):
-            return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv)
+            return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out)
     finally:
         stream.synchronize()
         engine.set_stream(None)
 
 
-def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv):
+def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out=None):
     mine = r1 - r0
     engine.reset_graph()
     n, _, L = engine.graph_info()
@@ -70,8 +90,11 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
             engine.consensus_partial(algo, part)                     # :150-159 / :273-280
         else:
             part.fill_(-1 if algo == LOUVAIN else 0)
-        if world > 1:   # louvain: k_last (MAX); lpm / new_consensus rule: counts (SUM)
-            dist.all_reduce(part, op=dist.ReduceOp.MAX if algo == LOUVAIN else dist.ReduceOp.SUM)
+        # louvain: k_last in [-1, n_p-1] (MAX); lpm / new_consensus rule: counts in [0, n_p] (SUM)
+        if algo == LOUVAIN:
+            _all_reduce_small(part, dist.ReduceOp.MAX, n_p, world, 1)
+        else:
+            _all_reduce_small(part, dist.ReduceOp.SUM, n_p, world, 0)
         st["partition_edges"] += n_p * m
         conv1, kept, unc = engine.consensus_apply(algo, n_p, tau, delta, part)   # :163-173
         if louv and conv1:
@@ -83,8 +106,7 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
             cnt = torch.zeros(nc, dtype=torch.int32, device=device)
             if mine > 0:
                 engine.closure_partial(cnt)                          # :186-190
-            if world > 1:
-                dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+            _all_reduce_small(cnt, dist.ReduceOp.SUM, n_p, world, 0)
         conv2, _ = engine.closure_apply(algo, n_p, delta, cnt, it)   # :193-202 / :307-310
         it += 1
         if conv2:
@@ -97,6 +119,9 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
     if mine > 0:
         engine.cd(algo, r0, mine, n_p, FINAL_PASS_ITER + it)         # final pass :383-392
     if not gather or world == 1:
+        if mine > 0 and out is not None and world == 1:
+            engine.get_labels_into(out, renumber=True)
+            return out, st
         return (engine.get_labels(mine, renumber=True) if mine > 0 else None), st
     # final partitions: exported straight into the gather buffer (no host round trip), one
     # all-gather, one download on rank 0
@@ -111,9 +136,11 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
     dist.all_gather(bufs, buf)
     if rank != 0:
         return None, st
-    out = np.empty((n_p, n), np.int32)
+    if out is None:
+        out = np.empty((n_p, n), np.int32)
+    host = torch.from_numpy(out)   # device -> the host array directly (no staging tensors)
     for g in range(world):
         a, b = shard(n_p, g, world)
         if b > a:
-            out[a:b] = bufs[g][:b - a].cpu().numpy()
+            host[a:b].copy_(bufs[g][:b - a])
     return out, st

@@ -295,6 +295,23 @@ def test_determinism_same_seed(fcmod):
         np.testing.assert_array_equal(a, b)
 
 
+def test_run_into_caller_buffer(fcmod):
+    """run(out=...) writes the same labelings into a reused host array (bench.py's path)."""
+    case, _ = _lfr1k_graph()
+    with fcmod.Engine(seed=99) as eng:
+        eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+        ref, st_ref = eng.run(0, 8, 0.2, 0.02)
+        out = np.full((8, case.N), -7, np.int32)
+        for _ in range(2):
+            got, st = eng.run(0, 8, 0.2, 0.02, out=out)
+            assert got is out
+            assert {k: v for k, v in st.items() if not k.endswith("_ms")} == \
+                {k: v for k, v in st_ref.items() if not k.endswith("_ms")}
+            np.testing.assert_array_equal(out, ref)
+        with pytest.raises(ValueError):
+            eng.run(0, 8, 0.2, 0.02, out=np.zeros((7, case.N), np.int32))
+
+
 def test_closure_sampler_properties(fcmod):
     """Device closure: every new edge joins two neighbours of some node in the
     post-threshold graph, was absent there, and carries the co-membership count."""
