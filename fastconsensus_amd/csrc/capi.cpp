@@ -131,7 +131,7 @@ void fc_destroy(fc_ctx* ctx) {
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
                       &c.hit, &c.mkey, &c.mkey2, &c.midx, &c.midx2, &c.sort_tmp, &c.nodetmp, &c.nodetmp2,
-                      &c.nodetmp3, &c.part, &c.ccount, &c.tailbuf, &c.tailmark, &c.sigma, &c.npos, &c.spos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
+                      &c.nodetmp3, &c.part, &c.ccount, &c.tailbuf, &c.tailmark, &c.sigma, &c.npos, &c.spos, &c.sinv, &c.tpos, &c.snpos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
                       &c.st_lab};
     for (auto* b : bufs) b->release();
     for (auto e : c.timer.pool) (void)hipEventDestroy(e);

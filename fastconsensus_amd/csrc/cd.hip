@@ -787,14 +787,15 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
     }
 }
 
+// Singletons: label row in slot order (slot i holds vertex sinv[i]), totals in vertex order.
 template <typename TT>
-__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, const int32_t* spos, int32_t* lab, TT* tot,
+__global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, const int32_t* sinv, int32_t* lab, TT* tot,
                           int louv) {
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
-    if (v >= n) return;
-    lab[(int64_t)r * n + spos[v]] = (int32_t)v;
-    if (louv) tot[(int64_t)r * n + v] = (TT)kdeg[v];
+    if (i >= n) return;
+    lab[(int64_t)r * n + i] = sinv[i];
+    if (louv) tot[(int64_t)r * n + i] = (TT)kdeg[i];
 }
 
 // ------------------------------------------------------------------ tail sweeps
@@ -1196,8 +1197,9 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     FC_HIP(hipMemsetAsync(red, 0, zero_bytes, c.stream));
     dim3 ig(nblk(N), rcount);
     const int32_t* spos = c.spos.as<int32_t>();
-    if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), spos, lab, (int32_t*)tot, louv ? 1 : 0);
-    else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), spos, lab, (int64_t*)tot, louv ? 1 : 0);
+    const int32_t* sinv = c.sinv.as<int32_t>();
+    if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int32_t*)tot, louv ? 1 : 0);
+    else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int64_t*)tot, louv ? 1 : 0);
     FC_REQUIRE(!louv || (double)g.max_kdeg * (double)g.M2 < 4.0e18, FC_ELIMIT,
                "edge weights too large for exact int64 modularity gains");
 
@@ -1306,23 +1308,26 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
 }
 
 // ------------------------------------------------------------------ transpose / renumber
-// lab [n_r][N] -> labT [N][ldT]  (64x64 tiles through LDS, both sides coalesced)
-__global__ __launch_bounds__(256) void k_transpose(int64_t N, int n_r, int ldT, const int32_t* lab, const int32_t* spos,
+// lab [n_r][N] (slot order) -> labT [N][ldT] (vertex rows): 64 slots x 64 replicas per tile
+// through LDS; rows read coalesced, each vertex's 64 labels written as one 256-byte run
+__global__ __launch_bounds__(256) void k_transpose(int64_t N, int n_r, int ldT, const int32_t* lab, const int32_t* sinv,
                                                   int32_t* labT) {
     __shared__ int32_t t[64][65];
-    const int64_t v0 = (int64_t)blockIdx.x * 64;
+    __shared__ int32_t sv[64];
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
     const int r0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    if (ty == 0) sv[tx] = s0 + tx < N ? sinv[s0 + tx] : -1;
     for (int rr = ty; rr < 64; rr += 4) {
         const int r = r0 + rr;
-        const int64_t v = v0 + tx;
-        if (r < n_r && v < N) t[rr][tx] = lab[(int64_t)r * N + spos[v]];
+        const int64_t s = s0 + tx;
+        if (r < n_r && s < N) t[rr][tx] = lab[(int64_t)r * N + s];
     }
     __syncthreads();
-    for (int vv = ty; vv < 64; vv += 4) {
-        const int64_t v = v0 + vv;
+    for (int ss = ty; ss < 64; ss += 4) {
+        const int32_t v = sv[ss];
         const int r = r0 + tx;
-        if (v < N && r < n_r) labT[v * ldT + r] = t[tx][vv];
+        if (v >= 0 && r < n_r) labT[(int64_t)v * ldT + r] = t[tx][ss];
     }
 }
 void labels_transpose(Ctx& c) {
@@ -1330,7 +1335,7 @@ void labels_transpose(Ctx& c) {
     c.ldT = (c.n_r + 3) & ~3;
     int32_t* labT = ensure<int32_t>(c.labT, (size_t)c.N * c.ldT);
     dim3 grid(nblk(c.N, 64), (c.n_r + 63) / 64);
-    k_transpose<<<grid, TB, 0, c.stream>>>(c.N, c.n_r, c.ldT, c.lab.as<int32_t>(), c.spos.as<int32_t>(), labT);
+    k_transpose<<<grid, TB, 0, c.stream>>>(c.N, c.n_r, c.ldT, c.lab.as<int32_t>(), c.sinv.as<int32_t>(), labT);
     c.labT_valid = true;
 }
 
@@ -1338,20 +1343,31 @@ __global__ void k_first_init(int64_t total, int32_t* first) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < total) first[i] = 0x7fffffff;
 }
-// first[r][c] = earliest NODE position of community c
-__global__ void k_first_min(int64_t N, const int32_t* lab, const int32_t* spos, const int32_t* npos, int32_t* first) {
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// first[r][c] = earliest NODE position of community c.  Rows walk in slot order, which is
+// community order at load, so a wave often holds one label: the lanes sharing lane 0's
+// label fold their minimum first and issue one atomic.
+__global__ __launch_bounds__(256) void k_first_min(int64_t N, const int32_t* lab, const int32_t* snpos, int32_t* first) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int r = blockIdx.y;
-    if (v < N) atomicMin(&first[(int64_t)r * N + lab[(int64_t)r * N + spos[v]]], npos[v]);
+    const bool ok = s < N;
+    const int32_t c = ok ? lab[(int64_t)r * N + s] : -1;
+    const int32_t t = ok ? snpos[s] : 0x7fffffff;
+    const int32_t c0 = __shfl(c, 0);
+    const bool same = ok && c == c0;
+    int32_t m = same ? t : 0x7fffffff;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = min(m, __shfl_xor(m, off));
+    if ((threadIdx.x & 63) == 0) { if (c0 >= 0) atomicMin(&first[(int64_t)r * N + c0], m); }
+    else if (ok && !same) atomicMin(&first[(int64_t)r * N + c], t);
 }
 // over node order t: out[r][t] = raw label of node t; flag = t opens its community
-__global__ void k_node_order(int64_t N, int64_t total, const int32_t* lab, const int32_t* sigma, const int32_t* spos,
+__global__ void k_node_order(int64_t N, int64_t total, const int32_t* lab, const int32_t* tpos,
                              const int32_t* first, int32_t* out, int32_t* flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > total) return;
     if (i == total) { if (flag) flag[i] = 0; return; }
     const int64_t r = i / N, t = i % N;
-    const int32_t c = lab[r * N + spos[sigma[t]]];
+    const int32_t c = lab[r * N + tpos[t]];
     out[i] = c;
     if (flag) flag[i] = first[r * N + c] == (int32_t)t ? 1 : 0;
 }
@@ -1371,11 +1387,10 @@ void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
     int32_t* rank = renumber ? ensure<int32_t>(c.hit, total + 1) : nullptr;
     if (renumber) {
         k_first_init<<<nblk(total), TB, 0, c.stream>>>(total, first);
-        k_first_min<<<dim3(nblk(N), c.n_r), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), c.spos.as<int32_t>(),
-                                                               c.npos.as<int32_t>(), first);
+        k_first_min<<<dim3(nblk(N), c.n_r), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), c.snpos.as<int32_t>(), first);
     }
-    k_node_order<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), c.sigma.as<int32_t>(),
-                                                       c.spos.as<int32_t>(), first, out, flag);
+    k_node_order<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), c.tpos.as<int32_t>(), first, out,
+                                                       flag);
     if (renumber) {
         exclusive_scan(c, flag, rank, total + 1);
         k_relabel_out<<<nblk(total), TB, 0, c.stream>>>(N, total, out, first, rank);
@@ -1384,12 +1399,11 @@ void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
     FC_HIP(hipMemcpyAsync(host, out, 4 * (size_t)total, hipMemcpyDefault, c.stream));
     sync(c);
 }
-__global__ void k_from_node_order(int64_t N, int64_t total, const int32_t* in, const int32_t* sigma,
-                                  const int32_t* spos, int32_t* lab) {
+__global__ void k_from_node_order(int64_t N, int64_t total, const int32_t* in, const int32_t* tpos, int32_t* lab) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total) return;
     const int64_t r = i / N, t = i % N;
-    lab[r * N + spos[sigma[t]]] = in[i];   // label values only matter through equality
+    lab[r * N + tpos[t]] = in[i];   // label values only matter through equality
 }
 // Host labelings in node order -> local replicas (replay).
 void labels_from_host(Ctx& c, int count, const int32_t* host) {
@@ -1397,7 +1411,7 @@ void labels_from_host(Ctx& c, int count, const int32_t* host) {
     int32_t* in = ensure<int32_t>(c.st_lab, total + 1);
     FC_HIP(hipMemcpyAsync(in, host, 4 * (size_t)total, hipMemcpyHostToDevice, c.stream));
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)total);
-    k_from_node_order<<<nblk(total), TB, 0, c.stream>>>(N, total, in, c.sigma.as<int32_t>(), c.spos.as<int32_t>(), lab);
+    k_from_node_order<<<nblk(total), TB, 0, c.stream>>>(N, total, in, c.tpos.as<int32_t>(), lab);
     sync(c);
 }
 
@@ -1437,4 +1451,21 @@ void store_order(Ctx& c) {
     c.n_r = 0;
     sync(c);
 }
+__global__ void k_slot_maps(int64_t N, const int32_t* spos, const int32_t* npos, int32_t* sinv, int32_t* tpos,
+                            int32_t* snpos) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= N) return;
+    const int32_t s = spos[v], t = npos[v];
+    sinv[s] = (int32_t)v;
+    snpos[s] = t;
+    tpos[t] = s;        // sigma[t] == v
+}
+void slot_maps(Ctx& c) {
+    const int64_t N = c.N;
+    int32_t* sinv = ensure<int32_t>(c.sinv, N);
+    int32_t* tpos = ensure<int32_t>(c.tpos, N);
+    int32_t* snpos = ensure<int32_t>(c.snpos, N);
+    k_slot_maps<<<nblk(N), TB, 0, c.stream>>>(N, c.spos.as<int32_t>(), c.npos.as<int32_t>(), sinv, tpos, snpos);
+}
+
 }  // namespace fc

@@ -92,6 +92,9 @@ struct Ctx {
     // internal vertex numbering: internal = sigma[node], node = npos[internal] (a seeded
     // random permutation, or the identity): engine behaviour is independent of input order
     DevBuf sigma, npos;             // int32 [N]
+    // label storage maps (int32 [N], slot_maps()): sinv slot -> internal vertex, tpos node
+    // position -> slot, snpos slot -> node position; label-row passes walk rows in slot order
+    DevBuf sinv, tpos, snpos;
     std::vector<int32_t> h_sigma;
     DevBuf st_u, st_v, st_w, st_age, st_lab;   // host-facing staging (node space)
     int key_bits = 1;               // bits to hold a node id (N <= 2^key_bits)
@@ -151,6 +154,7 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src);
 // cd.cpp
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
 void store_order(Ctx& c);             // Ctx::spos from a one-replica Louvain run (FC_OPT_STORE)
+void slot_maps(Ctx& c);               // Ctx::sinv / tpos / snpos from spos
 void graph_slots(Ctx& c, Graph& g);   // g.colp = spos[g.col]
 void labels_transpose(Ctx& c);
 void labels_to_host(Ctx& c, int32_t* out, bool renumber);   // node order [n_r][N]

@@ -190,10 +190,12 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
                                                     g.ew.as<int32_t>(), g.eage.as<int64_t>());
     c.m_original = mu;   // L = G.number_of_edges() (fast_consensus.py:132, :144)
     graph_build_csr(c, g);
+    slot_maps(c);        // identity storage (the ordering pass below runs on it)
     if (c.store_order && g.M2 > 0) {
         store_order(c);
         graph_slots(c, g);
     }
+    slot_maps(c);
     graph_copy(c, c.g0, g);
     c.labT_valid = false;
     sync(c);   // the mapped host edge arrays die here

@@ -20,3 +20,16 @@ pin = torch.empty(n, dtype=torch.int32, pin_memory=True)
 print("pinned copy_:", tm(lambda: pin.copy_(t)))
 a = np.empty(n, np.int32)
 print("pinned->fresh np copy:", tm(lambda: np.copyto(np.empty(n, np.int32), pin.numpy())))
+
+# hipMemcpyAsync kinds into a touched pageable numpy array (what labels_to_host does)
+import ctypes
+hip = ctypes.CDLL("libamdhip64.so")
+hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+a = np.zeros(n, np.int32)
+s = torch.cuda.current_stream().cuda_stream
+for kind, name in ((2, "DeviceToHost"), (4, "Default")):
+    def f():
+        assert hip.hipMemcpyAsync(a.ctypes.data, t.data_ptr(), 4 * n, kind, s) == 0
+        assert hip.hipStreamSynchronize(s) == 0
+    print("hipMemcpyAsync %s touched pageable:" % name, tm(f))
