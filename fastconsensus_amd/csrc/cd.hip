@@ -41,7 +41,12 @@ static constexpr int CHUNK = 16;
 static constexpr int TILE = 16;         // lanes per decision in k_apply's row scatter
 static constexpr int TILES = TB / TILE;
 static constexpr int WNT = 8;           // vertices per wave in the light decide (rows flattened over 64 lanes)
-static constexpr int LNT = WNT * (TB / 64);   // vertices per k_decide_light block (one item)
+#ifndef FC_DTB
+#define FC_DTB 64
+#endif
+static constexpr int DTB = FC_DTB;      // threads per k_decide_light block: one wave (LFR-1M 257.9 ms at 256,
+                                        // 255.6 at 128, 254.1 at 64; 266.5 at 512)
+static constexpr int LNT = WNT * (DTB / 64);  // vertices per k_decide_light block (one item)
 static constexpr int HCAP = 64;         // slots per tile table (>= LIGHT_MAX_DEG: every insert finds a slot)
 static constexpr int LIGHT_MAX_DEG = 64;
 static constexpr int HEAVY_LDS_SLOTS = 4096;
@@ -507,9 +512,9 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
 }
 
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int sweep, int X) {
-    __shared__ WaveShared s_ws[TB / 64];
-    __shared__ unsigned long long s_red[2][TB / 64][5];   // by item parity (no second barrier)
+__global__ __launch_bounds__(DTB) void k_decide_light(CDArgs a, int bucket, int sweep, int X) {
+    __shared__ WaveShared s_ws[DTB / 64];
+    __shared__ unsigned long long s_red[2][DTB / 64][5];   // by item parity (no second barrier)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // One item (LNT list entries of one replica) per block.  Every replica owns X item slots
     // (X = the sweep's largest per-replica round, from the host's one read per sweep); slots
@@ -564,7 +569,7 @@ __global__ __launch_bounds__(256) void k_decide_light(CDArgs a, int bucket, int 
     __syncthreads();
     if (threadIdx.x < 5) {
         unsigned long long sm = 0;
-        for (int k = 0; k < TB / 64; ++k) sm += s_red[par][k][threadIdx.x];
+        for (int k = 0; k < DTB / 64; ++k) sm += s_red[par][k][threadIdx.x];
         // fields: s_red 0 dq -> 0, 1 unstable -> 1, 2 verts -> 3, 3 entries -> 4, 4 cands -> 5
         if (sm) atomicAdd(red_slot(a, r, threadIdx.x < 2 ? threadIdx.x : threadIdx.x + 1), sm);
     }
@@ -1102,7 +1107,7 @@ static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy,
     const int ev = timer_begin(c);
     // one item per block: X item slots per replica, rounded up to whole XCD groups of 8
     const int64_t grid = (((int64_t)a.n_r * X + 7) / 8) * 8;
-    k_decide_light<LOUV, TT><<<(unsigned)grid, TB, 0, c.stream>>>(a, k, sweep, X);
+    k_decide_light<LOUV, TT><<<(unsigned)grid, DTB, 0, c.stream>>>(a, k, sweep, X);
     timer_end(c, 4, ev);
     if (any_heavy) k_decide_heavy<LOUV, TT><<<HEAVY_GRID, TB, 0, c.stream>>>(a, k, sweep);
     // apply: FC_APPLY_BLOCKS blocks per replica, more when few replicas share the GPU (a
