@@ -40,7 +40,11 @@ static constexpr int CHUNK = 16;
 
 static constexpr int TILE = 16;         // lanes per decision in k_apply's row scatter
 static constexpr int TILES = TB / TILE;
-static constexpr int WNT = 8;           // vertices per wave in the light decide (rows flattened over 64 lanes)
+#ifndef FC_WNT
+#define FC_WNT 8
+#endif
+static constexpr int WNT = FC_WNT;      // vertices per wave in the light decide (rows flattened over 64 lanes;
+                                        // LFR-1M 254 ms at 8, 308 ms at 4)
 #ifndef FC_DTB
 #define FC_DTB 64
 #endif
