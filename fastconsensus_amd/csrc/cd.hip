@@ -39,7 +39,11 @@ static constexpr int TB = 256;
 static constexpr int CHUNK = 16;
 
 static constexpr int TILE = 16;         // lanes per decision in k_apply's row scatter
-static constexpr int TILES = TB / TILE;
+#ifndef FC_ATB
+#define FC_ATB 256
+#endif
+static constexpr int ATB = FC_ATB;      // threads per k_apply block
+static constexpr int TILES = ATB / TILE;
 #ifndef FC_WNT
 #define FC_WNT 8
 #endif
@@ -708,7 +712,7 @@ __device__ __forceinline__ void apply_move(const CDArgs& a, int r, const int4& d
     }
 }
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
+__global__ __launch_bounds__(ATB) void k_apply(CDArgs a, int bucket) {
     const int r = blockIdx.y;
     if (!a.active[r]) return;
     const int64_t seg = (int64_t)bucket * a.n_r + r;
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(256) void k_apply(CDArgs a, int bucket) {
     const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
     int moved = 0;
     if (!push && !trk) {
-        for (int64_t di = (int64_t)blockIdx.x * TB + threadIdx.x; di < len; di += (int64_t)gridDim.x * TB) {
+        for (int64_t di = (int64_t)blockIdx.x * ATB + threadIdx.x; di < len; di += (int64_t)gridDim.x * ATB) {
             const int4 dv = decr[di];
             if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]); ++moved; }
         }
@@ -820,7 +824,10 @@ __global__ void k_cd_init(int64_t n, int n_r, const int64_t* kdeg, const int32_t
 //     barrier, moves applied, barrier.
 // The first sweep's visit list is the one k_list_fill built for it (bucketed, flags cleared).
 static constexpr int TAIL_MAXB = 256;
-static constexpr int TAIL_TB = 1024;     // threads per replica workgroup in k_cd_tail
+#ifndef FC_TAIL_TB
+#define FC_TAIL_TB 1024
+#endif
+static constexpr int TAIL_TB = FC_TAIL_TB;   // threads per replica workgroup in k_cd_tail
 template <bool LOUV, typename TT, int NTH>
 __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_sweeps, int32_t* tbuf,
                                                  int32_t* tmark, unsigned long long* tail_acc, int32_t* n_active_out) {
@@ -1119,7 +1126,7 @@ static void sub_round(Ctx& c, const CDArgs& a, int k, int sweep, bool any_heavy,
     // no more than the round's decisions fill (16-lane tiles)
     const int64_t ab = std::min<int64_t>(std::max<int64_t>(c.apply_blocks, (2048 + a.n_r - 1) / a.n_r),
                                          std::max<int64_t>(1, ((int64_t)X * LNT + TILES - 1) / TILES));
-    k_apply<LOUV, TT><<<dim3((unsigned)ab, a.n_r), TB, 0, c.stream>>>(a, k);
+    k_apply<LOUV, TT><<<dim3((unsigned)ab, a.n_r), ATB, 0, c.stream>>>(a, k);
 }
 
 __global__ void k_count_heavy(int64_t n, const int64_t* rowptr, int64_t thr, unsigned long long* out) {
