@@ -43,8 +43,10 @@ def _worker(rank, world, port, algo, n_p, tau, delta, out_path):
         N, e = _graph()
         eng = OracleEngine(seed=17, sigma=_sigma(N))
         eng.load_graph(N, e[:, 0], e[:, 1])
-        labels, st = run_sharded(eng, algo, n_p, tau, delta, device="cpu", max_iters=50)
+        host = np.full((n_p, N), -9, np.int32) if rank == 0 else None   # rank 0 downloads into it
+        labels, st = run_sharded(eng, algo, n_p, tau, delta, device="cpu", max_iters=50, out=host)
         if rank == 0:
+            assert labels is host
             u, v, w, age = eng.get_graph()
             np.savez(out_path, labels=labels, u=u, v=v, w=w, age=age, iters=st["iterations"],
                      pe=st["partition_edges"])
@@ -84,3 +86,40 @@ def test_shard_ranges_cover_contiguously():
             ranges = [shard(n_p, r, w) for r in range(w)]
             assert ranges[0][0] == 0 and ranges[-1][1] == n_p
             assert all(ranges[i][1] == ranges[i + 1][0] for i in range(w - 1))
+
+
+def _reduce_worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fastconsensus_amd.distributed import _all_reduce_small
+        res = {}
+        for n_p in (7, 255, 300):
+            rng = np.random.default_rng(100 * rank + n_p)
+            # k_last in [-1, n_p-1] (MAX); per-rank counts summing to <= n_p (SUM)
+            k = torch.from_numpy(rng.integers(-1, n_p, 1000).astype(np.int32))
+            c = torch.from_numpy(rng.integers(0, n_p // world + 1, 1000).astype(np.int32))
+            res["max%d" % n_p] = _all_reduce_small(k.clone(), dist.ReduceOp.MAX, n_p, world, 1).numpy()
+            res["sum%d" % n_p] = _all_reduce_small(c.clone(), dist.ReduceOp.SUM, n_p, world, 0).numpy()
+            res["k%d" % n_p], res["c%d" % n_p] = k.numpy(), c.numpy()
+        np.savez(out_path + ".%d.npz" % rank, **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_small_all_reduce_exact():
+    """uint8 collectives (n_p <= 255, k_last shifted by +1) and the int32 fallback give the
+    exact int32 MAX / SUM."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "red")
+        mp.spawn(_reduce_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        z = [np.load(out + ".%d.npz" % r) for r in range(world)]
+        for n_p in (7, 255, 300):
+            kmax = np.maximum(z[0]["k%d" % n_p], z[1]["k%d" % n_p])
+            csum = z[0]["c%d" % n_p] + z[1]["c%d" % n_p]
+            for r in range(world):
+                np.testing.assert_array_equal(z[r]["max%d" % n_p], kmax)
+                np.testing.assert_array_equal(z[r]["sum%d" % n_p], csum)
+                assert z[r]["max%d" % n_p].dtype == np.int32
