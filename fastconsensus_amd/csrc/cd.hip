@@ -1359,22 +1359,36 @@ __global__ void k_first_init(int64_t total, int32_t* first) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < total) first[i] = 0x7fffffff;
 }
-// first[r][c] = earliest NODE position of community c.  Rows walk in slot order, which is
-// community order at load, so a wave often holds one label: the lanes sharing lane 0's
-// label fold their minimum first and issue one atomic.
+// first[r][c] = earliest NODE position of community c.  A block takes FM_SPAN consecutive
+// slots of one row -- slot order is community order at load, so they hold few distinct
+// labels -- folds them into an LDS table (label -> min position), and issues one global
+// atomic per distinct label.  Labels overflowing the table (more distinct labels than
+// FM_SLOTS / 2 in a span) go straight to global memory.
+static constexpr int FM_SPAN = 2048, FM_SLOTS = 1024;
 __global__ __launch_bounds__(256) void k_first_min(int64_t N, const int32_t* lab, const int32_t* snpos, int32_t* first) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ int32_t key[FM_SLOTS], val[FM_SLOTS];
     const int r = blockIdx.y;
-    const bool ok = s < N;
-    const int32_t c = ok ? lab[(int64_t)r * N + s] : -1;
-    const int32_t t = ok ? snpos[s] : 0x7fffffff;
-    const int32_t c0 = __shfl(c, 0);
-    const bool same = ok && c == c0;
-    int32_t m = same ? t : 0x7fffffff;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = min(m, __shfl_xor(m, off));
-    if ((threadIdx.x & 63) == 0) { if (c0 >= 0) atomicMin(&first[(int64_t)r * N + c0], m); }
-    else if (ok && !same) atomicMin(&first[(int64_t)r * N + c], t);
+    const int64_t s0 = (int64_t)blockIdx.x * FM_SPAN;
+    const int32_t* labr = lab + (int64_t)r * N;
+    int32_t* fr = first + (int64_t)r * N;
+    for (int k = threadIdx.x; k < FM_SLOTS; k += 256) { key[k] = -1; val[k] = 0x7fffffff; }
+    __syncthreads();
+    for (int k = threadIdx.x; k < FM_SPAN; k += 256) {
+        const int64_t s = s0 + k;
+        if (s >= N) break;
+        const int32_t c = labr[s], t = snpos[s];
+        uint32_t h = hash32((uint32_t)c) & (FM_SLOTS - 1);
+        bool done = false;
+        for (int probe = 0; probe < 16 && !done; ++probe) {   // bounded probing, then global
+            const int32_t prev = atomicCAS(&key[h], -1, c);
+            if (prev == -1 || prev == c) { atomicMin(&val[h], t); done = true; }
+            else h = (h + 1) & (FM_SLOTS - 1);
+        }
+        if (!done) atomicMin(&fr[c], t);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < FM_SLOTS; k += 256)
+        if (key[k] >= 0) atomicMin(&fr[key[k]], val[k]);
 }
 // over node order t: out[r][t] = raw label of node t; flag = t opens its community
 __global__ void k_node_order(int64_t N, int64_t total, const int32_t* lab, const int32_t* tpos,
@@ -1403,7 +1417,8 @@ void labels_to_host(Ctx& c, int32_t* host, bool renumber) {
     int32_t* rank = renumber ? ensure<int32_t>(c.hit, total + 1) : nullptr;
     if (renumber) {
         k_first_init<<<nblk(total), TB, 0, c.stream>>>(total, first);
-        k_first_min<<<dim3(nblk(N), c.n_r), TB, 0, c.stream>>>(N, c.lab.as<int32_t>(), c.snpos.as<int32_t>(), first);
+        k_first_min<<<dim3((unsigned)((N + FM_SPAN - 1) / FM_SPAN), c.n_r), 256, 0, c.stream>>>(
+            N, c.lab.as<int32_t>(), c.snpos.as<int32_t>(), first);
     }
     k_node_order<<<nblk(total + 1), TB, 0, c.stream>>>(N, total, c.lab.as<int32_t>(), c.tpos.as<int32_t>(), first, out,
                                                        flag);
