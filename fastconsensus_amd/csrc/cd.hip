@@ -390,9 +390,13 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             ws.kown[t] = val;
             if (LOUV) { rec[it] = -1; continue; }   // LPA: the own label competes
         }
-        atomicMax(&ws.vm[t], val);
+        if (LOUV) atomicMax(&ws.vm[t], val);
+        // LPA: count and tie key in one packed max, (count << 32) | hash (the hash is a
+        // bijection of the label: no id tie remains; the winner is recovered by inversion)
+        else atomicMax(&ws.k2[t], ((unsigned long long)(uint32_t)val << 32) | hash32(ws.tvh[t] ^ (uint32_t)key));
     }
     wave_sync();
+    if (!LOUV && lane < WNT && ws.k2[lane]) ws.vm[lane] = (int32_t)(ws.k2[lane] >> 32);   // read by this lane only
     PST(5);
     int ncand = 0;
     auto score = [&](int32_t val, long long tt, long long kvt) -> long long {
@@ -415,7 +419,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     // winner's id is recovered by inverting it.  The separate tie pass runs only when a
     // lower-val candidate may still reach the best score (rare).
     constexpr bool PK = LOUV && sizeof(TT) == 4;
-    bool slow = !PK;                             // wave-uniform: generic tie pass (k2)
+    bool slow = LOUV && !PK;                     // wave-uniform: generic tie pass (k2)
     if (LOUV) {
         // among the max-val candidates the score is vm*2M - k_v*Sigma: the smallest Sigma wins
 #pragma unroll
@@ -499,7 +503,8 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     if (work && ws.vm[lane] != INT_MIN) {        // some candidate besides the own community (Louvain)
         const long long best_s = best_of(lane);
         {
-            const int32_t best_c = slow ? (int32_t)~(uint32_t)ws.k2[lane]
+            const int32_t best_c = !LOUV ? (int32_t)(hash32_inv((uint32_t)ws.k2[lane]) ^ ws.tvh[lane])
+                                 : slow ? (int32_t)~(uint32_t)ws.k2[lane]
                                         : (int32_t)(hash32_inv(~(uint32_t)ws.tb[lane]) ^ ws.tvh[lane]);
             const TT kown = (TT)ws.kown[lane];
             if (LOUV) {
