@@ -1,18 +1,26 @@
 #!/usr/bin/env python3
-"""Benchmark: fast_consensus() hot path on MI355X (BASELINE.json metric).
+"""Benchmark: fast_consensus() hot path on MI355X (BASELINE.json metric, SURVEY.md §8(d)).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config lfr1m|lfr100k|lfr1k|sbm4m]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config lfr1m|lfr100k|lfr100k_lpm|lfr1k|sbm4m]
 
-One step = one whole fast_consensus(G, algorithm, n_p, tau, delta) run on a synthetic
-graph that is already resident in HBM (every iteration + the final pass, final labels
-landed on the host).  value = partition*edges/s = (sum_iter n_p*m_iter + n_p*m_final) /
-wall, aggregated over all ranks (replicas are sharded: strong scaling, n_p fixed).
-Multi-GPU: launched by torch.distributed.run, one rank per GPU, RCCL all-reduces.
+One step = one whole fast_consensus(G, algorithm, n_p, tau, delta) call as §8(d) metric (1)
+defines it: graph upload from host arrays (PCIe + device ingest + CSR build) -> every
+consensus iteration -> the final pass -> the n_p final labelings landed in a host array.
+value = partition*edges/s = (sum_iter n_p*m_iter + n_p*m_final) / wall, aggregated over all
+ranks (replicas are sharded: strong scaling, n_p fixed).  The loop alone (graph already
+resident) is reported beside it as `loop_ms_per_step`.
+
+--gpus N > 1 without a torch.distributed launcher: this script starts N ranks under
+torch.distributed.run itself (one per GPU, RCCL) and exits with their status.  Under a
+launcher, --gpus must equal WORLD_SIZE (a mismatch exits non-zero, never a mislabelled line).
 Progress goes to stderr; rank 0 prints ONE JSON line on stdout.
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -56,31 +64,92 @@ def make_graph(cfg, seed):
     return cfg["n"], u, v, planted
 
 
-def cpu_baseline(n, u, v, cfg, budget_s=20.0):
-    """Reference-semantics CPU port (oracle/, kind 'port') on the host cores: sequential
-    python-louvain level-0 / igraph-LPA restatement per replica, replicas in parallel over
-    threads, then the O(m*n_p) consensus update on those replicas.  Bounded sample."""
+# ------------------------------------------------------------------------------- CPU baseline
+def host_cpu_share():
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU quota (a GPU box
+    grants each GPU a share of the machine; os.cpu_count() shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, p = open(path).read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, math.ceil(int(q) / int(p))))
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            n = min(n, max(1, math.ceil(q / p)))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(n, u, v, cfg, seed):
+    """Reference-semantics CPU port (oracle/, kind 'port') on every host core this process may
+    use: ONE full consensus iteration (fast_consensus.py:141-202 louvain / :260-310 lpm) --
+    the sequential python-louvain level-0 / igraph-LPA restatement per replica (replicas in
+    parallel over threads), the O(m*n_p) consensus rule, threshold, check, closure over
+    L = m attempts (O(L): the reference's O(N)-per-sample NodeView conversion is NOT
+    reproduced) and isolate repair.  Bounded sample: the CD runs `threads` replicas (one
+    per thread, all in parallel); the per-iteration time for n_p replicas scales the CD and
+    consensus parts by ceil(n_p / threads) and n_p / threads."""
     from oracle import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = host_cpu_share()
     algo = 0 if cfg["algo"] == "louvain" else 1
+    n_p = cfg["n_p"]
+    reps = max(1, min(n_p, threads))
     g = orc.EdgeGraph.from_lines(n, np.stack([u, v], 1))
-    # calibrate: one replica on one thread, then size the parallel sample to the budget
+    t = {}
     t0 = time.perf_counter()
-    orc.cd_batch(algo, 1, g, seed=1, nthreads=1)
-    one = time.perf_counter() - t0
-    reps = max(1, min(cfg["n_p"], threads * max(1, int(budget_s / max(one, 1e-3) / 2))))
-    reps = max(1, min(reps, threads * 2))
+    lab, _ = orc.cd_batch(algo, reps, g, seed=seed, nthreads=threads)
+    t["cd"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    lab, _ = orc.cd_batch(algo, reps, g, seed=2, nthreads=threads)
-    t_cd = time.perf_counter() - t0
+    w = orc.consensus(algo, g, lab, reps)
+    t["consensus"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    orc.consensus(algo, g, lab, reps)
-    t_cons = time.perf_counter() - t0
-    pe = reps * g.m
-    return {"value": pe / (t_cd + t_cons), "unit": "partition·edges/s", "cores": threads, "kind": "port",
-            "sample": "%d %s replicas (one level-0 run each, sequential reference semantics, %d threads) + "
-                      "consensus update over them on the same graph (n=%d, m=%d): %.1fs CD + %.2fs consensus; "
-                      "closure/repair not sampled" % (reps, cfg["algo"], threads, n, g.m, t_cd, t_cons)}
+    keep = orc.threshold(w, cfg["tau"], reps)
+    kept = orc.EdgeGraph(n, g.u[keep], g.v[keep], w[keep], g.age[keep])
+    orc.check(kept.w, reps, cfg["delta"])
+    t["threshold"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    pairs = orc.closure_sample_pairs(kept, g.m, seed, 0)
+    cu, cv, cw, cf = orc.closure_from_pairs(algo, kept, pairs, lab, reps)
+    closure = orc.EdgeGraph(n, cu, cv, cw, (np.int64(1) << orc.AGE_ITER_SHIFT) + cf)
+    t["closure"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    parts = [kept, closure]
+    if algo == 0:
+        ru, rv, rw, rx = orc.repair(g, kept.degrees() + closure.degrees())
+        parts.append(orc.EdgeGraph(n, ru, rv, rw, (np.int64(1) << orc.AGE_ITER_SHIFT) + orc.AGE_REPAIR_OFFSET + rx))
+    new = orc.concat(parts)
+    orc.check(new.w, reps, cfg["delta"])
+    t["repair_swap"] = time.perf_counter() - t0
+    sample_s = sum(t.values())
+    full_s = (t["cd"] * math.ceil(n_p / reps) + t["consensus"] * n_p / reps + t["threshold"] + t["closure"]
+              + t["repair_swap"])
+    return {"value": n_p * g.m / full_s, "unit": "partition·edges/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "iteration_s": full_s, "sample_s": sample_s,
+            "sample": "ONE full consensus iteration of the reference-semantics C port on %d threads (the CPU "
+                      "share of this process: affinity/cgroup quota; %d CPUs visible; %s): %d sequential %s "
+                      "level-0 replicas in parallel %.2fs, consensus %.2fs, threshold+check %.2fs, closure over "
+                      "L=%d attempts %.2fs, repair+swap %.2fs (n=%d, m=%d). value = n_p*m / one iteration at "
+                      "n_p=%d (CD scaled by ceil(n_p/threads)=%d, consensus by n_p/threads): %.1fs per iteration"
+                      % (threads, os.cpu_count() or 0, cpu_model(), reps, cfg["algo"], t["cd"], t["consensus"],
+                         t["threshold"], g.m, t["closure"], t["repair_swap"], n, g.m, n_p,
+                         math.ceil(n_p / reps), full_s)}
 
 
 def load_traffic(config):
@@ -90,6 +159,26 @@ def load_traffic(config):
             d = json.load(f)
         return d.get("decide_hbm_bytes_per_launch")
     return None
+
+
+# ------------------------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """Start n ranks of this script under torch.distributed.run (a child process: nothing in
+    this parent touches the GPU) and return their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this pool (RCCL)
+    log("[launcher] %s" % " ".join(cmd))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -105,138 +194,184 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) in production; gloo to rehearse N>1 on one GPU")
     ap.add_argument("--prune", type=int, default=-1, help="CD vertex pruning (engine option; -1 = default)")
     ap.add_argument("--relabel", type=int, default=-1, help="internal vertex numbering (engine option; -1 = default)")
+    ap.add_argument("--store", type=int, default=-1, help="label storage order (engine option; -1 = default)")
     ap.add_argument("--coarsen", type=int, default=-1, help="experimental coarse rounds, largest g (engine option)")
     ap.add_argument("--n-p", type=int, default=0, help="experiment: override the config's n_p")
-    ap.add_argument("--ids", default="generator", choices=["generator", "planted"],
-                    help="experiment: renumber node ids by planted community before loading")
+    ap.add_argument("--resident", action="store_true",
+                    help="experiment: time the loop only (graph loaded once before timing)")
+    ap.add_argument("--engine-model", action="store_true",
+                    help="TEST HOOK (launcher tests on CPU): the oracle-backed CPU model of the engine "
+                         "replaces the HIP engine; the line is marked and carries no throughput claim")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.n_p > 0:
         cfg["n_p"] = args.n_p
         cfg["desc"] += " (n_p overridden: %d)" % args.n_p
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            log("bench.py: --gpus %d but WORLD_SIZE=%d: refusing to report a mislabelled line" % (args.gpus, world))
+            sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+
     import torch
     import torch.distributed as dist
 
-    import fastconsensus_amd as fc
+    model = args.engine_model
+    if model:
+        local, dev = 0, "cpu"
+    else:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU
+        dev = "cuda:%d" % local
+    backend = "gloo" if model else args.dist_backend
+    if world > 1:
+        if not model:
+            torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        ws = dist.get_world_size()
+        one = torch.ones(1, dtype=torch.int32, device=dev)
+        dist.all_reduce(one)                       # the collective path itself agrees on the world
+        log("[rank %d] process group: backend=%s world_size=%d all_reduce(1)=%d"
+            % (rank, dist.get_backend(), ws, int(one.item())))
+        if ws != args.gpus or int(one.item()) != args.gpus:
+            log("bench.py: process group reports %d ranks, --gpus %d" % (ws, args.gpus))
+            sys.exit(2)
+
     from fastconsensus_amd.core import ALGORITHMS
     from fastconsensus_amd.distributed import run_sharded
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(1, torch.cuda.device_count())   # rehearsal: several ranks may share one GPU
-    if world > 1:
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.dist_backend)
-    dev = "cuda:%d" % local
-
     t0 = time.time()
     n, u, v, planted = make_graph(cfg, args.seed)
-    if args.ids == "planted" and planted is not None:
-        order = np.argsort(planted, kind="stable")
-        newid = np.empty(n, np.int32)
-        newid[order] = np.arange(n, dtype=np.int32)
-        u, v = newid[u], newid[v]
     log("[rank %d] graph n=%d m=%d generated in %.1fs" % (rank, n, len(u), time.time() - t0))
-    eng = fc.Engine(device=local, seed=args.seed)
-    if args.buckets:
-        eng.set_params(buckets=args.buckets)
-    if args.chunk >= 0:
-        eng.set_option("chunk", args.chunk)
-    if args.prune >= 0:
-        eng.set_option("prune", args.prune)
-    if args.relabel >= 0:
-        eng.set_option("relabel", args.relabel)
-    if args.coarsen >= 0:
-        eng.set_option("coarsen", args.coarsen)
-    t0 = time.time()
-    eng.load_graph(n, u, v)
-    torch.cuda.synchronize()
-    m0 = eng.m
-    log("[rank %d] graph resident in HBM (m=%d) in %.2fs (PCIe upload + ingest, not timed)" % (rank, m0, time.time() - t0))
+    if model:
+        from tests.cpu_engine import OracleEngine
+        eng = OracleEngine(seed=args.seed)
+    else:
+        import fastconsensus_amd as fc
+        eng = fc.Engine(device=local, seed=args.seed)
+        if args.buckets:
+            eng.set_params(buckets=args.buckets)
+        for name in ("chunk", "prune", "relabel", "store", "coarsen"):
+            val = getattr(args, name)
+            if val >= 0:
+                eng.set_option(name, val)
     algo = ALGORITHMS[cfg["algo"]]
 
-    # the final labelings land in ONE host array, allocated and faulted in before timing (as
-    # the graph is resident before timing): a fresh 256 MB array costs ~20 ms of OS page
-    # zeroing on first touch, which is the allocator's cost, not the path's; the PCIe
-    # download itself (~4.5 ms for 256 MB) stays inside every step
+    # the final labelings land in ONE host array, allocated and faulted in before timing: a
+    # fresh 256 MB array costs ~20 ms of OS page zeroing on first touch, which is the
+    # allocator's cost, not the path's; the PCIe download itself stays inside every step
     host_out = np.zeros((cfg["n_p"], n), np.int32) if rank == 0 else None
 
-    def step():
-        if world == 1:
-            labels, st = eng.run(algo, cfg["n_p"], cfg["tau"], cfg["delta"], out=host_out)
-        else:
-            labels, st = run_sharded(eng, algo, cfg["n_p"], cfg["tau"], cfg["delta"], device=dev, out=host_out)
-        return labels, st
+    def sync():
+        if not model:
+            torch.cuda.synchronize()
 
-    for w in range(args.warmup):
+    def step(load):
+        """(stats, load seconds, loop seconds) of one fast_consensus call."""
         t = time.perf_counter()
-        labels, st = step()
-        log("[rank %d] warmup %d: %.1f ms, iterations=%d exit=%d m_final=%d" %
-            (rank, w, 1e3 * (time.perf_counter() - t), st["iterations"], st["exit_check"], st["m_final"]))
-    eng.set_timing(True)
-    eng.collect_timing()  # reset the event log
+        if load:
+            eng.load_graph(n, u, v)            # §8(d) metric (1): upload + ingest are inside the call
+        t1 = time.perf_counter()
+        if world == 1 and not model:
+            _, st = eng.run(algo, cfg["n_p"], cfg["tau"], cfg["delta"], out=host_out)
+        else:
+            _, st = run_sharded(eng, algo, cfg["n_p"], cfg["tau"], cfg["delta"], device=dev, out=host_out)
+        sync()
+        t2 = time.perf_counter()
+        return st, t1 - t, t2 - t1
+
+    if args.resident:
+        eng.load_graph(n, u, v)
+        sync()
+    m0 = len(u)
+    for w in range(args.warmup):
+        st, tl, tr = step(not args.resident)
+        m0 = eng.graph_info()[2]
+        log("[rank %d] warmup %d: load %.1f ms + loop %.1f ms, iterations=%d exit=%d m_final=%d" %
+            (rank, w, 1e3 * tl, 1e3 * tr, st["iterations"], st["exit_check"], st["m_final"]))
+    if not model:
+        eng.set_timing(True)
+        eng.collect_timing()  # reset the event log
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
-    pe_total, iters = 0, []
+    pe_total, iters, m_finals, load_s, loop_s = 0, [], [], 0.0, 0.0
     for k in range(args.steps):
-        t = time.perf_counter()
-        labels, st = step()
+        st, tl, tr = step(not args.resident)
         pe_total += st["partition_edges"]
         iters.append(st["iterations"])
-        log("[rank %d] step %d: %.1f ms, iterations=%d exit=%d m_final=%d" %
-            (rank, k, 1e3 * (time.perf_counter() - t), st["iterations"], st["exit_check"], st["m_final"]))
-    torch.cuda.synchronize()
+        m_finals.append(st["m_final"])
+        load_s += tl
+        loop_s += tr
+        log("[rank %d] step %d: load %.1f ms + loop %.1f ms, iterations=%d exit=%d m_final=%d" %
+            (rank, k, 1e3 * tl, 1e3 * tr, st["iterations"], st["exit_check"], st["m_final"]))
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    tim = eng.collect_timing()
-    eng.set_timing(False)
+    m0 = eng.graph_info()[2]
+    tim = eng.collect_timing() if not model else None
+    if not model:
+        eng.set_timing(False)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, load_s, loop_s], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed, load_s, loop_s = (float(x) for x in tt.tolist())
     value = pe_total / elapsed
 
-    # roofline of the dominant kernel (light local-moving decide), measured with HIP events
-    # on the engine's stream over the timed region; bytes = the algorithmic model
-    launches = max(1, tim["decide_launches"])
-    avg_s = tim["decide_ms"] / launches / 1e3
-    bytes_per_launch = tim["decide_bytes"] / launches
-    achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
-            "kernel": "k_decide_light<%s>" % ("true" if algo == 0 else "false"), "launches": tim["decide_launches"],
-            "avg_us": avg_s * 1e6, "algorithmic_bytes_per_launch": bytes_per_launch}
-    phases = {k: tim[k] / args.steps for k in ("cd_ms", "consensus_ms", "closure_ms", "rebuild_ms", "decide_ms")}
+    roof, phases = None, None
+    if tim is not None:
+        # roofline of the dominant kernel (light local-moving decide), measured with HIP
+        # events on the engine's stream over the timed region; bytes = the algorithmic model
+        launches = max(1, tim["decide_launches"])
+        avg_s = tim["decide_ms"] / launches / 1e3
+        bytes_per_launch = tim["decide_bytes"] / launches
+        achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
+                "kernel": "k_decide_light<%s>" % ("true" if algo != 1 else "false"),
+                "launches": tim["decide_launches"], "avg_us": avg_s * 1e6,
+                "algorithmic_bytes_per_launch": bytes_per_launch}
+        phases = {k: tim[k] / args.steps for k in ("cd_ms", "consensus_ms", "closure_ms", "rebuild_ms", "decide_ms")}
 
-    result = {}
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not model:
             t = time.perf_counter()
-            cpu = cpu_baseline(n, u, v, cfg)
+            cpu = cpu_baseline(n, u, v, cfg, args.seed)
             log("[rank 0] cpu baseline %.3g %s in %.1fs" % (cpu["value"], cpu["unit"], time.perf_counter() - t))
         result = {
             "metric": METRIC, "value": value, "unit": "partition·edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic (native LFR/SBM generator, seed %d; graph resident in HBM before timing)" % args.seed,
+            "data": "synthetic (native LFR/SBM generator, seed %d)" % args.seed,
             "config": {"workload": cfg["desc"], "n": n, "m": m0, "algorithm": cfg["algo"], "n_p": cfg["n_p"],
                        "tau": cfg["tau"], "delta": cfg["delta"], "parallelism": "replica-sharded x%d" % world,
-                       "iterations": iters, "host_labels": "preallocated int32 [n_p][n], downloaded every step"},
+                       "iterations": iters, "m_final": m_finals,
+                       "step": ("loop only, graph resident before timing (--resident)" if args.resident else
+                                "fast_consensus() end to end: host edge arrays -> PCIe upload + device ingest "
+                                "-> every iteration + final pass -> n_p labelings in a preallocated host array")},
+            "consensus_wall_ms": 1e3 * elapsed / args.steps,
+            "load_ms_per_step": 1e3 * load_s / args.steps,
+            "loop_ms_per_step": 1e3 * loop_s / args.steps,
+            "dist": {"backend": backend if world > 1 else None, "world_size": world},
             "roofline": roof,
             "cpu_baseline": cpu,
             "phase_ms_per_step_rank0": phases,
-            "consensus_wall_ms": 1e3 * elapsed / args.steps,
         }
-    if rank == 0:
+        if model:
+            result["engine"] = "cpu-model (TEST HOOK: oracle-backed model of the engine, not the product)"
+            result["value"] = None
         print(json.dumps(result))
 
 

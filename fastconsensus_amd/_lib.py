@@ -22,7 +22,7 @@ ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 SYMBOLS = [
     "fc_last_error", "fc_version", "fc_create", "fc_destroy", "fc_set_stream", "fc_synchronize", "fc_set_timing",
     "fc_collect_timing", "fc_set_params", "fc_set_option", "fc_load_graph", "fc_graph_info", "fc_get_node_map", "fc_reset_graph", "fc_get_graph", "fc_get_nextgraph", "fc_run",
-    "fc_cd", "fc_set_labels", "fc_get_labels", "fc_consensus_partial", "fc_consensus_apply",
+    "fc_cd", "fc_set_labels", "fc_replica_info", "fc_get_labels", "fc_consensus_partial", "fc_consensus_apply",
     "fc_closure_sample", "fc_closure_set_pairs", "fc_closure_partial", "fc_closure_apply",
     "fc_generate_lfr", "fc_generate_sbm", "fc_read_edgelist",
 ]
@@ -85,7 +85,8 @@ def load():
     L.fc_run.argtypes = [vp, c_int, c_int, dbl, dbl, vp, P(Stats)]
     L.fc_cd.argtypes = [vp, c_int, c_int, c_int, c_int, c_int]
     L.fc_set_labels.argtypes = [vp, c_int, _i32p]
-    L.fc_get_labels.argtypes = [vp, vp, c_int]   # host array or device buffer
+    L.fc_replica_info.argtypes = [vp, P(c_int), P(c_int), P(c_int)]
+    L.fc_get_labels.argtypes = [vp, vp, i64, c_int]   # host array or device buffer, capacity
     L.fc_consensus_partial.argtypes = [vp, c_int, vp]
     L.fc_consensus_apply.argtypes = [vp, c_int, c_int, dbl, dbl, vp, P(c_int), P(i64), P(i64)]
     L.fc_closure_sample.argtypes = [vp, i64, c_int, P(i64)]

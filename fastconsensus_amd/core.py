@@ -166,24 +166,50 @@ class Engine:
         check(self._L.fc_cd(self._ctx, int(algo), int(rbegin), int(rcount), int(n_p_total), int(iteration)))
 
     def set_labels(self, labels):
+        """Install host labelings [count][n] (node order).  Any integer community ids are
+        accepted: a row with ids outside [0, n) (1-based memberships, sparse or negative ids)
+        is compacted first -- ids only matter through equality (fc_set_labels requires
+        [0, n))."""
+        labels = np.asarray(labels)
+        if labels.ndim != 2 or labels.shape[1] != self.n:
+            raise ValueError("labelings must have shape (count, %d)" % self.n)
+        if labels.size and (labels.min() < 0 or labels.max() >= self.n):
+            labels = np.stack([np.unique(row, return_inverse=True)[1].reshape(-1) for row in labels])
         labels = np.ascontiguousarray(labels, dtype=np.int32)
         check(self._L.fc_set_labels(self._ctx, labels.shape[0], labels))
 
+    def replica_info(self):
+        """(local replica count, first global replica index, n_p of the run)."""
+        n, b, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self._L.fc_replica_info(self._ctx, ctypes.byref(n), ctypes.byref(b), ctypes.byref(t)))
+        return n.value, b.value, t.value
+
+    def _check_count(self, count):
+        n_r = self.replica_info()[0]
+        if count != n_r:
+            raise ValueError("the engine holds %d local labelings, %d requested" % (n_r, count))
+
     def get_labels(self, count, renumber=False, dev_out=None):
-        """[count][n] labelings in node order: a new numpy array, or written into the device
-        tensor `dev_out` (int32, >= count*n elements) when given."""
+        """[count][n] labelings in node order (count must equal the local replica count): a
+        new numpy array, or written into the device tensor `dev_out` (int32, >= count*n
+        elements) when given."""
+        self._check_count(count)
         if dev_out is not None:
-            assert dev_out.dtype == torch_int32() and dev_out.numel() >= count * self.n
-            check(self._L.fc_get_labels(self._ctx, self._dev(dev_out), 1 if renumber else 0))
+            if dev_out.dtype != torch_int32() or dev_out.numel() < count * self.n:
+                raise ValueError("dev_out must be an int32 tensor of >= %d elements" % (count * self.n))
+            check(self._L.fc_get_labels(self._ctx, self._dev(dev_out), int(dev_out.numel()), 1 if renumber else 0))
             return dev_out
         out = np.empty((count, self.n), np.int32)
-        check(self._L.fc_get_labels(self._ctx, ptr(out), 1 if renumber else 0))
+        check(self._L.fc_get_labels(self._ctx, ptr(out), out.size, 1 if renumber else 0))
         return out
 
     def get_labels_into(self, out, renumber=False):
         """Like get_labels(out.shape[0], ...) into a caller-owned C-contiguous int32 host array."""
-        assert out.dtype == np.int32 and out.ndim == 2 and out.shape[1] == self.n and out.flags.c_contiguous
-        check(self._L.fc_get_labels(self._ctx, ptr(out), 1 if renumber else 0))
+        if not (isinstance(out, np.ndarray) and out.dtype == np.int32 and out.ndim == 2 and out.shape[1] == self.n
+                and out.flags.c_contiguous):
+            raise ValueError("out must be a C-contiguous int32 array of shape (count, %d)" % self.n)
+        self._check_count(out.shape[0])
+        check(self._L.fc_get_labels(self._ctx, ptr(out), out.size, 1 if renumber else 0))
         return out
 
     def consensus_partial(self, algo, dev_out):

@@ -259,16 +259,36 @@ int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels) {
     FC_API_BEGIN
     FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
     FC_REQUIRE(count >= 1 && labels, FC_EINVAL, "bad labelings");
+    // community ids index per-replica [N] tables (first-node minima, totals): out-of-range
+    // ids would be out-of-bounds device accesses, so they are refused here
+    const int64_t total = (int64_t)count * c.N;
+    const uint32_t lim = (uint32_t)c.N;
+    for (int64_t i = 0; i < total; ++i)
+        FC_REQUIRE((uint32_t)labels[i] < lim, FC_EINVAL,
+                   "label " + std::to_string(labels[i]) + " at index " + std::to_string(i) + " outside [0, n)");
     labels_from_host(c, count, labels);
     c.n_r = count; c.rbase = 0; c.n_p_total = count;
     c.labT_valid = false;
     FC_API_END
 }
 
-int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber) {
+int fc_replica_info(fc_ctx* ctx, int* count, int* rbegin, int* n_p_total) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    if (count) *count = c.n_r;
+    if (rbegin) *rbegin = c.rbase;
+    if (n_p_total) *n_p_total = c.n_p_total;
+    FC_API_END
+}
+
+int fc_get_labels(fc_ctx* ctx, int32_t* labels, int64_t capacity, int renumber) {
     FC_CTX(ctx)
     FC_API_BEGIN
     FC_REQUIRE(c.n_r > 0, FC_ESTATE, "no labelings");
+    FC_REQUIRE(labels, FC_EINVAL, "null output buffer");
+    FC_REQUIRE(capacity >= (int64_t)c.n_r * c.N, FC_EINVAL,
+               "output buffer holds " + std::to_string(capacity) + " labels; " + std::to_string(c.n_r) +
+                   " replicas x " + std::to_string(c.N) + " nodes needed");
     labels_to_host(c, labels, renumber != 0);
     FC_API_END
 }

@@ -1152,7 +1152,7 @@ static int64_t count_heavy(Ctx& c, int64_t thr) {
 
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
-    FC_REQUIRE(c.g.rowptr.p, FC_ESTATE, "no graph loaded");
+    FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
     const int sl0 = timer_begin(c);
     const bool louv = is_louvain(algo);
     const int64_t N = c.N;
@@ -1296,8 +1296,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     if (c.trace)
         fprintf(stderr, "[fc] cd it=%d done: %d multi-kernel sweeps, %.2f sweeps per replica\n", iteration, sweep,
                 (double)rep_sweeps / rcount);
-    c.acc.cd_sweeps += (int64_t)rep_sweeps;
-    c.prof.cd_sweeps += (int64_t)rep_sweeps;
+    if (!c.order_pass) {
+        c.acc.cd_sweeps += (int64_t)rep_sweeps;
+        c.prof.cd_sweeps += (int64_t)rep_sweeps;
+    }
     c.hpin[0] = c.hpin[1] = c.hpin[2] = 0;
     int64_t tv = 0, te = 0;
     for (int r = 0; r < rcount; ++r) {
@@ -1312,6 +1314,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int64_t db = louv ? c.hpin[0] * (40 + tsz) + c.hpin[1] * 8 + c.hpin[2] * tsz
                             : c.hpin[0] * 32 + c.hpin[1] * 4;
     for (fc_stats* s : {&c.acc, &c.prof}) {
+        if (c.order_pass) break;                 // load-time ordering run (store_order)
         s->cd_vertex_visits += c.hpin[0] + tv;   // light kernel + tail kernel
         s->cd_edge_visits += c.hpin[1] + te;
         s->decide_bytes += db;                   // light kernel only (its time is decide_ms)
@@ -1471,10 +1474,12 @@ void store_order(Ctx& c) {
     const int64_t N = c.N;
     // int64 totals: the pass runs the k_decide_light<true, long> instance, so kernel
     // statistics of the int32 instance cover the consensus runs alone
+    // and it is load-time work: neither its kernels nor its counters enter the run statistics
     struct Pass {
         Ctx& c;
-        explicit Pass(Ctx& x) : c(x) { c.order_pass = true; }
-        ~Pass() { c.order_pass = false; }
+        bool timer_on;
+        explicit Pass(Ctx& x) : c(x), timer_on(x.timer.on) { c.order_pass = true; c.timer.on = false; }
+        ~Pass() { c.order_pass = false; c.timer.on = timer_on; }
     } pass(c);
     cd_run(c, FC_ALGO_LOUVAIN, 0, 1, 1, 0x3fffffff);
     uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, N);

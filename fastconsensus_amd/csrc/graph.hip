@@ -8,6 +8,9 @@
 #include "fc_ctx.h"
 #include "fc_device.h"
 
+#include <chrono>
+#include <cstdio>
+
 namespace fc {
 
 static constexpr int TB = 256;
@@ -86,19 +89,37 @@ int64_t read_i64(Ctx& c, const int64_t* dev) {
 }
 
 // ------------------------------------------------------------------ ingest kernels
-__global__ void k_make_keys(int64_t m, const int32_t* u, const int32_t* v, int bits, uint64_t* key,
-                            int64_t* idx) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    int32_t a = u[i], b = v[i];
-    uint64_t sent = (bits >= 32) ? ~0ull : ((1ull << (2 * bits)) - 1ull);
-    uint64_t k = sent;
-    if (a != b) {
-        uint64_t lo = (uint64_t)(a < b ? a : b), hi = (uint64_t)(a < b ? b : a);
-        k = (lo << bits) | hi;
+// Internal numbering sigma[node] (a seeded Feistel bijection, or the identity), its inverse,
+// and the identity label storage (store_order() replaces it).
+__global__ void k_sigma(int64_t n, Perm P, int relabel, int32_t* sigma, int32_t* npos, int32_t* spos) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = relabel ? (int32_t)perm_apply(P, (uint32_t)i) : (int32_t)i;
+    sigma[i] = s;
+    npos[s] = (int32_t)i;
+    spos[i] = (int32_t)i;
+}
+// Input edge i (node ids, file order) -> canonical key (min, max) in internal ids, or the
+// sentinel for a self loop; endpoints outside [0, n) are counted (the load then fails).
+__global__ void k_make_keys(int64_t m, int64_t n, const int32_t* u, const int32_t* v, const int32_t* sigma, int bits,
+                            uint64_t* key, int64_t* idx, unsigned long long* bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool oob = false;
+    if (i < m) {
+        const int32_t a0 = u[i], b0 = v[i];
+        const uint64_t sent = (bits >= 32) ? ~0ull : ((1ull << (2 * bits)) - 1ull);
+        uint64_t k = sent;
+        oob = (uint32_t)a0 >= (uint64_t)n || (uint32_t)b0 >= (uint64_t)n;
+        if (!oob && a0 != b0) {
+            const int32_t a = sigma[a0], b = sigma[b0];
+            const uint64_t lo = (uint64_t)(a < b ? a : b), hi = (uint64_t)(a < b ? b : a);
+            k = (lo << bits) | hi;
+        }
+        key[i] = k;
+        idx[i] = i;
     }
-    key[i] = k;
-    idx[i] = i;
+    const unsigned long long bl = __ballot(oob);
+    if ((threadIdx.x & 63) == 0 && bl) atomicAdd(shard(bad, 1, 0), (unsigned long long)__popcll(bl));
 }
 
 __global__ void k_unique_flags(int64_t m, const uint64_t* key, int bits, int64_t* flag) {
@@ -122,54 +143,52 @@ __global__ void k_scatter_unique(int64_t m, const uint64_t* key, const int64_t* 
     eage[p] = idx[i];   // first occurrence (stable sort) = networkx adjacency age
 }
 
+// Host edge arrays -> device graph.  Everything after the PCIe upload of u and v runs on the
+// device: validation, internal numbering, canonical keys, dedupe (stable radix sort keeps
+// the first occurrence = networkx adjacency age), CSR, label storage order.
 void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v) {
     FC_REQUIRE(n >= 1 && n < (int64_t(1) << 31), FC_EINVAL, "node count out of range");
     FC_REQUIRE(m >= 0 && m < (int64_t(1) << 31), FC_EINVAL, "edge count out of range");
-    for (int64_t i = 0; i < m; ++i)
-        FC_REQUIRE(u[i] >= 0 && u[i] < n && v[i] >= 0 && v[i] < n, FC_EINVAL, "edge endpoint out of range");
-    c.N = n;
-    // internal numbering (see Ctx::sigma); input edges are mapped on the host
-    c.h_sigma.resize(n);
-    for (int64_t i = 0; i < n; ++i) c.h_sigma[i] = (int32_t)i;
-    if (c.relabel) {
-        uint64_t st = mix64(c.seed ^ 0x51A7E5EDull);
-        for (int64_t i = n - 1; i > 0; --i) {
-            st = mix64(st + 0x9E3779B97F4A7C15ull);
-            const int64_t j = (int64_t)(((unsigned __int128)st * (uint64_t)(i + 1)) >> 64);
-            std::swap(c.h_sigma[i], c.h_sigma[j]);
-        }
-    }
-    std::vector<int32_t> h_npos(n);
-    for (int64_t i = 0; i < n; ++i) h_npos[c.h_sigma[i]] = (int32_t)i;
-    ensure<int32_t>(c.sigma, n); ensure<int32_t>(c.npos, n);
-    {   // label storage slots: identity until store_order() below
-        std::vector<int32_t> id(n);
-        for (int64_t i = 0; i < n; ++i) id[i] = (int32_t)i;
-        ensure<int32_t>(c.spos, n);
-        FC_HIP(hipMemcpyAsync(c.spos.p, id.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {   // FC_TRACE: per-phase wall time of the load
+        if (!c.trace) return;
         sync(c);
-    }
-    FC_HIP(hipMemcpyAsync(c.sigma.p, c.h_sigma.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
-    FC_HIP(hipMemcpyAsync(c.npos.p, h_npos.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
-    std::vector<int32_t> mu_(m), mv_(m);
-    for (int64_t i = 0; i < m; ++i) { mu_[i] = c.h_sigma[u[i]]; mv_[i] = c.h_sigma[v[i]]; }
-    u = mu_.data();
-    v = mv_.data();
-    int bits = 1;
-    while ((int64_t(1) << bits) < n) ++bits;
-    c.key_bits = bits;
-    int64_t mm = m > 0 ? m : 1;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[fc] load %-14s %8.2f ms\n", what,
+                1e-6 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t - t_last).count());
+        t_last = t;
+    };
+    c.N = 0;   // no graph until this load completes
+    const int64_t mm = m > 0 ? m : 1;
     int32_t* du = ensure<int32_t>(c.cu, mm);
     int32_t* dv = ensure<int32_t>(c.cv, mm);
-    FC_HIP(hipMemcpyAsync(du, u, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
-    FC_HIP(hipMemcpyAsync(dv, v, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+    if (m > 0) {
+        FC_HIP(hipMemcpyAsync(du, u, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+        FC_HIP(hipMemcpyAsync(dv, v, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+    }
+    int32_t* sigma = ensure<int32_t>(c.sigma, n);
+    int32_t* npos = ensure<int32_t>(c.npos, n);
+    int32_t* spos = ensure<int32_t>(c.spos, n);
+    k_sigma<<<nblk(n), TB, 0, c.stream>>>(n, make_perm((uint32_t)n, (uint32_t)mix64(c.seed ^ 0x51A7E5EDull)),
+                                          c.relabel ? 1 : 0, sigma, npos, spos);
+    int bits = 1;
+    while ((int64_t(1) << bits) < n) ++bits;
     uint64_t* k1 = ensure<uint64_t>(c.mkey, mm);
     uint64_t* k2 = ensure<uint64_t>(c.mkey2, mm);
     int64_t* i1 = ensure<int64_t>(c.midx, mm);
     int64_t* i2 = ensure<int64_t>(c.midx2, mm);
     int64_t* fl = ensure<int64_t>(c.ckey, mm + 1);
     int64_t* ps = ensure<int64_t>(c.ckey2, mm + 1);
-    k_make_keys<<<nblk(m), TB, 0, c.stream>>>(m, du, dv, bits, k1, i1);
+    unsigned long long* bad = shards_begin(c, 1);
+    if (m > 0) k_make_keys<<<nblk(m), TB, 0, c.stream>>>(m, n, du, dv, sigma, bits, k1, i1, bad);
+    int64_t nbad = 0;
+    shards_fold(c, 1, 0u, &nbad);
+    FC_REQUIRE(nbad == 0, FC_EINVAL, std::to_string(nbad) + " edge endpoints out of range [0, n)");
+    mark("upload+keys");
+    c.N = n;
+    c.key_bits = bits;
+    c.h_sigma.resize(n);
+    FC_HIP(hipMemcpyAsync(c.h_sigma.data(), sigma, 4 * n, hipMemcpyDeviceToHost, c.stream));
     sort_pairs(c, k1, k2, i1, i2, m, 2 * bits);
     k_unique_flags<<<nblk(m), TB, 0, c.stream>>>(m, k2, bits, fl);
     exclusive_scan(c, fl, ps, m);
@@ -189,16 +208,20 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
     k_scatter_unique<<<nblk(m), TB, 0, c.stream>>>(m, k2, i2, fl, ps, bits, g.eu.as<int32_t>(), g.ev.as<int32_t>(),
                                                     g.ew.as<int32_t>(), g.eage.as<int64_t>());
     c.m_original = mu;   // L = G.number_of_edges() (fast_consensus.py:132, :144)
+    mark("sort+dedupe");
     graph_build_csr(c, g);
     slot_maps(c);        // identity storage (the ordering pass below runs on it)
+    mark("csr");
     if (c.store_order && g.M2 > 0) {
         store_order(c);
         graph_slots(c, g);
     }
     slot_maps(c);
+    mark("store_order");
     graph_copy(c, c.g0, g);
     c.labT_valid = false;
-    sync(c);   // the mapped host edge arrays die here
+    sync(c);
+    mark("copy");
 }
 
 // ------------------------------------------------------------------ node-space export

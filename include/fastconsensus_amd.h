@@ -135,11 +135,18 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
  * Randomness depends on (seed, global replica index, iteration), not on the sharding. */
 int fc_cd(fc_ctx* ctx, int algo, int replica_begin, int replica_count, int n_p_total,
           int iteration);
-/* Replay: install host labelings [count][n] as the local replicas (begin = 0). */
+/* Replay: install host labelings [count][n] as the local replicas (begin = 0).  Every label
+ * must lie in [0, n) (community ids are vertex-sized indices on the device); FC_EINVAL
+ * otherwise -- a host with arbitrary ids (1-based, sparse, negative) compacts them first
+ * (fastconsensus_amd.Engine.set_labels does). */
 int fc_set_labels(fc_ctx* ctx, int count, const int32_t* labels);
+/* The local replica range the next fc_get_labels exports: count (n_r), first global index
+ * and the run's n_p.  count = 0 before any fc_cd / fc_set_labels. */
+int fc_replica_info(fc_ctx* ctx, int* count, int* replica_begin, int* n_p_total);
 /* Download local labelings [count][n] (in node order) into host memory or a device buffer of
- * the context's GPU; renumber != 0 -> ids 0..k-1 by first node. */
-int fc_get_labels(fc_ctx* ctx, int32_t* labels, int renumber);
+ * the context's GPU; renumber != 0 -> ids 0..k-1 by first node.  capacity: int32 elements
+ * the caller's buffer holds; FC_EINVAL if it is below count * n (nothing is written). */
+int fc_get_labels(fc_ctx* ctx, int32_t* labels, int64_t capacity, int renumber);
 /* Per-edge partial over the local replicas into caller device buffer dev_out (int32[m]):
  * louvain -> largest global replica index whose labels split the edge, or -1
  * (reduce with MAX); lpm and louvain_nc -> number of local replicas co-clustering it

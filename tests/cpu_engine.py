@@ -109,6 +109,10 @@ class OracleEngine:
         node_order = self.lab[:, self.sigma]          # [r][t] = label of node t
         return orc.renumber(node_order) if renumber else node_order.copy()
 
+    def get_labels_into(self, out, renumber=False):
+        out[...] = self.get_labels(out.shape[0], renumber)
+        return out
+
     def get_graph(self):
         """Node space, canonical and sorted (fc_get_graph)."""
         a, b = self.npos[self.g.u], self.npos[self.g.v]

@@ -1,0 +1,337 @@
+"""Community-detection parity on the device, at the BASELINE configs (C2, C3, C5).
+
+python-louvain 0.15 and python-igraph 0.9.7 (requirements.txt:4-5) are absent, so the CD
+arithmetic is "parity unpinned" (DESIGN.md): the device's replica-batched Louvain level 0 and
+LPA are held STATISTICALLY to
+  * the oracle's sequential restatements of the published algorithms (orc_louvain_level0,
+    orc_lpa: python-louvain __one_level / igraph community_label_propagation), and
+  * the labelings the reference run itself recorded (tests/golden/*_np20.npz `cd_labels`,
+    the reference's loop with networkx stand-ins for the two libraries, make_golden.py),
+and the whole consensus to the reference's own final partitions (`final_labels`,
+fast_consensus.py:383-392).  The tolerances are written in each test (and in DESIGN.md);
+every measured value is printed (pytest -s) so the margins are on record.
+Deterministic parts at full size (consensus update, closure growth) stay bit-exact.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests import golden_io
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def fcmod():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import fastconsensus_amd as fc
+    return fc
+
+
+def nmi(a, b):
+    from sklearn.metrics import normalized_mutual_info_score
+    return normalized_mutual_info_score(a, b)
+
+
+def summary(g, labels, planted, weighted=True):
+    """mean modularity, mean NMI to the planted communities, mean community count."""
+    q = float(np.mean([orc.modularity(g, l, weighted=weighted) for l in labels]))
+    s = float(np.mean([nmi(planted, l) for l in labels]))
+    k = float(np.mean([len(np.unique(l)) for l in labels]))
+    return {"q": q, "nmi": s, "k": k}
+
+
+def lfr1k():
+    case = golden_io.load("lfr1k_louvain_np20")
+    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu04_planted.npy")[case.z["nodes"]]
+    return case, orc.EdgeGraph.from_lines(case.N, case.edges_file), planted
+
+
+def device_cd(fcmod, algo, N, e, count, seed):
+    with fcmod.Engine(seed=seed) as eng:
+        eng.load_graph(N, e[:, 0], e[:, 1])
+        eng.cd(algo, 0, count, count, 0)
+        return eng.get_labels(count)
+
+
+# ------------------------------------------------------------------------------ C2 (LFR-1k)
+# Tolerances (C2): mean modularity within 0.02 of the restatement and not below it by more
+# than 0.01; mean NMI to planted >= restatement - 0.03; mean community count within 25 %.
+# Against the reference run's own recorded labelings (networkx stand-ins): modularity
+# >= reference - 0.02, NMI >= reference - 0.03.
+def test_c2_louvain_vs_restatement_and_reference_run(fcmod):
+    case, g, planted = lfr1k()
+    e = case.edges_file
+    gpu = summary(g, device_cd(fcmod, 0, case.N, e, 32, seed=11), planted)
+    ref_lab, _ = orc.cd_batch(0, 32, g, seed=5)
+    ref = summary(g, ref_lab, planted)
+    run = summary(g, case.cd_batches[0], planted)        # the reference run's first CD batch (:148)
+    print("C2 louvain gpu", gpu, "restatement", ref, "reference-run", run)
+    assert gpu["q"] >= ref["q"] - 0.01 and abs(gpu["q"] - ref["q"]) <= 0.02
+    assert gpu["nmi"] >= ref["nmi"] - 0.03
+    assert abs(gpu["k"] - ref["k"]) <= 0.25 * ref["k"]
+    assert gpu["q"] >= run["q"] - 0.02 and gpu["nmi"] >= run["nmi"] - 0.03
+
+
+def test_c2_lpa_vs_restatement_and_reference_run(fcmod):
+    """LPA is called without weights (fast_consensus.py:270): unweighted modularity."""
+    case = golden_io.load("lfr1k_lpm_np20")
+    _, g, planted = lfr1k()
+    e = case.edges_file
+    gpu = summary(g, device_cd(fcmod, 1, case.N, e, 32, seed=12), planted, weighted=False)
+    ref_lab, _ = orc.cd_batch(1, 32, g, seed=6)
+    ref = summary(g, ref_lab, planted, weighted=False)
+    run = summary(g, case.cd_batches[0], planted, weighted=False)   # reference run's LPA batch (:270)
+    print("C2 lpa gpu", gpu, "restatement", ref, "reference-run", run)
+    assert abs(gpu["q"] - ref["q"]) <= 0.02
+    assert gpu["nmi"] >= ref["nmi"] - 0.03
+    assert abs(gpu["k"] - ref["k"]) <= 0.25 * ref["k"]
+    assert gpu["q"] >= run["q"] - 0.02 and gpu["nmi"] >= run["nmi"] - 0.03
+
+
+@pytest.mark.parametrize("name", ["lfr1k_louvain_np20", "lfr1k_lpm_np20"])
+def test_c2_consensus_nmi_vs_reference_final_partitions(fcmod, name):
+    """The whole consensus against the reference's OWN output (its n_p final partitions,
+    fast_consensus.py:383-392): mean NMI to planted >= reference - 0.02 (3 seeds)."""
+    case = golden_io.load(name)
+    _, g, planted = lfr1k()
+    ref = float(np.mean([nmi(planted, l) for l in case.z["final_labels"]]))
+    e = case.edges_file
+    got = []
+    for seed in (1, 2, 3):
+        with fcmod.Engine(seed=seed) as eng:
+            eng.load_graph(case.N, e[:, 0], e[:, 1])
+            labels, st = eng.run(case.algo, case.n_p, case.tau, case.delta)
+        assert st["iterations"] >= 1 and not st["hit_iter_cap"]
+        got.append(float(np.mean([nmi(planted, l) for l in labels])))
+    k_ref = float(np.mean([len(np.unique(l)) for l in case.z["final_labels"]]))
+    print(name, "device consensus NMI", got, "reference final NMI %.4f" % ref, "reference k %.1f" % k_ref)
+    assert np.mean(got) >= ref - 0.02
+
+
+# ------------------------------------------------------------------------------ C3 (LFR-100k)
+@pytest.fixture(scope="module")
+def lfr100k():
+    from fastconsensus_amd import synth
+    u, v, planted = synth.lfr(100_000, 0.5, seed=42)
+    return 100_000, np.stack([u, v], 1), planted
+
+
+# Tolerances (C3): mean modularity within 0.01 of the restatement (louvain: not below it
+# by more than 0.005), mean NMI to planted >= restatement - 0.02, community count within 25 %.
+@pytest.mark.parametrize("algo", [0, 1])
+def test_c3_cd_vs_restatement(fcmod, lfr100k, algo):
+    n, e, planted = lfr100k
+    g = orc.EdgeGraph.from_lines(n, e)
+    gpu = summary(g, device_cd(fcmod, algo, n, e, 16, seed=21), planted, weighted=algo == 0)
+    ref_lab, _ = orc.cd_batch(algo, 8, g, seed=7, nthreads=16)
+    ref = summary(g, ref_lab, planted, weighted=algo == 0)
+    print("C3", ["louvain", "lpa"][algo], "gpu", gpu, "restatement", ref)
+    assert abs(gpu["q"] - ref["q"]) <= 0.01
+    if algo == 0:
+        assert gpu["q"] >= ref["q"] - 0.005
+    assert gpu["nmi"] >= ref["nmi"] - 0.02
+    assert abs(gpu["k"] - ref["k"]) <= 0.25 * ref["k"]
+
+
+@pytest.mark.parametrize("algo,tau", [(0, 0.2), (1, 0.8)])
+def test_c3_consensus_update_bit_exact_and_run(fcmod, lfr100k, algo, tau):
+    """BASELINE configs[2]: n_p=64 device labelings -> consensus rule / count, threshold and
+    check bit-exact against the oracle's literal loop; then a whole run at C3."""
+    n, e, planted = lfr100k
+    with fcmod.Engine(seed=3) as eng:
+        eng.load_graph(n, e[:, 0], e[:, 1])
+        eng.cd(algo, 0, 64, 64, 0)
+        lab = eng.get_labels(64)
+        part = torch.zeros(eng.m, dtype=torch.int32, device="cuda")
+        eng.consensus_partial(algo, part)
+        conv, kept, unc = eng.consensus_apply(algo, 64, tau, 0.02, part)
+        g = orc.EdgeGraph.from_lines(n, e)
+        w_ref = orc.consensus(algo, g, lab, 64)
+        keep = orc.threshold(w_ref, tau, 64)
+        ku, kv, kw, _ = eng.get_nextgraph()
+        assert kept == int(keep.sum())
+        np.testing.assert_array_equal(kw, w_ref[keep])
+        np.testing.assert_array_equal(ku, g.u[keep])
+        np.testing.assert_array_equal(kv, g.v[keep])
+        oc, ocnt = orc.check(w_ref[keep], 64, 0.02)
+        assert unc == ocnt and (algo == 1 or conv == oc)
+        labels, st = eng.run(algo, 64, tau, 0.02)
+    assert labels.shape == (64, n) and st["exit_check"] in (1, 2) and not st["hit_iter_cap"]
+    assert st["m_final"] > 0 and st["partition_edges"] >= 64 * st["m_final"]
+    for row in labels[:4]:
+        assert row[0] == 0 and row.max() + 1 == len(np.unique(row))
+    s = float(np.mean([nmi(planted, l) for l in labels[:8]]))
+    print("C3 run", ["louvain", "lpm"][algo], st, "NMI %.4f" % s)
+    if algo == 0:
+        assert s > 0.8
+
+
+# ------------------------------------------------------------------------------ C5 (SBM-4M lpm)
+@pytest.mark.timeout(900)
+def test_c5_lpm_count_update_and_closure_growth_full_size(fcmod):
+    """BASELINE configs[4] on one GPU: n=4M, ~40M edges, lpm n_p=128.  The co-membership
+    count of 128 device LPA labelings is bit-exact against the oracle's literal count
+    (fast_consensus.py:273-280) at full size; closure then grows the graph by exactly the new
+    candidates, every one with weight 0 (fast_consensus.py:300-304, `a in communities[i]`
+    is always False), and the check runs after closure (:309)."""
+    from fastconsensus_amd import synth
+    n = 4_000_000
+    u, v = synth.sbm(n, seed=42)
+    e = np.stack([u, v], 1)
+    with fcmod.Engine(seed=5) as eng:
+        eng.load_graph(n, u, v)
+        m0 = eng.m
+        assert m0 > 35_000_000
+        eng.cd(1, 0, 128, 128, 0)
+        lab = eng.get_labels(128)
+        part = torch.zeros(m0, dtype=torch.int32, device="cuda")
+        eng.consensus_partial(1, part)
+        conv, kept, unc = eng.consensus_apply(1, 128, 0.8, 0.02, part)
+        g = orc.EdgeGraph.from_lines(n, e)
+        w_ref = orc.consensus(1, g, lab, 128)
+        del lab
+        keep = orc.threshold(w_ref, 0.8, 128)
+        ku, kv, kw, kage = eng.get_nextgraph()
+        assert kept == int(keep.sum())
+        np.testing.assert_array_equal(kw, w_ref[keep])
+        np.testing.assert_array_equal(ku, g.u[keep])
+        assert unc == orc.check(w_ref[keep], 128, 0.02)[1]
+        nc = eng.closure_sample(m0, 0)
+        assert 0 < nc <= m0
+        conv2, m1 = eng.closure_apply(1, 128, 0.02, None, 0)
+        assert m1 == kept + nc                    # lpm: no isolate repair (:260-310)
+        gu, gv, gw, gage = eng.get_graph()
+        new = (gage >> 40) == 1                   # closure edges of iteration 0
+        assert int(new.sum()) == nc and (gw[new] == 0).all()
+        kept_set_w = gw[~new]
+        np.testing.assert_array_equal(np.sort(kept_set_w), np.sort(kw))
+        unc2 = int(((gw != 0) & (gw != 128)).sum())
+        assert conv2 == (not unc2 > 0.02 * m1)
+        labels, st = eng.run(1, 128, 0.8, 0.02)
+    print("C5 one iteration: m0 %d kept %d closure %d m1 %d; run %s" % (m0, kept, nc, m1, st))
+    assert st["exit_check"] == 2 and not st["hit_iter_cap"] and st["m_final"] > 0
+    assert labels.shape == (128, n)
+
+
+# ------------------------------------------------------------------------------ closure
+@pytest.mark.parametrize("name", ["lfr1k_louvain_np20", "lfr1k_lpm_np20", "karate_louvain_np50"])
+def test_device_closure_sampler_is_the_measured_one(fcmod, name):
+    """fc_closure_sample on the reference's kept graph draws exactly the candidates of the
+    restated sampler (orc_closure_sample) -- the one whose deviation from the reference's
+    sequential sampler tests/test_closure_deviation.py measures."""
+    case = golden_io.load(name)
+    graphs, traces, _ = orc.replay(case.algo, case.N, case.edges_file, case.n_p, case.tau, case.delta,
+                                   case.cd_batches, case.pair_batches)
+    seed = 77
+    with fcmod.Engine(seed=seed) as eng:
+        eng.set_option("relabel", 0)              # restated sampler runs in node ids
+        e = case.edges_file
+        eng.load_graph(case.N, e[:, 0], e[:, 1])
+        eng.set_labels(case.cd_batches[0])
+        part = torch.zeros(eng.m, dtype=torch.int32, device="cuda")
+        eng.consensus_partial(case.algo, part)
+        eng.consensus_apply(case.algo, case.n_p, case.tau, case.delta, part)
+        kept = traces[0]["kept"]
+        L = graphs[0].m
+        nc = eng.closure_sample(L, 0)
+        pairs = orc.closure_sample_pairs(kept, L, seed, 0)
+        cu, cv, _, _ = orc.closure_from_pairs(case.algo, kept, pairs, case.cd_batches[0], case.n_p)
+        assert nc == len(cu)
+
+
+# ------------------------------------------------------------------------------ CLI end to end
+@pytest.mark.parametrize("alg,argv", [("louvain", ["--alg", "louvain", "-np", "50", "-t", "0.2", "-d", "0.1"]),
+                                      ("lpm", ["--alg", "lpm", "-np", "20"])])
+def test_cli_end_to_end_on_device(fcmod, tmp_path, alg, argv):
+    """python fast_consensus.py -f karate ... (fast_consensus.py:414-466) through the engine:
+    directory names, one file per partition, every node covered exactly once per partition,
+    memberships "{node+1}\\t{comm+1}" sorted by node (louvain; empty directory for lpm)."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    shutil.copy(os.path.join(golden_io.GOLDEN, "karate_club.txt"), tmp_path / "karate.txt")
+    p = subprocess.run([sys.executable, os.path.join(root, "fast_consensus.py"), "-f", "karate.txt"] + argv,
+                       cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    n_p = int(argv[argv.index("-np") + 1])
+    tau = argv[argv.index("-t") + 1] if "-t" in argv else "0.8"
+    delta = argv[argv.index("-d") + 1] if "-d" in argv else "0.02"
+    suffix = "t%s_d%s_np%d" % (tau, delta, n_p)
+    assert sorted(os.listdir(tmp_path)) == sorted(["karate.txt", "out_partitions_" + suffix,
+                                                   "memberships_" + suffix])
+    nodes = set()
+    for line in open(tmp_path / "karate.txt"):
+        nodes.update(int(x) for x in line.split()[:2])
+    outd = tmp_path / ("out_partitions_" + suffix)
+    assert sorted(os.listdir(outd), key=int) == [str(i) for i in range(1, n_p + 1)]
+    for fn in os.listdir(outd):
+        members = [int(x) for ln in (outd / fn).read_text().splitlines() for x in ln.split()]
+        assert sorted(members) == sorted(nodes)
+    memd = tmp_path / ("memberships_" + suffix)
+    if alg == "louvain":
+        assert sorted(os.listdir(memd), key=int) == [str(i) for i in range(n_p)]
+        for fn in os.listdir(memd):
+            rows = [ln.split("\t") for ln in (memd / fn).read_text().splitlines()]
+            assert [int(r[0]) for r in rows] == sorted(x + 1 for x in nodes)
+            assert all(len(r) == 2 and int(r[1]) >= 1 for r in rows)
+    else:
+        assert os.listdir(memd) == []
+
+
+# ------------------------------------------------------------------------------ label export
+@pytest.mark.parametrize("distinct", [37, 5000, 0])
+def test_renumber_multi_span_exact(fcmod, distinct):
+    """get_labels(renumber=True) over several 2048-slot spans of k_first_min, with few,
+    many (LDS table overflow -> global fallback) and all-distinct labels: exactly the
+    first-appearance renumbering (orc.renumber)."""
+    rng = np.random.default_rng(distinct + 1)
+    N = 5 * 2048 + 123
+    u = rng.integers(0, N, 8 * N).astype(np.int32)
+    v = rng.integers(0, N, 8 * N).astype(np.int32)
+    hi = distinct if distinct else N
+    lab = rng.integers(0, hi, (3, N)).astype(np.int32)
+    if not distinct:
+        lab = np.stack([rng.permutation(N) for _ in range(3)]).astype(np.int32)
+    with fcmod.Engine(seed=4) as eng:
+        eng.load_graph(N, u, v)
+        eng.set_labels(lab)
+        np.testing.assert_array_equal(eng.get_labels(3), lab)
+        np.testing.assert_array_equal(eng.get_labels(3, renumber=True), orc.renumber(lab))
+
+
+def test_set_labels_range_and_capacity_contract(fcmod):
+    """fc_set_labels refuses ids outside [0, n) (they would index device tables); the host
+    compacts 1-based / sparse ids; fc_get_labels refuses a short buffer."""
+    import ctypes
+    from fastconsensus_amd import _lib
+    case = golden_io.load("karate_louvain_np50")
+    e = case.edges_file
+    lab = case.cd_batches[0][:4]
+    with fcmod.Engine(seed=1) as eng:
+        eng.load_graph(case.N, e[:, 0], e[:, 1])
+        L = _lib.load()
+        bad = np.ascontiguousarray(lab + 1, dtype=np.int32)
+        bad[0, 0] = case.N
+        assert L.fc_set_labels(eng._ctx, 4, bad) == -1                       # FC_EINVAL
+        neg = np.ascontiguousarray(lab, dtype=np.int32)
+        neg[1, 3] = -1
+        assert L.fc_set_labels(eng._ctx, 4, neg) == -1
+        eng.set_labels(lab * 7 + 1)                                           # sparse, 1-based: compacted
+        np.testing.assert_array_equal(eng.get_labels(4, renumber=True), orc.renumber(lab))
+        assert eng.replica_info() == (4, 0, 4)
+        short = np.zeros(4 * case.N - 1, np.int32)
+        assert L.fc_get_labels(eng._ctx, short.ctypes.data, short.size, 0) == -1
+        assert (short == 0).all()
+        with pytest.raises(ValueError):
+            eng.get_labels(3)
+        with pytest.raises(ValueError):
+            eng.get_labels_into(np.zeros((5, case.N), np.int32))
+        big = torch.zeros(4 * case.N - 1, dtype=torch.int32, device="cuda")
+        with pytest.raises(ValueError):
+            eng.get_labels(4, dev_out=big)
