@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Reference-semantics consensus distributions: the REFERENCE's own loop with the oracle's CD.
+
+Runs in the development container only (needs /root/reference; the GPU box never runs
+this).  `/root/reference/fast_consensus.py` is executed unmodified; its absent CD libraries
+are stubbed as in make_golden.py, but the stubs run the oracle's sequential restatements of
+the published algorithms instead of networkx stand-ins:
+
+* ``community.generate_dendrogram`` -> orc_louvain_level0 (python-louvain 0.15 level 0,
+  fast_consensus.py:148, :384), one fresh seed per call;
+* ``igraph.Graph.community_label_propagation`` -> orc_lpa (igraph 0.9.7 LPA, unweighted as
+  called at :270, :392) on the vertex-id graph nx_to_igraph (:41-52) builds.
+
+Everything else -- consensus rule, threshold, checks, the SEQUENTIAL closure over the growing
+graph (np.random.choice / random.sample, :175-190, :292-304), isolate repair, loop exits and
+final pass -- is the reference's own code.  For 30 seeds the mean NMI of the n_p final
+partitions to the planted communities is recorded, so a device run is compared with the
+reference's distribution, not with a single sample (the consensus NMI varies from run to run:
+0.80-0.95 on LFR-1k).  Output: tests/golden/refsem_*.json (data only).
+
+Usage:  python tests/golden/make_refsem.py
+"""
+import importlib.util
+import json
+import os
+import random
+import sys
+import types
+
+import networkx as nx
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.dont_write_bytecode = True
+REF = "/root/reference/fast_consensus.py"
+
+from oracle import oracle as orc  # noqa: E402
+
+STATE = {"calls": 0, "seed": 0, "idx": None}
+
+
+def _edgegraph(pairs_w, N):
+    u = np.array([min(a, b) for a, b, _ in pairs_w], np.int64)
+    v = np.array([max(a, b) for a, b, _ in pairs_w], np.int64)
+    w = np.array([w for _, _, w in pairs_w], np.int64)
+    assert np.all(w == np.round(w))
+    return orc.EdgeGraph(N, u, v, w.astype(np.int32), np.arange(len(u))).sorted_by_key()
+
+
+def _gen_dendrogram(graph, part_init=None, weight="weight", resolution=1.0, randomize=None, random_state=None):
+    STATE["calls"] += 1
+    idx = STATE["idx"]
+    g = _edgegraph([(idx[a], idx[b], d.get(weight, 1)) for a, b, d in graph.edges(data=True)], len(idx))
+    lab, _ = orc.cd_batch(0, 1, g, seed=STATE["seed"] * 1000003 + STATE["calls"])
+    return [{x: int(lab[0][idx[x]]) for x in graph.nodes()}]
+
+
+class _Cover:
+    def __init__(self, comms):
+        self._c = comms
+
+    def as_cover(self):
+        return self._c
+
+
+class _Graph:
+    """The part of igraph.Graph that nx_to_igraph (:41-52) and :270 use."""
+
+    def __init__(self):
+        self.names, self.edges, self.es = [], [], {}
+
+    def add_vertices(self, names):
+        self.names = list(names)
+
+    def add_edges(self, edges):
+        self.edges = [(int(a), int(b)) for a, b in edges]
+
+    def __setitem__(self, key, value):
+        pass  # edge weights (:51) are ignored by community_label_propagation() as called
+
+    def community_label_propagation(self, *a, **k):
+        STATE["calls"] += 1
+        g = _edgegraph([(a, b, 1) for a, b in self.edges], len(self.names))
+        lab, _ = orc.cd_batch(1, 1, g, seed=STATE["seed"] * 1000003 + STATE["calls"])
+        comms = {}
+        for vid, c in enumerate(lab[0].tolist()):
+            comms.setdefault(c, []).append(vid)
+        return _Cover(list(comms.values()))
+
+
+def load_reference():
+    community = types.ModuleType("community")
+    community.generate_dendrogram = _gen_dendrogram
+    community.partition_at_level = lambda d, level: dict(d[level])
+    igraph = types.ModuleType("igraph")
+    igraph.Graph = _Graph
+    sys.modules["community"] = community
+    sys.modules["igraph"] = igraph
+    sys.modules["leidenalg"] = types.ModuleType("leidenalg")
+    spec = importlib.util.spec_from_file_location("fc_reference_refsem", REF)
+    fc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fc)
+    return fc
+
+
+def labels_of(part, nodes, idx):
+    if isinstance(part, dict):
+        return np.array([part[x] for x in nodes])
+    lab = np.full(len(nodes), -1)
+    for ci, c in enumerate(part):
+        for x in c:
+            lab[idx[x]] = ci
+    assert (lab >= 0).all()
+    return lab
+
+
+def run(fc, name, edgefile, planted_file, algorithm, n_p, tau, delta, seeds):
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    G = nx.read_edgelist(edgefile, nodetype=int)
+    nodes = list(G.nodes())
+    idx = {x: i for i, x in enumerate(nodes)}
+    if algorithm == "lpm":
+        assert sorted(nodes) == list(range(len(nodes)))      # nx_to_igraph needs labels 0..N-1 (README:62)
+    planted = np.load(planted_file)[np.array(nodes)]
+    STATE["idx"] = idx
+    rec = {"name": name, "algorithm": algorithm, "n_p": n_p, "tau": tau, "delta": delta, "graph": os.path.basename(edgefile),
+           "N": len(nodes), "m": G.number_of_edges(), "seeds": [], "nmi": [], "k": [], "cd_calls": [],
+           "cd": "oracle restatement (orc_louvain_level0 / orc_lpa) inside the unmodified reference loop",
+           "reference": "fast_consensus.py (ytabatabaee/fastconsensus @ 2025-02-25)"}
+    for seed in seeds:
+        STATE["seed"], STATE["calls"] = seed, 0
+        random.seed(seed)
+        np.random.seed(seed)
+        out = fc.fast_consensus(G, algorithm=algorithm, n_p=n_p, thresh=tau, delta=delta)
+        labs = [labels_of(p, nodes, idx) for p in out]
+        rec["seeds"].append(seed)
+        rec["nmi"].append(float(np.mean([nmi(planted, l) for l in labs])))
+        rec["k"].append(float(np.mean([len(np.unique(l)) for l in labs])))
+        rec["cd_calls"].append(STATE["calls"])
+        print(name, seed, "NMI %.4f k %.1f calls %d" % (rec["nmi"][-1], rec["k"][-1], STATE["calls"]), flush=True)
+    rec["nmi_mean"] = float(np.mean(rec["nmi"]))
+    rec["nmi_sd"] = float(np.std(rec["nmi"]))
+    with open(os.path.join(HERE, "refsem_%s.json" % name), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(name, "mean %.4f sd %.4f min %.4f" % (rec["nmi_mean"], rec["nmi_sd"], min(rec["nmi"])))
+
+
+def make_lfr1k_mu055_synth():
+    """A graph where LPA finds structure (on the networkx LFR-1k at mu=0.4 every LPA run
+    collapses to one community): the native generator's LFR n=1000 mu=0.55 seed 7."""
+    from fastconsensus_amd import synth
+    path = os.path.join(HERE, "lfr1k_mu055_synth.txt")
+    u, v, planted = synth.lfr(1000, 0.55, seed=7)
+    with open(path, "w") as f:
+        for a, b in zip(u.tolist(), v.tolist()):
+            f.write("%d %d\n" % (a, b))
+    np.save(os.path.join(HERE, "lfr1k_mu055_synth_planted.npy"), planted)
+    return path
+
+
+def main():
+    fc = load_reference()
+    seeds = list(range(30))
+    run(fc, "lfr1k_louvain_np20", os.path.join(HERE, "lfr1k_mu04.txt"), os.path.join(HERE, "lfr1k_mu04_planted.npy"),
+        "louvain", 20, 0.2, 0.02, seeds)
+    syn = make_lfr1k_mu055_synth()
+    run(fc, "lfr1k_mu055_lpm_np20", syn, os.path.join(HERE, "lfr1k_mu055_synth_planted.npy"), "lpm", 20, 0.8, 0.02,
+        seeds)
+
+
+if __name__ == "__main__":
+    main()

@@ -59,7 +59,8 @@ def device_cd(fcmod, algo, N, e, count, seed):
 
 # ------------------------------------------------------------------------------ C2 (LFR-1k)
 # Tolerances (C2): mean modularity within 0.02 of the restatement and not below it by more
-# than 0.01; mean NMI to planted >= restatement - 0.03; mean community count within 25 %.
+# than 0.01 (louvain); mean NMI to planted >= restatement - 0.03; mean community count within
+# 25 % (LPA: or one community).
 # Against the reference run's own recorded labelings (networkx stand-ins): modularity
 # >= reference - 0.02, NMI >= reference - 0.03.
 def test_c2_louvain_vs_restatement_and_reference_run(fcmod):
@@ -88,28 +89,69 @@ def test_c2_lpa_vs_restatement_and_reference_run(fcmod):
     print("C2 lpa gpu", gpu, "restatement", ref, "reference-run", run)
     assert abs(gpu["q"] - ref["q"]) <= 0.02
     assert gpu["nmi"] >= ref["nmi"] - 0.03
-    assert abs(gpu["k"] - ref["k"]) <= 0.25 * ref["k"]
+    # on this graph LPA floods: the restatement and the reference run collapse to ONE
+    # community in every replica; the count tolerance is 25 % or one community
+    assert abs(gpu["k"] - ref["k"]) <= max(0.25 * ref["k"], 1.0)
     assert gpu["q"] >= run["q"] - 0.02 and gpu["nmi"] >= run["nmi"] - 0.03
 
 
-@pytest.mark.parametrize("name", ["lfr1k_louvain_np20", "lfr1k_lpm_np20"])
-def test_c2_consensus_nmi_vs_reference_final_partitions(fcmod, name):
-    """The whole consensus against the reference's OWN output (its n_p final partitions,
-    fast_consensus.py:383-392): mean NMI to planted >= reference - 0.02 (3 seeds)."""
-    case = golden_io.load(name)
-    _, g, planted = lfr1k()
-    ref = float(np.mean([nmi(planted, l) for l in case.z["final_labels"]]))
-    e = case.edges_file
-    got = []
-    for seed in (1, 2, 3):
+def refsem(name):
+    """The reference loop's own consensus NMI over 30 seeds (tests/golden/make_refsem.py)."""
+    import json
+    with open(golden_io.GOLDEN + "/refsem_%s.json" % name) as f:
+        return json.load(f)
+
+
+def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds):
+    out = []
+    for seed in seeds:
         with fcmod.Engine(seed=seed) as eng:
-            eng.load_graph(case.N, e[:, 0], e[:, 1])
-            labels, st = eng.run(case.algo, case.n_p, case.tau, case.delta)
+            eng.load_graph(N, e[:, 0], e[:, 1])
+            labels, st = eng.run(algo, n_p, tau, delta)
         assert st["iterations"] >= 1 and not st["hit_iter_cap"]
-        got.append(float(np.mean([nmi(planted, l) for l in labels])))
-    k_ref = float(np.mean([len(np.unique(l)) for l in case.z["final_labels"]]))
-    print(name, "device consensus NMI", got, "reference final NMI %.4f" % ref, "reference k %.1f" % k_ref)
-    assert np.mean(got) >= ref - 0.02
+        out.append(float(np.mean([nmi(planted, l) for l in labels])))
+    return np.array(out)
+
+
+def test_c2_louvain_consensus_nmi_vs_reference(fcmod):
+    """The whole louvain consensus against the reference's own output.  The consensus NMI
+    varies from run to run (0.80-0.95 on LFR-1k), so the device's mean over 16 seeds is held
+    to the REFERENCE LOOP's mean over 30 seeds (its unmodified code with the restated CD,
+    refsem fixture): >= reference - 0.025 (about 2.3 standard errors of the difference); the
+    reference run's recorded final partitions (fast_consensus.py:383-392, one sample) are
+    printed beside it."""
+    case = golden_io.load("lfr1k_louvain_np20")
+    _, g, planted = lfr1k()
+    ref = refsem("lfr1k_louvain_np20")
+    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(100, 116))
+    one = float(np.mean([nmi(planted, l) for l in case.z["final_labels"]]))
+    print("C2 louvain consensus NMI: device mean %.4f sd %.4f min %.4f | reference loop mean %.4f sd %.4f min %.4f "
+          "| reference run's recorded output %.4f" % (got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"],
+                                                        min(ref["nmi"]), one))
+    assert got.mean() >= ref["nmi_mean"] - 0.025
+
+
+def test_c2_lpm_consensus_nmi_vs_reference(fcmod):
+    """lpm consensus on a graph where LPA sits at its detectability edge (native LFR n=1000
+    mu=0.55: the reference loop either recovers the communities, NMI ~0.95, or collapses to one,
+    NMI 0 -- 14 of 30 seeds recover).  Device over 24 seeds: recovery rate >= reference - 0.3
+    (~3 binomial standard errors) and mean NMI of the recovering runs >= reference - 0.03.  On
+    the networkx LFR-1k (mu=0.4) every reference LPA run and every consensus collapses (NMI 0),
+    as the recorded reference output shows; printed."""
+    ref = refsem("lfr1k_mu055_lpm_np20")
+    e = np.loadtxt(golden_io.GOLDEN + "/lfr1k_mu055_synth.txt", dtype=np.int32).reshape(-1, 2)
+    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu055_synth_planted.npy")
+    got = device_runs(fcmod, 1, len(planted), e, 20, 0.8, 0.02, planted, range(200, 224))
+    r_ok = np.array(ref["nmi"]) > 0.5
+    d_ok = got > 0.5
+    case = golden_io.load("lfr1k_lpm_np20")
+    _, _, pl04 = lfr1k()
+    one = float(np.mean([nmi(pl04, l) for l in case.z["final_labels"]]))
+    print("C2 lpm consensus: device recovery %d/%d (NMI %.4f) | reference loop %d/%d (NMI %.4f) | mu=0.4 reference "
+          "output NMI %.4f" % (d_ok.sum(), len(got), got[d_ok].mean() if d_ok.any() else 0.0, r_ok.sum(), len(r_ok),
+                               np.array(ref["nmi"])[r_ok].mean(), one))
+    assert d_ok.mean() >= r_ok.mean() - 0.3
+    assert d_ok.any() and got[d_ok].mean() >= np.array(ref["nmi"])[r_ok].mean() - 0.03
 
 
 # ------------------------------------------------------------------------------ C3 (LFR-100k)

@@ -244,24 +244,19 @@ def test_louvain_quality_vs_sequential_restatement(fcmod):
 
 
 # ------------------------------------------------------------------------- end to end
-def test_run_lfr1k_nmi_not_worse(fcmod):
-    """Consensus NMI vs planted >= the reference-semantics CPU port's (tol 0.02)."""
-    from sklearn.metrics import normalized_mutual_info_score as nmi
+def test_run_lfr1k_well_formed(fcmod):
+    """A whole run: shape, statistics, and labels renumbered 0..k-1 by first node.  (Consensus
+    quality against the reference loop: tests/test_gpu_cd_parity.py.)"""
     case, g = _lfr1k_graph()
-    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu04_planted.npy")[case.z["nodes"]]
     eng = fcmod.Engine(seed=21)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     labels, st = eng.run(0, 20, 0.2, 0.02)
     assert labels.shape == (20, case.N)
-    assert st["iterations"] >= 1 and st["partition_edges"] > 0
-    s = np.mean([nmi(planted, l) for l in labels])
-    # reference-semantics single CD run (no consensus) as the floor
-    ref, _ = orc.cd_batch(0, 20, g, seed=5)
-    s_ref = np.mean([nmi(planted, l) for l in ref])
-    assert s >= s_ref - 0.02, (s, s_ref)
-    # renumbered 0..k-1 by first node
+    assert st["iterations"] >= 1 and st["partition_edges"] > 0 and st["exit_check"] in (1, 2)
     for l in labels:
         assert l[0] == 0 and l.max() == len(np.unique(l)) - 1
+        first = np.unique(l, return_index=True)[1]
+        assert np.all(np.diff(first) > 0)          # community c first appears before c + 1
     eng.close()
 
 
@@ -378,7 +373,7 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     for a, b in zip(eng.get_graph(), cpu.get_graph()):
         np.testing.assert_array_equal(a, b)
     # the Python sharded driver (world = 1, torch stream) == the native driver
-    labels2, st2 = run_sharded(eng, algo, n_p, tau, 0.02, device="cuda")
+    labels2, st2 = run_sharded(eng, algo, n_p, tau, 0.02, device="cuda", max_iters=50)
     np.testing.assert_array_equal(labels2, labels)
     assert st2["partition_edges"] == st["partition_edges"]
     eng.close()
