@@ -184,7 +184,7 @@ def launch_ranks(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="lfr1m", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=42)
@@ -275,8 +275,14 @@ def main():
         if not model:
             torch.cuda.synchronize()
 
-    def step(load):
-        """(stats, load seconds, loop seconds) of one fast_consensus call."""
+    def step(load, seed):
+        """(stats, load seconds, loop seconds) of one fast_consensus call with engine seed
+        `seed` (the run's randomness -- numbering, CD orders, closure -- and so its iteration
+        count vary with it; SURVEY §8(d): several seeds, each step its own)."""
+        if model:
+            eng.seed = seed
+        elif load:
+            eng.set_option("seed", seed)
         t = time.perf_counter()
         if load:
             eng.load_graph(n, u, v)            # §8(d) metric (1): upload + ingest are inside the call
@@ -294,7 +300,7 @@ def main():
         sync()
     m0 = len(u)
     for w in range(args.warmup):
-        st, tl, tr = step(not args.resident)
+        st, tl, tr = step(not args.resident, args.seed + 1000 + w)
         m0 = eng.graph_info()[2]
         log("[rank %d] warmup %d: load %.1f ms + loop %.1f ms, iterations=%d exit=%d m_final=%d" %
             (rank, w, 1e3 * tl, 1e3 * tr, st["iterations"], st["exit_check"], st["m_final"]))
@@ -306,8 +312,11 @@ def main():
     sync()
     t_start = time.perf_counter()
     pe_total, iters, m_finals, load_s, loop_s = 0, [], [], 0.0, 0.0
+    per_step = []
     for k in range(args.steps):
-        st, tl, tr = step(not args.resident)
+        st, tl, tr = step(not args.resident, args.seed + k)
+        per_step.append({"seed": args.seed + k, "ms": 1e3 * (tl + tr), "iterations": st["iterations"],
+                         "partition_edges": st["partition_edges"]})
         pe_total += st["partition_edges"]
         iters.append(st["iterations"])
         m_finals.append(st["m_final"])
@@ -354,7 +363,8 @@ def main():
             "metric": METRIC, "value": value, "unit": "partition·edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic (native LFR/SBM generator, seed %d)" % args.seed,
+            "data": "synthetic (native LFR/SBM generator, graph seed %d; engine seed %d + step index)"
+                    % (args.seed, args.seed),
             "config": {"workload": cfg["desc"], "n": n, "m": m0, "algorithm": cfg["algo"], "n_p": cfg["n_p"],
                        "tau": cfg["tau"], "delta": cfg["delta"], "parallelism": "replica-sharded x%d" % world,
                        "iterations": iters, "m_final": m_finals,
@@ -363,6 +373,9 @@ def main():
                                 "-> every iteration + final pass -> n_p labelings in a preallocated host array")},
             "consensus_wall_ms": 1e3 * elapsed / args.steps,
             "load_ms_per_step": 1e3 * load_s / args.steps,
+            "per_step": per_step,
+            "step_value_median": float(np.median([p["partition_edges"] / p["ms"] * 1e3 for p in per_step])),
+            "step_value_min": float(np.min([p["partition_edges"] / p["ms"] * 1e3 for p in per_step])),
             "loop_ms_per_step": 1e3 * loop_s / args.steps,
             "dist": {"backend": backend if world > 1 else None, "world_size": world},
             "roofline": roof,

@@ -94,6 +94,10 @@ class Engine:
         check(self._L.fc_set_params(self._ctx, int(buckets), int(max_sweeps), int(max_iters)))
 
     def set_option(self, name, value):
+        if name == "seed":
+            value = int(value) & (2 ** 64 - 1)
+            self.seed = value
+            value = value - 2 ** 64 if value >= 2 ** 63 else value   # int64_t on the C side
         check(self._L.fc_set_option(self._ctx, _lib.OPTIONS[name], int(value)))
 
     # -- graph -----------------------------------------------------------------------

@@ -187,6 +187,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_RELABEL: c.relabel = value != 0; break;
         case FC_OPT_STORE: c.store_order = value != 0; break;
         case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
+        case FC_OPT_SEED: c.seed = (uint64_t)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }

@@ -102,6 +102,8 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 Louvain run at load orders the vertices), so the neighbour-label
                                 gathers of a sweep hit nearby lines; 0: internal-id order.  Storage
                                 only: results are identical either way.                         */
+#define FC_OPT_SEED 10       /* replace the seed fc_create took; everything random after the call
+                                (the next fc_load_graph's numbering, CD, closure) follows it     */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */
