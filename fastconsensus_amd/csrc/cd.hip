@@ -101,6 +101,10 @@ struct CDArgs {
     unsigned long long* red;
     // pruning (list mode): per sweep >= 1 only vertices whose neighbour moved are visited
     uint8_t* aff;                // [n_r][N] affected flags (set by moves, read+cleared by list build)
+    int own_bal;                 // 1: own-label entries summed by wave ballots, not inserted in the LDS table
+    int wbits;                   // bits of the largest edge weight (LPA: 1)
+    int track_div, push_div;     // pruning starts after a sweep moving < N/track_div; pull -> push after < N/push_div (0: never)
+    int unitw;                   // every weight is 1: no weight loads
     int32_t* track;              // [n_r] moves mark neighbours affected this sweep; [n_r..2n_r) list filters;
                                  // [2n_r..3n_r) push mode: nlab is current (else decide gathers lab[col]);
                                  // [3n_r..4n_r) transition sweep: decide writes the nlab rows it gathers,
@@ -320,6 +324,11 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     const int E = __shfl(inc, WNT - 1);
     wave_sync();
     PST(1);
+    // own labels of the 8 vertices (wave-uniform) and, on lane t, vertex t's own-label weight
+    int32_t own_s[WNT];
+#pragma unroll
+    for (int q = 0; q < WNT; ++q) own_s[q] = __builtin_amdgcn_readlane(work ? own : -1, q);
+    int kacc = 0;
     // ---- flattened rows: at most 2 chunks of 4 x 64 entries (8 rows of <= 64)
     int rec[8];                                  // owned slots: (t << 8) | slot, or -1
 #pragma unroll
@@ -338,7 +347,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             jq[u] = __shfl(jb, t) + e;
             const bool ok = e < E;
             kq[u] = ok ? (push ? nlr[jq[u]] : a.colp[jq[u]]) : -1;   // pull: a label slot
-            wq[u] = ok ? (LOUV ? a.cw[jq[u]] : 1) : 0;
+            wq[u] = ok ? ((LOUV && !a.unitw) ? a.cw[jq[u]] : 1) : 0;
             tq[u] = t;
         }
         PST(2);
@@ -350,6 +359,27 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (kq[u] >= 0) nlw[jq[u]] = kq[u];
+            }
+        }
+        if (a.own_bal) {                         // wave-uniform
+            // Entries carrying their vertex's OWN label skip the table: in a settled pull sweep
+            // about half of a row does (its in-community neighbours), and those same-address
+            // LDS atomics serialise.  With 0/1 weights (LPA, the input graph; a.own_bal is set
+            // only then) their weight sum per vertex is a count: lane t (< 8) counts its lanes
+            // [ex - base, inc - base) of each load in one ballot.
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                int32_t ow = own_s[0];
+#pragma unroll
+                for (int q = 1; q < WNT; ++q) ow = tq[u] == q ? own_s[q] : ow;
+                const bool isown = kq[u] >= 0 && kq[u] == ow;
+                if (isown) kq[u] = -2;
+                const int base = c * 256 + u * 64;
+                const int lo = min(max(ex - base, 0), 64), hi = min(max(inc - base, 0), 64);
+                const unsigned long long msk = (hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) &
+                                               ~(lo == 64 ? ~0ull : ((1ull << lo) - 1ull));
+                const unsigned long long bal = __ballot(isown && (wq[u] & 1));
+                if (bal && lane < WNT) kacc += (int)__popcll(bal & msk);
             }
         }
         PST(3);
@@ -378,6 +408,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         }
         PST(4);
     }
+    if (a.own_bal && lane < WNT) ws.kown[lane] = kacc;   // read after the barrier below
     wave_sync();
     // ---- candidates: own-community weight; max val over the foreign ones (Louvain) or over
     // all labels (LPA)
@@ -396,6 +427,10 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         else atomicMax(&ws.k2[t], ((unsigned long long)(uint32_t)val << 32) | hash32(ws.tvh[t] ^ (uint32_t)key));
     }
     wave_sync();
+    if (!LOUV && a.own_bal && lane < WNT && kacc > 0) {   // LPA: the own label competes
+        const unsigned long long ko = ((unsigned long long)(uint32_t)kacc << 32) | hash32(ws.tvh[lane] ^ (uint32_t)own);
+        if (ko > ws.k2[lane]) ws.k2[lane] = ko;   // every other lane's max landed before the barrier
+    }
     if (!LOUV && lane < WNT && ws.k2[lane]) ws.vm[lane] = (int32_t)(ws.k2[lane] >> 32);   // read by this lane only
     PST(5);
     int ncand = 0;
@@ -779,12 +814,16 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         atomicAdd(&vis, f[3]);
         if (a.prune) {   // lists filter next sweep iff moves were tracked this sweep
             a.track[a.n_r + r] = a.track[r];
-            if (f[2] * 4 < (unsigned long long)a.N) a.track[r] = 1;
+            if (f[2] * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
         }
         // pull -> push once a sweep moved < N/4 vertices (push pays d writes per MOVE,
         // pull d gathers per VISIT), through one transition sweep that builds nlab
         if (a.track[3 * a.n_r + r]) { a.track[3 * a.n_r + r] = 0; a.track[2 * a.n_r + r] = 1; }
-        else if (!a.track[2 * a.n_r + r] && f[2] * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
+        // (only into an UNFILTERED sweep: the transition writes the nlab row of every vertex it
+        // visits, so it must visit them all; a replica already filtering stays in pull mode)
+        else if (a.push_div && !a.track[2 * a.n_r + r] && !a.track[a.n_r + r] &&
+                 f[2] * (unsigned long long)a.push_div < (unsigned long long)a.N)
+            a.track[3 * a.n_r + r] = 1;
         if (a.active[r]) {
             atomicAdd(&cnt0, 1);
             bool stop;
@@ -972,10 +1011,12 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             atomicAdd((unsigned long long*)(n_active_out + 4), 1ull);
             if (a.prune) {
                 a.track[a.n_r + r] = a.track[r];
-                if (moves * 4 < (unsigned long long)a.N) a.track[r] = 1;
+                if (moves * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
             }
             if (a.track[3 * a.n_r + r]) { a.track[3 * a.n_r + r] = 0; a.track[2 * a.n_r + r] = 1; }
-            else if (!a.track[2 * a.n_r + r] && moves * 4 < (unsigned long long)a.N) a.track[3 * a.n_r + r] = 1;
+            else if (a.push_div && !a.track[2 * a.n_r + r] && !a.track[a.n_r + r] &&
+                     moves * (unsigned long long)a.push_div < (unsigned long long)a.N)
+                a.track[3 * a.n_r + r] = 1;
             bool stop;
             if (LOUV) stop = moves == 0 || ((double)s_acc[0] / DQ_SCALE) < 1e-7;
             else stop = s_acc[1] == 0;
@@ -1235,6 +1276,14 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
     a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
     a.hcap = std::max<int64_t>(n_heavy, 1);
+    a.track_div = c.track_div; a.push_div = c.push_div;
+    a.unitw = (!louv || (g.max_w == 1 && g.M2 == 2 * g.m)) ? 1 : 0;
+    a.wbits = 1;
+    if (louv) while (a.wbits < 31 && (g.max_w >> a.wbits) != 0) ++a.wbits;
+    // own-label register sums: with 0/1 weights (one ballot per load); weighted rows keep the
+    // table, where the sums were measured cheaper than the wave scan (LFR-1M consensus graph
+    // decide 29.0 vs 32.7 ms per batch)
+    a.own_bal = (c.own_ballot && a.wbits == 1) ? 1 : 0;
 
     // One host round trip per sweep, after the visit lists are planned: it returns the number
     // of rounds (coarse buckets) and the largest per-replica round (decide item slots), so
@@ -1283,8 +1332,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             sync(c);
             static auto t_last = std::chrono::steady_clock::now();
             const auto t_now = std::chrono::steady_clock::now();
-            fprintf(stderr, "[fc] cd it=%d sweep=%d rounds=%d visits=%llu dt_us=%.0f\n", iteration, sweep, rounds,
-                    visits, 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
+            int32_t st4[4];   // n_active[0] active, [2..3] moves of this sweep (all replicas)
+            FC_HIP(hipMemcpy(st4, n_active, sizeof(st4), hipMemcpyDeviceToHost));
+            fprintf(stderr, "[fc] cd it=%d sweep=%d rounds=%d visits=%llu moves=%llu active=%d dt_us=%.0f\n", iteration,
+                    sweep, rounds, visits, *(unsigned long long*)(st4 + 2), st4[0],
+                    1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
             t_last = t_now;
         }
     }
@@ -1481,7 +1533,18 @@ void store_order(Ctx& c) {
         explicit Pass(Ctx& x) : c(x), timer_on(x.timer.on) { c.order_pass = true; c.timer.on = false; }
         ~Pass() { c.order_pass = false; c.timer.on = timer_on; }
     } pass(c);
-    cd_run(c, FC_ALGO_LOUVAIN, 0, 1, 1, 0x3fffffff);
+    // The first sweeps place almost every vertex (LFR-1M: 89 % and 52 % of the vertices move
+    // in sweeps 0 and 1, < 6 % from sweep 3 on), so a few sweeps give the storage order; the
+    // remaining one-replica sweeps would only pay latency (FC_ORDER_SWEEPS, default 4).
+    const int ms = c.max_sweeps;
+    c.max_sweeps = std::max(1, std::min(ms, c.order_sweeps));
+    try {
+        cd_run(c, FC_ALGO_LOUVAIN, 0, 1, 1, 0x3fffffff);
+    } catch (...) {
+        c.max_sweeps = ms;
+        throw;
+    }
+    c.max_sweeps = ms;
     uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, N);
     uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, N);
     int32_t* i1 = (int32_t*)ensure<int64_t>(c.midx, N);

@@ -70,6 +70,7 @@ struct Graph {
     int64_t M2 = 0;                 // sum of kdeg = 2 * total weight
     int32_t max_deg = 0;
     int64_t max_kdeg = 0;
+    int32_t max_w = 0;              // largest edge weight (unit-weight graphs skip the weight loads)
     void release() {
         DevBuf* b[] = {&eu, &ev, &ew, &eage, &rowptr, &col, &cw, &ceid, &crev, &colp, &vrec, &kdeg};
         for (auto* x : b) x->release();
@@ -136,9 +137,17 @@ struct Ctx {
     int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 16384;  // per replica; 0 = off
     bool order_pass = false;        // store_order()'s CD run (int64 totals, see there)
     int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
+    int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 4;   // sweeps of that pass
     DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
     int coarsen = 0;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
+    // CD kernel variant that leaves every decision unchanged (A/B switch, default on):
+    // own-label entries summed in registers (ballots / wave scan) instead of the LDS table
+    int own_ballot = getenv("FC_OWN_BALLOT") ? atoi(getenv("FC_OWN_BALLOT")) : 1;
+    // sweep-mode thresholds (experiment switches): tracking/pruning after a sweep moving
+    // < N/track_div vertices, pull -> push after < N/push_div (0: stay in pull mode)
+    int track_div = getenv("FC_TRACK_DIV") ? atoi(getenv("FC_TRACK_DIV")) : 4;
+    int push_div = getenv("FC_PUSH_DIV") ? atoi(getenv("FC_PUSH_DIV")) : 4;
     bool trace = getenv("FC_TRACE") && *getenv("FC_TRACE") && *getenv("FC_TRACE") != '0';  // per-sweep stderr
     Timer timer;
     fc_stats acc{};                 // accumulated during a run (fc_run)

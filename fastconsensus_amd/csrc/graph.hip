@@ -278,7 +278,7 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
     cp(dst.colp, src.colp, 8 * m);
     cp(dst.vrec, src.vrec, 16 * n);
     cp(dst.kdeg, src.kdeg, 8 * n);
-    dst.m = src.m; dst.M2 = src.M2; dst.max_deg = src.max_deg; dst.max_kdeg = src.max_kdeg;
+    dst.m = src.m; dst.M2 = src.M2; dst.max_deg = src.max_deg; dst.max_kdeg = src.max_kdeg; dst.max_w = src.max_w;
     c.labT_valid = false;
 }
 
@@ -339,28 +339,30 @@ __global__ void k_fill_rev(int64_t m, const int32_t* posu, const int32_t* posv, 
 }
 __global__ void k_kdeg(int64_t n, const int64_t* rowptr, const int32_t* cw, int64_t* kdeg, unsigned long long* red) {
     int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int64_t s = 0, d = 0;
+    int64_t s = 0, d = 0, mw = 0;
     if (x < n) {
-        for (int64_t j = rowptr[x]; j < rowptr[x + 1]; ++j) s += cw[j];
+        for (int64_t j = rowptr[x]; j < rowptr[x + 1]; ++j) { s += cw[j]; mw = max(mw, (int64_t)cw[j]); }
         kdeg[x] = s;
         d = rowptr[x + 1] - rowptr[x];
     }
-    // block reduce: sum(kdeg), max(deg), max(kdeg)
-    __shared__ long long ss[TB], sd[TB], sk[TB];
-    ss[threadIdx.x] = s; sd[threadIdx.x] = d; sk[threadIdx.x] = s;
+    // block reduce: sum(kdeg), max(deg), max(kdeg), max(w)
+    __shared__ long long ss[TB], sd[TB], sk[TB], sw[TB];
+    ss[threadIdx.x] = s; sd[threadIdx.x] = d; sk[threadIdx.x] = s; sw[threadIdx.x] = mw;
     __syncthreads();
     for (int o = TB / 2; o > 0; o >>= 1) {
         if ((int)threadIdx.x < o) {
             ss[threadIdx.x] += ss[threadIdx.x + o];
             sd[threadIdx.x] = max(sd[threadIdx.x], sd[threadIdx.x + o]);
             sk[threadIdx.x] = max(sk[threadIdx.x], sk[threadIdx.x + o]);
+            sw[threadIdx.x] = max(sw[threadIdx.x], sw[threadIdx.x + o]);
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        atomicAdd(shard(red, 3, 0), (unsigned long long)ss[0]);
-        atomicMax(shard(red, 3, 1), (unsigned long long)sd[0]);
-        atomicMax(shard(red, 3, 2), (unsigned long long)sk[0]);
+        atomicAdd(shard(red, 4, 0), (unsigned long long)ss[0]);
+        atomicMax(shard(red, 4, 1), (unsigned long long)sd[0]);
+        atomicMax(shard(red, 4, 2), (unsigned long long)sk[0]);
+        atomicMax(shard(red, 4, 3), (unsigned long long)sw[0]);
     }
 }
 
@@ -416,13 +418,14 @@ void graph_build_csr(Ctx& c, Graph& g) {
         k_fill_rev<<<nblk(m), TB, 0, c.stream>>>(m, posu, posv, rev);
     }
     int64_t* kdeg = ensure<int64_t>(g.kdeg, n);
-    unsigned long long* red = shards_begin(c, 3);
+    unsigned long long* red = shards_begin(c, 4);
     k_kdeg<<<nblk(n), TB, 0, c.stream>>>(n, rowptr, cw, kdeg, red);
-    int64_t h[3];
-    shards_fold(c, 3, 0x6u, h);
+    int64_t h[4];
+    shards_fold(c, 4, 0xEu, h);
     g.M2 = h[0];
     g.max_deg = (int32_t)h[1];
     g.max_kdeg = h[2];
+    g.max_w = (int32_t)h[3];
     graph_slots(c, g);
 }
 
