@@ -127,12 +127,29 @@ struct CDArgs {
     unsigned long long* sacc;    // [n_r][4] light-kernel vertices / entries / candidates, summed by k_sweep_end
 };
 
-// Vertex at sweep position p, or -1 for a padding slot of the last chunk.
+// Sweep order of replica rg: a random permutation of the vertices, or of chunks of CHUNK
+// consecutive vertices whose grid is shifted by a per-(replica, sweep) offset in [0, CHUNK):
+// with a fixed grid, two vertices closer than CHUNK would share a chunk -- and so decide
+// simultaneously -- in every sweep (a dyad whose ends each join the other's singleton then
+// swaps forever; LFR-1M final pass: 200 sweeps).  The chunk domain has room for the shift
+// (cd_run: NC = (N + 2*CHUNK - 2) / CHUNK).  oracle/fc_oracle.c tw_pos_vertex restates it.
+__device__ __forceinline__ Perm sweep_perm(const CDArgs& a, int rg, int sweep) {
+    Perm P = make_perm(a.perm_n, stream_key(a.seed, (uint32_t)rg, a.iter, (uint32_t)sweep, 1));
+    if (a.chunk) P.off = stream_key(a.seed, (uint32_t)rg, a.iter, (uint32_t)sweep, 3) & (CHUNK - 1);
+    return P;
+}
+// Vertex at sweep position p, or -1 for a padding slot.
 __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, int64_t p) {
     const uint32_t p32 = (uint32_t)p;
     if (!a.chunk) return (int32_t)perm_apply(P, p32);
-    const uint32_t v = perm_apply(P, p32 / CHUNK) * CHUNK + (p32 % CHUNK);
-    return v < (uint32_t)a.N ? (int32_t)v : -1;
+    const int64_t w = (int64_t)perm_apply(P, p32 / CHUNK) * CHUNK + (p32 % CHUNK) - (int64_t)P.off;
+    return (w >= 0 && w < a.N) ? (int32_t)w : -1;
+}
+// Sweep position of vertex v (inverse of pos_vertex).
+__device__ __forceinline__ uint32_t vertex_pos(const CDArgs& a, const Perm& P, uint32_t v) {
+    if (!a.chunk) return perm_invert(P, v);
+    const uint32_t w = v + P.off;
+    return perm_invert(P, w / CHUNK) * CHUNK + w % CHUNK;
 }
 // Replica r's sweep visits every position (no pruning filter yet): its "list" is implicit,
 // entry di of bucket k = position k*S + di.
@@ -583,7 +600,7 @@ __global__ __launch_bounds__(DTB) void k_decide_light(CDArgs a, int bucket, int 
     const int rg = a.rbase + r;
     int32_t v = -1;
     if (in_range) {
-        if (rr.z & RR_FULL) v = pos_vertex(a, make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1)),
+        if (rr.z & RR_FULL) v = pos_vertex(a, sweep_perm(a, rg, sweep),
                                            (int64_t)rr.x + di);
         else v = a.list[(int64_t)r * a.PN + rr.x + di];                  // vertex ids
     }
@@ -902,7 +919,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         const bool full = rep_full(a, r);
         const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
         const bool dpush = a.track[2 * a.n_r + r] != 0, dtrans = a.track[3 * a.n_r + r] != 0;
-        const Perm P = make_perm(a.perm_n, stream_key(a.seed, rg, a.iter, sweep, 1));
+        const Perm P = sweep_perm(a, rg, sweep);
         const int32_t stamp = sweep + 1;
         for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
         if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
@@ -918,7 +935,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         } else if (!full) {                   // bucket the worklist (order inside a bucket is immaterial)
             for (int i = threadIdx.x; i < n; i += NTH) {
                 const uint32_t v = (uint32_t)wl[i];
-                const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
+                const uint32_t pos = vertex_pos(a, P, v);
                 atomicAdd(&s_off[pos / (uint32_t)a.S + 1], 1);
             }
             __syncthreads();
@@ -927,7 +944,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             __syncthreads();
             for (int i = threadIdx.x; i < n; i += NTH) {
                 const uint32_t v = (uint32_t)wl[i];
-                const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
+                const uint32_t pos = vertex_pos(a, P, v);
                 bl[atomicAdd(&s_cur[pos / (uint32_t)a.S], 1)] = (int32_t)v;
             }
             __syncthreads();
@@ -1043,7 +1060,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
 // per-replica lists [n_r][PN] and clears the flags.  Dynamic LDS: 2 * B ints.
 static constexpr int LB_PER = 16;        // vertices per thread in k_list_count / k_list_fill
 __device__ __forceinline__ uint32_t vertex_bucket(const CDArgs& a, const Perm& P, uint32_t v) {
-    const uint32_t pos = a.chunk ? perm_invert(P, v / CHUNK) * CHUNK + v % CHUNK : perm_invert(P, v);
+    const uint32_t pos = vertex_pos(a, P, v);
     return pos / (uint32_t)a.S;
 }
 __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t* cntfine) {
@@ -1052,7 +1069,7 @@ __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t
     if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
     for (int k = threadIdx.x; k < B; k += TB) s_lb[k] = 0;
     __syncthreads();
-    const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
+    const Perm P = sweep_perm(a, a.rbase + r, sweep);
     const uint8_t* aff = a.aff + (int64_t)r * a.N;
     const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
 #pragma unroll
@@ -1133,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const in
     for (int k = threadIdx.x; k < B; k += TB) s_cnt[k] = 0;
     __syncthreads();
     const int g = gco[r];
-    const Perm P = make_perm(a.perm_n, stream_key(a.seed, a.rbase + r, a.iter, sweep, 1));
+    const Perm P = sweep_perm(a, a.rbase + r, sweep);
     uint8_t* aff = a.aff + (int64_t)r * a.N;
     int bk[LB_PER], loc[LB_PER];
     const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
@@ -1203,7 +1220,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // sweep positions: vertices in a random order, or whole chunks of CHUNK consecutive
     // vertices in a random chunk order (coalesced per-vertex accesses)
     const int CH = c.chunk;
-    const int64_t NC = CH ? (N + CH - 1) / CH : N;
+    const int64_t NC = CH ? (N + 2 * CH - 2) / CH : N;   // room for the chunk-grid shift (sweep_perm)
     const int B = (int)std::min<int64_t>(c.buckets, NC);
     const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);

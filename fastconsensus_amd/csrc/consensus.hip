@@ -12,6 +12,7 @@ namespace fc {
 template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
 template <class K, class V>
 void sort_pairs_public(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int64_t n, int end_bit);
+void sort_keys_public(Ctx& c, const uint64_t* kin, uint64_t* kout, int64_t n, int end_bit);
 
 static constexpr int TB = 256;
 static inline unsigned nblk(int64_t n, int tb = TB) {
@@ -223,33 +224,70 @@ __device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int
 }
 
 // Attempt t (fast_consensus.py:175-184): node uniform over all N (np.random.choice over
-// nextgraph.nodes(), :177); if it has >= 2 neighbours in the post-threshold graph, two
-// distinct neighbours uniformly (random.sample, :181); candidate iff not an edge (:183).
-// Samples are drawn from the post-threshold graph, not the growing one: statistical
-// parity.  Invalid attempts get the sentinel key (sorted to the end).
-__global__ __launch_bounds__(256) void k_closure_sample(int64_t attempts, int64_t n, uint32_t k0, uint32_t k1,
+// nextgraph.nodes(), :177); if it has >= 2 neighbours, two distinct neighbours uniformly
+// (random.sample, :181); candidate iff not an edge (:183).  The reference's nextgraph GROWS
+// while it samples (a closure edge is a neighbour for every later attempt); the attempts run
+// here in closure_rounds consecutive blocks, and a block draws from the post-threshold graph
+// (krowptr/kcol) plus the C graph of every closure edge the earlier blocks found (crowptr/
+// ccol, sorted rows; null in the first block).  A node's neighbours are its kept row then
+// its C row.  Invalid attempts and existing edges get the sentinel key (sorted to the end).
+// The CPU twin in oracle/fc_oracle.c restates it bit for bit.
+__global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt, int64_t n, uint32_t k0, uint32_t k1,
                                                         uint32_t iter, const int64_t* __restrict__ krowptr,
-                                                        const int32_t* __restrict__ kcol, int bits,
-                                                        uint64_t* key, int64_t* val) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= attempts) return;
+                                                        const int32_t* __restrict__ kcol,
+                                                        const int64_t* __restrict__ crowptr,
+                                                        const int32_t* __restrict__ ccol, int bits, uint64_t* key,
+                                                        int64_t* val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cnt) return;
+    const int64_t t = t0 + i;
     const uint64_t sent = (1ull << (2 * bits)) - 1ull;
     U4 ctr = {(uint32_t)t, (uint32_t)(t >> 32), iter, 0x5eedu};
     const U4 r = philox(ctr, k0, k1);
     const int32_t x = (int32_t)below(r.x, (uint32_t)n);
-    const int64_t rb = krowptr[x];
-    const int64_t d = krowptr[x + 1] - rb;
+    const int64_t kb = krowptr[x];
+    const int64_t dk = krowptr[x + 1] - kb;
+    const int64_t cb = crowptr ? crowptr[x] : 0;
+    const int64_t d = dk + (crowptr ? crowptr[x + 1] - cb : 0);
     uint64_t k = sent;
     if (d >= 2) {
         const uint32_t i1 = below(r.y, (uint32_t)d);
         uint32_t i2 = below(r.z, (uint32_t)(d - 1));
         if (i2 >= i1) ++i2;
-        const int32_t a = kcol[rb + i1], b = kcol[rb + i2];
+        const int32_t a = (int64_t)i1 < dk ? kcol[kb + i1] : ccol[cb + i1 - dk];
+        const int32_t b = (int64_t)i2 < dk ? kcol[kb + i2] : ccol[cb + i2 - dk];
         const int32_t u = a < b ? a : b, v = a < b ? b : a;
-        if (!has_edge_sorted(krowptr, kcol, u, v)) k = ((uint64_t)u << bits) | (uint64_t)v;
+        if (!has_edge_sorted(krowptr, kcol, u, v) && !(crowptr && has_edge_sorted(crowptr, ccol, u, v)))
+            k = ((uint64_t)u << bits) | (uint64_t)v;
     }
-    key[t] = k;
-    val[t] = t;
+    key[i] = k;
+    val[i] = t;
+}
+// Round candidates (sorted; first occurrence of each key) appended to the accumulated list.
+__global__ void k_append_cand(int64_t n, const int64_t* flag, const int64_t* pos, const uint64_t* key,
+                              const int64_t* val, int64_t base, uint64_t* akey, int64_t* aval) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    akey[base + pos[i]] = key[i];
+    aval[base + pos[i]] = val[i];
+}
+// Directed entries of the C graph: candidate (u, v) -> keys (u, v) and (v, u).
+__global__ void k_cgraph_keys(int64_t k, const uint64_t* akey, int bits, uint64_t* dkey) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const uint64_t u = akey[i] >> bits, v = akey[i] & ((1ull << bits) - 1ull);
+    dkey[2 * i] = (u << bits) | v;
+    dkey[2 * i + 1] = (v << bits) | u;
+}
+// Sorted directed keys -> CSR: rowptr[x] = first entry with row >= x (written once per node,
+// no atomics), col = low bits.
+__global__ void k_cgraph_csr(int64_t m2, const uint64_t* dkey, int bits, int64_t n, int64_t* rowptr, int32_t* col) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > m2) return;
+    const int64_t lo = i == 0 ? -1 : (int64_t)(dkey[i - 1] >> bits);
+    const int64_t hi = i == m2 ? n : (int64_t)(dkey[i] >> bits);
+    for (int64_t x = lo + 1; x <= hi; ++x) rowptr[x] = i;
+    if (i < m2) col[i] = (int32_t)(dkey[i] & ((1ull << bits) - 1ull));
 }
 __global__ void k_pairs_keys(int64_t np_, const int32_t* pairs, const int64_t* krowptr, const int32_t* kcol,
                              int bits, uint64_t* key, int64_t* val) {
@@ -307,14 +345,46 @@ static void finish_candidates(Ctx& c, int64_t n, uint64_t* k1, int64_t* v1, int 
 void closure_sample(Ctx& c, int64_t attempts, int iteration) {
     const int sl = timer_begin(c);
     const int64_t cap = attempts > 0 ? attempts : 1;
-    uint64_t* k1 = ensure<uint64_t>(c.mkey, cap);
-    int64_t* v1 = ensure<int64_t>(c.midx, cap);
+    const int R = (int)std::max<int64_t>(1, std::min<int64_t>(c.closure_rounds, cap));
+    const int64_t rcap = (cap + R - 1) / R + 1;   // attempts per block (at most)
+    uint64_t* k1 = ensure<uint64_t>(c.mkey, rcap);
+    int64_t* v1 = ensure<int64_t>(c.midx, rcap);
+    uint64_t* k2 = ensure<uint64_t>(c.mkey2, rcap);
+    int64_t* v2 = ensure<int64_t>(c.midx2, rcap);
+    uint64_t* akey = ensure<uint64_t>(c.clo_akey, cap);
+    int64_t* aval = ensure<int64_t>(c.clo_aval, cap);
+    const int64_t fcap = std::max<int64_t>(rcap + 1, 2 * (c.g.m + 1) + 1);
+    int64_t* fl = ensure<int64_t>(c.flag, fcap);
+    int64_t* ps = ensure<int64_t>(c.pos, fcap);
+    int64_t* crow = ensure<int64_t>(c.clo_rowptr, c.N + 1);
     const uint64_t s = mix64(c.seed ^ 0xC105u);
-    if (attempts > 0)
-        k_closure_sample<<<nblk(attempts), TB, 0, c.stream>>>(attempts, c.N, (uint32_t)s, (uint32_t)(s >> 32),
-                                                             (uint32_t)iteration, c.krowptr.as<int64_t>(),
-                                                             c.kcol.as<int32_t>(), c.key_bits, k1, v1);
-    finish_candidates(c, attempts, k1, v1, iteration);
+    const int bits = c.key_bits;
+    int64_t nacc = 0;
+    for (int r = 0; r < R; ++r) {
+        const int64_t t0 = attempts * r / R, t1 = attempts * (r + 1) / R, n = t1 - t0;
+        if (n <= 0) continue;
+        const bool have_c = nacc > 0;
+        k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
+                                                      c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
+                                                      have_c ? crow : nullptr,
+                                                      have_c ? c.clo_col.as<int32_t>() : nullptr, bits, k1, v1);
+        // this block's candidates: sorted, first sample of each pair (stable sort keeps sample order)
+        sort_pairs_public(c, (const uint64_t*)k1, k2, (const int64_t*)v1, v2, n, 2 * bits);
+        k_first_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, k2, bits, fl);
+        exclusive_scan(c, fl, ps, n + 1);
+        k_append_cand<<<nblk(n), TB, 0, c.stream>>>(n, fl, ps, k2, v2, nacc, akey, aval);
+        nacc += read_i64(c, ps + n);
+        if (r + 1 == R || nacc == 0) continue;
+        // C graph of every candidate so far (symmetric, sorted rows) for the next block
+        uint64_t* dk = ensure<uint64_t>(c.clo_dkey, 2 * nacc);
+        uint64_t* dk2 = ensure<uint64_t>(c.clo_dkey2, 2 * nacc);
+        int32_t* ccol = ensure<int32_t>(c.clo_col, 2 * nacc);
+        k_cgraph_keys<<<nblk(nacc), TB, 0, c.stream>>>(nacc, akey, bits, dk);
+        sort_keys_public(c, (const uint64_t*)dk, dk2, 2 * nacc, 2 * bits);
+        k_cgraph_csr<<<nblk(2 * nacc + 1), TB, 0, c.stream>>>(2 * nacc, dk2, bits, c.N, crow, ccol);
+    }
+    // the blocks' candidate sets are disjoint: one key sort (first-sample ages ride along)
+    finish_candidates(c, nacc, akey, aval, iteration);
     timer_end(c, 2, sl);
 }
 

@@ -124,6 +124,11 @@ struct Ctx {
     DevBuf deg_next, iso, isoflag, target, tw, active, active2, hit;
     int64_t n_iso = 0;
     DevBuf mkey, mkey2, midx, midx2;  // merge sort
+    // closure over closure_rounds blocks of attempts (closure_sample): accumulated candidates
+    // (uint64 key, int64 first sample), the C graph of the earlier blocks' closure edges
+    // (sorted directed keys, CSR rowptr int64 [N+1] / col int32)
+    DevBuf clo_akey, clo_aval, clo_dkey, clo_dkey2, clo_rowptr, clo_col;
+    int closure_rounds = 16;        // FC_OPT_CLOSURE_ROUNDS
     DevBuf sort_tmp;                // hipcub temporary storage
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)

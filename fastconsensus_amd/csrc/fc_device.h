@@ -43,6 +43,7 @@ FC_HD uint32_t stream_key(uint64_t seed, uint32_t rg, uint32_t iter, uint32_t sw
 struct Perm {
     uint32_t n, hb, mask;
     uint32_t k0, k1, k2, k3;
+    uint32_t off;   // chunked CD orders: shift of the chunk grid (cd.hip sweep_perm), else 0
 };
 FC_HD Perm make_perm(uint32_t n, uint32_t key) {
     Perm p;
@@ -53,6 +54,7 @@ FC_HD Perm make_perm(uint32_t n, uint32_t key) {
     p.n = n; p.hb = hb; p.mask = (1u << hb) - 1u;
     p.k0 = hash2(key, 0x1234567u); p.k1 = hash2(key, 0x89abcdefu);
     p.k2 = hash2(key, 0x2468aceu); p.k3 = hash2(key, 0x13579bdu);
+    p.off = 0;
     return p;
 }
 FC_HD uint32_t feistel_round(uint32_t x, const Perm& p) {

@@ -30,6 +30,13 @@ static void sort_pairs(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, int
     FC_HIP(hipcub::DeviceRadixSort::SortPairs(c.sort_tmp.p, tmp, kin, kout, vin, vout, (int)n, 0, end_bit,
                                               c.stream));
 }
+void sort_keys_public(Ctx& c, const uint64_t* kin, uint64_t* kout, int64_t n, int end_bit) {
+    if (n <= 0) return;
+    size_t tmp = 0;
+    FC_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, kin, kout, (int)n, 0, end_bit, c.stream));
+    c.sort_tmp.ensure(tmp);
+    FC_HIP(hipcub::DeviceRadixSort::SortKeys(c.sort_tmp.p, tmp, kin, kout, (int)n, 0, end_bit, c.stream));
+}
 template <class T>
 void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n) {
     if (n <= 0) return;

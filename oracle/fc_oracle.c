@@ -489,6 +489,19 @@ static uint32_t tw_perm_apply(const tw_perm* p, uint32_t x) {
     } while (x >= p->n);
     return x;
 }
+/* Vertex at sweep position p (or >= N: a padding slot).  Chunked orders visit chunks of
+ * `chunk` consecutive vertices; the chunk grid is shifted by a per-(replica, sweep) offset
+ * off in [0, chunk) (engine cd.hip pos_vertex), so two vertices closer than `chunk` do not
+ * share a chunk -- and decide simultaneously -- in every sweep: a fixed grid kept such a pair
+ * swapping communities forever (a dyad whose ends each join the other's singleton). */
+static inline i64 tw_pos_vertex(const tw_perm* P, int chunk, uint32_t off, i64 N, i64 p) {
+    if (!chunk) return (i64)tw_perm_apply(P, (uint32_t)p);
+    const i64 w = (i64)tw_perm_apply(P, (uint32_t)(p / chunk)) * chunk + p % chunk - (i64)off;
+    return (w < 0 || w >= N) ? N : w;
+}
+static inline uint32_t tw_chunk_off(int chunk, u64 seed, uint32_t rg, uint32_t iter, uint32_t sweep) {
+    return chunk ? tw_stream_key(seed, rg, iter, sweep, 3) & (uint32_t)(chunk - 1) : 0u;
+}
 static inline uint32_t tw_tie(uint32_t tbk, i32 v, i32 c) { return tw_hash32(tw_hash32(tbk ^ (uint32_t)v) ^ (uint32_t)c); }
 static inline int tw_better(long long s1, uint32_t h1, i32 c1, long long s2, uint32_t h2, i32 c2) {
     if (s1 != s2) return s1 > s2;
@@ -523,7 +536,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     u8* seen = (u8*)calloc((size_t)N, 1);
     i32* keys = (i32*)malloc(sizeof(i32) * (size_t)(N + 1));
     /* visit order: vertices, or chunks of `chunk` consecutive vertices, in random order */
-    const i64 NC = chunk ? (N + chunk - 1) / chunk : N;
+    const i64 NC = chunk ? (N + 2 * (i64)chunk - 2) / chunk : N;   /* room for the chunk-grid shift */
     const i64 PN = chunk ? NC * chunk : N;
     const int B = (int)(buckets < NC ? buckets : NC);
     const i64 S = chunk ? ((NC + B - 1) / B) * chunk : (N + B - 1) / B;
@@ -537,6 +550,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     for (; sweep < max_sweeps && active; ++sweep) {
         const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, rg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
+        const uint32_t off = tw_chunk_off(chunk, seed, rg, iter, (uint32_t)sweep);
         unsigned long long dq = 0, moves = 0, unstable = 0;
         const int listed = prune && sweep > 0;
         if (listed) {   /* all lists are built (and flags cleared) at the sweep start;
@@ -547,9 +561,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
                 i64 blen = PN - (i64)k * S;
                 if (blen > S) blen = S;
                 for (i64 i = 0; i < blen; ++i) {
-                    const i64 p = (i64)k * S + i;
-                    const i64 vv = chunk ? (i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk
-                                         : (i64)tw_perm_apply(&P, (uint32_t)p);
+                    const i64 vv = tw_pos_vertex(&P, chunk, off, N, (i64)k * S + i);
                     if (vv < N) {
                         if (!prune_now || aff[vv]) lists[n++] = i;
                         aff[vv] = 0;
@@ -571,9 +583,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
                 dec[e] = -1;
                 /* position: listed entries of round [k, k1) carry their own bucket */
                 const int kb = listed ? bucket_of_entry(loff, k, k1, loff[k] + e) : k;
-                const i64 p = (i64)kb * S + i;
-                const i64 vv = chunk ? (i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk
-                                     : (i64)tw_perm_apply(&P, (uint32_t)p);
+                const i64 vv = tw_pos_vertex(&P, chunk, off, N, (i64)kb * S + i);
                 if (vv >= N) continue;
                 const i32 v = (i32)vv;
                 const i64 rb = rowptr[v], re = rowptr[v + 1];
@@ -613,9 +623,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
                 if (dec[e] < 0) continue;
                 const i64 i = listed ? lists[loff[k] + e] : e;
                 const int kb = listed ? bucket_of_entry(loff, k, k1, loff[k] + e) : k;
-                const i64 p = (i64)kb * S + i;
-                const i32 v = chunk ? (i32)((i64)tw_perm_apply(&P, (uint32_t)(p / chunk)) * chunk + p % chunk)
-                                    : (i32)tw_perm_apply(&P, (uint32_t)p);
+                const i32 v = (i32)tw_pos_vertex(&P, chunk, off, N, (i64)kb * S + i);
                 const i32 old = lab[v], nw = dec[e];
                 lab[v] = nw;
                 if (louv) { tot[old] -= kdeg[v]; tot[nw] += kdeg[v]; csz[old]--; csz[nw]++; }
@@ -677,21 +685,83 @@ static tw_u4 tw_philox(tw_u4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 static inline uint32_t tw_below(uint32_t r, uint32_t n) { return (uint32_t)(((u64)r * n) >> 32); }
+static int cmp_u64(const void* a, const void* b) {
+    const u64 x = *(const u64*)a, y = *(const u64*)b;
+    return x < y ? -1 : x > y;
+}
+static int tw_has_edge(const i64* rowptr, const i32* col, i32 a, i32 b) {
+    i64 lo = rowptr[a], hi = rowptr[a + 1];
+    while (lo < hi) {
+        const i64 mid = (lo + hi) >> 1;
+        if (col[mid] < b) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < rowptr[a + 1] && col[lo] == b;
+}
+/* The engine's closure sampler (consensus.hip closure_sample), restated.  The reference
+ * draws its L = m attempts SEQUENTIALLY from the growing nextgraph (fast_consensus.py:175-190,
+ * :292-304): a closure edge is a neighbour for every later attempt.  The engine runs the
+ * attempts in `rounds` consecutive blocks; a block draws in parallel from the post-threshold
+ * graph plus every closure edge the earlier blocks found (the "C" graph, sorted rows).
+ * Attempt t draws Philox4x32-10(counter = {t_lo, t_hi, iteration, 0x5eed}): node x uniform
+ * over N; if x has d >= 2 neighbours (kept row ++ C row, both ascending), two distinct
+ * positions uniformly.  pairs[t] = (a, b), or (-1, -1).  orc_closure_pairs on these pairs
+ * (has_edge in the kept graph, first occurrence of each pair) gives the engine's candidates:
+ * a pair that repeats an earlier block's candidate is a duplicate there. */
 void orc_closure_sample(i64 N, const i64* krowptr, const i32* kcol, i64 attempts, u64 seed, int iteration,
-                        i32* pairs) {
+                        int rounds, i32* pairs) {
     const u64 s = tw_mix64(seed ^ 0xC105u);
     const uint32_t k0 = (uint32_t)s, k1 = (uint32_t)(s >> 32);
-    for (i64 t = 0; t < attempts; ++t) {
-        tw_u4 ctr = {(uint32_t)t, (uint32_t)((u64)t >> 32), (uint32_t)iteration, 0x5eedu};
-        const tw_u4 r = tw_philox(ctr, k0, k1);
-        const i32 x = (i32)tw_below(r.x, (uint32_t)N);
-        const i64 rb = krowptr[x], d = krowptr[x + 1] - rb;
-        pairs[2 * t] = pairs[2 * t + 1] = -1;
-        if (d < 2) continue;
-        const uint32_t i1 = tw_below(r.y, (uint32_t)d);
-        uint32_t i2 = tw_below(r.z, (uint32_t)(d - 1));
-        if (i2 >= i1) ++i2;
-        pairs[2 * t] = kcol[rb + i1];
-        pairs[2 * t + 1] = kcol[rb + i2];
+    if (rounds < 1) rounds = 1;
+    if (attempts > 0 && rounds > attempts) rounds = (int)attempts;
+    i64* crow = (i64*)calloc((size_t)N + 1, sizeof(i64));   /* C graph: empty */
+    i32* ccol = (i32*)malloc(sizeof(i32));
+    u64* cand = (u64*)malloc(sizeof(u64) * (size_t)(attempts > 0 ? attempts : 1));   /* all C edges (u << 32 | v) */
+    u64* rk = (u64*)malloc(sizeof(u64) * (size_t)(attempts > 0 ? attempts : 1));
+    i64 nc = 0;
+    for (int r = 0; r < rounds; ++r) {
+        const i64 t0 = attempts * r / rounds, t1 = attempts * (r + 1) / rounds;
+        i64 nr = 0;
+        for (i64 t = t0; t < t1; ++t) {
+            tw_u4 ctr = {(uint32_t)t, (uint32_t)((u64)t >> 32), (uint32_t)iteration, 0x5eedu};
+            const tw_u4 q = tw_philox(ctr, k0, k1);
+            const i32 x = (i32)tw_below(q.x, (uint32_t)N);
+            const i64 kb = krowptr[x], dk = krowptr[x + 1] - kb;
+            const i64 cb = crow[x], d = dk + (crow[x + 1] - cb);
+            pairs[2 * t] = pairs[2 * t + 1] = -1;
+            if (d < 2) continue;
+            const uint32_t i1 = tw_below(q.y, (uint32_t)d);
+            uint32_t i2 = tw_below(q.z, (uint32_t)(d - 1));
+            if (i2 >= i1) ++i2;
+            const i32 a = (i64)i1 < dk ? kcol[kb + i1] : ccol[cb + i1 - dk];
+            const i32 b = (i64)i2 < dk ? kcol[kb + i2] : ccol[cb + i2 - dk];
+            pairs[2 * t] = a;
+            pairs[2 * t + 1] = b;
+            const i32 u = a < b ? a : b, v = a < b ? b : a;
+            if (!tw_has_edge(krowptr, kcol, u, v) && !tw_has_edge(crow, ccol, u, v))
+                rk[nr++] = ((u64)(uint32_t)u << 32) | (uint32_t)v;
+        }
+        if (r + 1 == rounds) break;
+        qsort(rk, (size_t)nr, sizeof(u64), cmp_u64);
+        for (i64 i = 0; i < nr; ++i)
+            if (i == 0 || rk[i] != rk[i - 1]) cand[nc++] = rk[i];
+        /* rebuild C as a symmetric CSR with ascending rows */
+        u64* dk2 = (u64*)malloc(sizeof(u64) * (size_t)(2 * nc + 1));
+        for (i64 i = 0; i < nc; ++i) {
+            const u64 u = cand[i] >> 32, v = cand[i] & 0xffffffffull;
+            dk2[2 * i] = (u << 32) | v;
+            dk2[2 * i + 1] = (v << 32) | u;
+        }
+        qsort(dk2, (size_t)(2 * nc), sizeof(u64), cmp_u64);
+        free(ccol);
+        ccol = (i32*)malloc(sizeof(i32) * (size_t)(2 * nc + 1));
+        memset(crow, 0, sizeof(i64) * ((size_t)N + 1));
+        for (i64 i = 0; i < 2 * nc; ++i) {
+            crow[(dk2[i] >> 32) + 1]++;
+            ccol[i] = (i32)(dk2[i] & 0xffffffffull);
+        }
+        for (i64 x = 0; x < N; ++x) crow[x + 1] += crow[x];
+        free(dk2);
     }
+    free(crow); free(ccol); free(cand); free(rk);
 }

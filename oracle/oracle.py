@@ -72,7 +72,7 @@ def lib():
         L.orc_engine_cd.argtypes = [ctypes.c_int, i64, _i64p, _i32p, _i32p, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, _i32p, _i32p]
-        L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, _i32p]
+        L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
         _lib = L
     return _lib
@@ -182,11 +182,17 @@ def closure_from_pairs(algo, g, pairs, labels, n_p):
     return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), of[:k].copy()
 
 
-def closure_sample_pairs(kept, attempts, seed, iteration):
-    """Engine's device sampler, restated: the (a, b) pair of every attempt (or (-1, -1))."""
+CLOSURE_ROUNDS = 16   # the engine's default (fc_ctx.h closure_rounds, FC_OPT_CLOSURE_ROUNDS)
+
+
+def closure_sample_pairs(kept, attempts, seed, iteration, rounds=CLOSURE_ROUNDS):
+    """Engine's device sampler, restated: the (a, b) pair of every attempt (or (-1, -1)), the
+    attempts in `rounds` blocks, each drawing from the kept graph plus the earlier blocks'
+    closure edges (orc_closure_sample)."""
     rowptr, col, _ = kept.csr()
     pairs = np.empty((max(int(attempts), 1), 2), np.int32)
-    lib().orc_closure_sample(kept.N, rowptr, col, int(attempts), int(seed) & (2**64 - 1), int(iteration), pairs)
+    lib().orc_closure_sample(kept.N, rowptr, col, int(attempts), int(seed) & (2**64 - 1), int(iteration),
+                             int(rounds), pairs)
     return pairs[:attempts]
 
 

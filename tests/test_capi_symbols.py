@@ -72,3 +72,6 @@ def test_cpu_twin_defaults_match_engine_defaults():
         assert twin[k].default == v, k
         if k in model:
             assert model[k].default == v, k
+    rounds = int(re.search(r"\bclosure_rounds = (\d+)", src).group(1))
+    assert orc.CLOSURE_ROUNDS == rounds
+    assert inspect.signature(orc.closure_sample_pairs).parameters["rounds"].default == rounds

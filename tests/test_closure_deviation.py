@@ -2,17 +2,22 @@
 
 The reference samples its L = m attempts SEQUENTIALLY from the growing graph
 (fast_consensus.py:175-190 louvain, :292-304 lpm): a closure edge added by attempt t is a
-neighbour for attempt t+1 and `has_edge` sees it.  The device draws all L attempts in
-parallel from the post-threshold graph (consensus.hip k_closure_sample, restated bit-exactly
-by orc_closure_sample; tests/test_gpu_cd_parity.py checks the device against it).
+neighbour for attempt t+1 and `has_edge` sees it.  The device runs the L attempts in 16
+consecutive blocks; a block draws in parallel from the post-threshold graph plus every
+closure edge the earlier blocks found (consensus.hip k_closure_sample, restated bit-exactly
+by the twin; tests/test_gpu_cd_parity.py checks the device against it).
 
 For every golden iteration the reference ran, the reference's own closure (its recorded
 samples on its kept graph) is compared with the device sampler on the SAME kept graph over
 8 seeds.  Measured (this file prints it): LFR-1k louvain it 0 (the kept graph of 5,252 edges
-more than doubles during closure) 5,951 reference candidates vs 5,647 +- 42 device (-5.1 %);
-LFR-1k lpm 12,417 vs 12,250 +- 33 (-1.3 %); mean closure weight 19.61 vs 19.66.
-Tolerances: candidate count within 8 % of the reference (LFR-1k), mean co-membership
-weight of the closure edges within 5 % (louvain).  Karate (6-13 candidates) is printed only.
+more than doubles during closure) 5,951 reference candidates vs 6,070 +- 40 device (+2.0 %;
+a sequential restatement averages 6,124 over 6 seeds: the reference's one sample is low);
+LFR-1k lpm 12,417 vs 12,414 +- 34; mean closure weight 19.61 vs 19.59.  With ONE block
+(every attempt from the post-threshold graph, round 1's sampler) the count was 5,647 (-5.1 %)
+and the whole consensus lost ~0.025 NMI against the reference loop on LFR-1k
+(tests/test_engine_semantics.py).  Tolerances: candidate count within 4 % of the reference
+(LFR-1k), mean co-membership weight of the closure edges within 3 % (louvain).  Karate
+(6-13 candidates) is printed only.
 """
 import numpy as np
 import pytest
@@ -49,9 +54,9 @@ def test_closure_candidates_vs_reference_sequential_sampler(name):
     assert rows
     for r in rows:
         print(name, r)
-        assert abs(r["dev"] - r["ref"]) <= 0.08 * r["ref"], r
+        assert abs(r["dev"] - r["ref"]) <= 0.04 * r["ref"], r
         if case.algo != 1:
-            assert abs(r["dev_w"] - r["ref_w"]) <= 0.05 * r["ref_w"], r
+            assert abs(r["dev_w"] - r["ref_w"]) <= 0.03 * r["ref_w"], r
         else:
             assert r["ref_w"] == 0.0 and r["dev_w"] == 0.0      # lpm closure weight is always 0 (:302-304)
 

@@ -115,15 +115,15 @@ def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds):
 
 def test_c2_louvain_consensus_nmi_vs_reference(fcmod):
     """The whole louvain consensus against the reference's own output.  The consensus NMI
-    varies from run to run (0.80-0.95 on LFR-1k), so the device's mean over 16 seeds is held
+    varies from run to run (0.78-0.95 on LFR-1k), so the device's mean over 32 seeds is held
     to the REFERENCE LOOP's mean over 30 seeds (its unmodified code with the restated CD,
-    refsem fixture): >= reference - 0.025 (about 2.3 standard errors of the difference); the
+    refsem fixture): >= reference - 0.025 (about 2.5 standard errors of the difference); the
     reference run's recorded final partitions (fast_consensus.py:383-392, one sample) are
     printed beside it."""
     case = golden_io.load("lfr1k_louvain_np20")
     _, g, planted = lfr1k()
     ref = refsem("lfr1k_louvain_np20")
-    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(100, 116))
+    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(100, 132))
     one = float(np.mean([nmi(planted, l) for l in case.z["final_labels"]]))
     print("C2 louvain consensus NMI: device mean %.4f sd %.4f min %.4f | reference loop mean %.4f sd %.4f min %.4f "
           "| reference run's recorded output %.4f" % (got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"],

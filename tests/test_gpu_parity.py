@@ -308,8 +308,10 @@ def test_run_into_caller_buffer(fcmod):
 
 
 def test_closure_sampler_properties(fcmod):
-    """Device closure: every new edge joins two neighbours of some node in the
-    post-threshold graph, was absent there, and carries the co-membership count."""
+    """Device closure: every new edge joins two neighbours of some node in the GROWING graph
+    (post-threshold graph plus the closure edges of earlier attempt blocks,
+    fast_consensus.py:175-184), was absent from the post-threshold graph, and carries the
+    co-membership count (:186-190)."""
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=5)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
@@ -333,8 +335,11 @@ def test_closure_sampler_properties(fcmod):
     new = [(a, b, c, t) for a, b, c, t in zip(u, v, w, age) if (a, b) not in kept]
     closure = [x for x in new if ((x[3] >> 40) == 1) and not (x[3] & (1 << 39))]
     assert len(closure) == nc
+    for a, b, _, _ in closure:
+        nbrs[a].add(b)
+        nbrs[b].add(a)
     for a, b, c, _ in closure[:2000]:
-        assert nbrs[a] & nbrs[b], "closure edge must close a 2-path"
+        assert (nbrs[a] & nbrs[b]) - {a, b}, "closure edge must close a 2-path"
         assert c == int((lab[:, a] == lab[:, b]).sum())
     eng.close()
 
