@@ -227,21 +227,26 @@ __device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int
 // nextgraph.nodes(), :177); if it has >= 2 neighbours, two distinct neighbours uniformly
 // (random.sample, :181); candidate iff not an edge (:183).  The reference's nextgraph GROWS
 // while it samples (a closure edge is a neighbour for every later attempt); the attempts run
-// here in closure_rounds consecutive blocks, and a block draws from the post-threshold graph
-// (krowptr/kcol) plus the C graph of every closure edge the earlier blocks found (crowptr/
-// ccol, sorted rows; null in the first block).  A node's neighbours are its kept row then
-// its C row.  Invalid attempts and existing edges get the sentinel key (sorted to the end).
-// The CPU twin in oracle/fc_oracle.c restates it bit for bit.
+// here in closure_rounds consecutive blocks [t0, t1), and a block draws from the
+// post-threshold graph (krowptr/kcol) plus the C graph of every closure edge the earlier
+// blocks found (crowptr/ccol, ascending rows; null in the first block).  A node's neighbours
+// are its kept row then its C row.  The CPU twin in oracle/fc_oracle.c restates it bit for bit.
+// A block's candidates are deduplicated in an open-addressing table cleared per block (key
+// (u << bits) | v, value the first attempt of the block that drew it, atomicMin); the thread
+// whose CAS creates a slot lists it.  The table holds one block's pairs only (2x slots), so
+// it stays in the Infinity Cache; earlier blocks' candidates are C edges (has_edge in C).
+constexpr uint64_t CLO_EMPTY = ~0ull;
+__device__ __forceinline__ uint64_t clo_slot(uint64_t key, uint64_t mask) { return mix64(key) & mask; }
 __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt, int64_t n, uint32_t k0, uint32_t k1,
                                                         uint32_t iter, const int64_t* __restrict__ krowptr,
                                                         const int32_t* __restrict__ kcol,
                                                         const int64_t* __restrict__ crowptr,
-                                                        const int32_t* __restrict__ ccol, int bits, uint64_t* key,
-                                                        int64_t* val) {
+                                                        const int32_t* __restrict__ ccol, int bits,
+                                                        uint64_t* hkey, uint32_t* hval, uint64_t hmask,
+                                                        int64_t* list, unsigned long long* nlist) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cnt) return;
     const int64_t t = t0 + i;
-    const uint64_t sent = (1ull << (2 * bits)) - 1ull;
     U4 ctr = {(uint32_t)t, (uint32_t)(t >> 32), iter, 0x5eedu};
     const U4 r = philox(ctr, k0, k1);
     const int32_t x = (int32_t)below(r.x, (uint32_t)n);
@@ -249,45 +254,81 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
     const int64_t dk = krowptr[x + 1] - kb;
     const int64_t cb = crowptr ? crowptr[x] : 0;
     const int64_t d = dk + (crowptr ? crowptr[x + 1] - cb : 0);
-    uint64_t k = sent;
-    if (d >= 2) {
-        const uint32_t i1 = below(r.y, (uint32_t)d);
-        uint32_t i2 = below(r.z, (uint32_t)(d - 1));
-        if (i2 >= i1) ++i2;
-        const int32_t a = (int64_t)i1 < dk ? kcol[kb + i1] : ccol[cb + i1 - dk];
-        const int32_t b = (int64_t)i2 < dk ? kcol[kb + i2] : ccol[cb + i2 - dk];
-        const int32_t u = a < b ? a : b, v = a < b ? b : a;
-        if (!has_edge_sorted(krowptr, kcol, u, v) && !(crowptr && has_edge_sorted(crowptr, ccol, u, v)))
-            k = ((uint64_t)u << bits) | (uint64_t)v;
+    if (d < 2) return;
+    const uint32_t i1 = below(r.y, (uint32_t)d);
+    uint32_t i2 = below(r.z, (uint32_t)(d - 1));
+    if (i2 >= i1) ++i2;
+    const int32_t a = (int64_t)i1 < dk ? kcol[kb + i1] : ccol[cb + i1 - dk];
+    const int32_t b = (int64_t)i2 < dk ? kcol[kb + i2] : ccol[cb + i2 - dk];
+    const int32_t u = a < b ? a : b, v = a < b ? b : a;
+    if (has_edge_sorted(krowptr, kcol, u, v)) return;
+    if (crowptr && has_edge_sorted(crowptr, ccol, u, v)) return;   // an earlier block's candidate
+    const uint64_t key = ((uint64_t)u << bits) | (uint64_t)v;
+    uint64_t h = clo_slot(key, hmask);
+    while (true) {
+        uint64_t k = hkey[h];
+        if (k == CLO_EMPTY) {
+            k = atomicCAS((unsigned long long*)&hkey[h], (unsigned long long)CLO_EMPTY, (unsigned long long)key);
+            if (k == CLO_EMPTY) {                 // created: a candidate of this block
+                atomicMin(&hval[h], (uint32_t)i);
+                list[atomicAdd(nlist, 1ull)] = (int64_t)h;
+                return;
+            }
+        }
+        if (k == key) { atomicMin(&hval[h], (uint32_t)i); return; }   // drawn again in this block
+        h = (h + 1) & hmask;
     }
-    key[i] = k;
-    val[i] = t;
 }
-// Round candidates (sorted; first occurrence of each key) appended to the accumulated list.
-__global__ void k_append_cand(int64_t n, const int64_t* flag, const int64_t* pos, const uint64_t* key,
-                              const int64_t* val, int64_t base, uint64_t* akey, int64_t* aval) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    akey[base + pos[i]] = key[i];
-    aval[base + pos[i]] = val[i];
-}
-// Directed entries of the C graph: candidate (u, v) -> keys (u, v) and (v, u).
-__global__ void k_cgraph_keys(int64_t k, const uint64_t* akey, int bits, uint64_t* dkey) {
+// This block's candidates (listed slots) appended to the accumulated list.
+__global__ void k_append_cand(int64_t k, const int64_t* list, const uint64_t* hkey, const uint32_t* hval, int64_t t0,
+                              uint64_t* akey, int64_t* aval) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= k) return;
-    const uint64_t u = akey[i] >> bits, v = akey[i] & ((1ull << bits) - 1ull);
-    dkey[2 * i] = (u << bits) | v;
-    dkey[2 * i + 1] = (v << bits) | u;
+    const int64_t h = list[i];
+    akey[i] = hkey[h];
+    aval[i] = t0 + (int64_t)hval[h];
 }
-// Sorted directed keys -> CSR: rowptr[x] = first entry with row >= x (written once per node,
-// no atomics), col = low bits.
-__global__ void k_cgraph_csr(int64_t m2, const uint64_t* dkey, int bits, int64_t n, int64_t* rowptr, int32_t* col) {
+// C graph, grown block by block: the new block's entries (both directions) are counted and
+// scattered per node (int32 atomics), then every node merges its old row with its sorted new
+// entries into the other buffer: row x starts at crow[x] + nrow[x] (both exclusive prefix
+// sums), rows stay ascending.  Work per block: O(new entries) atomics + one pass over N and
+// the rows; no sort of the whole C graph.
+__global__ void k_cgraph_ndeg(int64_t k, const uint64_t* akey, int bits, int32_t* ndeg) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > m2) return;
-    const int64_t lo = i == 0 ? -1 : (int64_t)(dkey[i - 1] >> bits);
-    const int64_t hi = i == m2 ? n : (int64_t)(dkey[i] >> bits);
-    for (int64_t x = lo + 1; x <= hi; ++x) rowptr[x] = i;
-    if (i < m2) col[i] = (int32_t)(dkey[i] & ((1ull << bits) - 1ull));
+    if (i >= k) return;
+    atomicAdd(&ndeg[akey[i] >> bits], 1);
+    atomicAdd(&ndeg[akey[i] & ((1ull << bits) - 1ull)], 1);
+}
+__global__ void k_cgraph_nfill(int64_t k, const uint64_t* akey, int bits, const int32_t* nrow, int32_t* cur,
+                               int32_t* ncol) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const int32_t u = (int32_t)(akey[i] >> bits), v = (int32_t)(akey[i] & ((1ull << bits) - 1ull));
+    ncol[nrow[u] + atomicAdd(&cur[u], 1)] = v;
+    ncol[nrow[v] + atomicAdd(&cur[v], 1)] = u;
+}
+__global__ void k_cgraph_merge(int64_t n, const int64_t* crow, const int32_t* col, const int32_t* nrow,
+                               int32_t* ncol, int64_t* crow2, int32_t* col2) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x > n) return;
+    const int64_t o = crow[x] + nrow[x];
+    crow2[x] = o;
+    if (x == n) return;
+    const int32_t nb = nrow[x], ne = nrow[x + 1];
+    for (int32_t i = nb + 1; i < ne; ++i) {      // the node's new entries (a few): insertion sort
+        const int32_t y = ncol[i];
+        int32_t j = i - 1;
+        while (j >= nb && ncol[j] > y) { ncol[j + 1] = ncol[j]; --j; }
+        ncol[j + 1] = y;
+    }
+    int64_t p = crow[x];
+    const int64_t pe = crow[x + 1];
+    int32_t q = nb;
+    int64_t w = o;
+    while (p < pe || q < ne) {
+        if (q >= ne || (p < pe && col[p] < ncol[q])) col2[w++] = col[p++];
+        else col2[w++] = ncol[q++];
+    }
 }
 __global__ void k_pairs_keys(int64_t np_, const int32_t* pairs, const int64_t* krowptr, const int32_t* kcol,
                              int bits, uint64_t* key, int64_t* val) {
@@ -346,44 +387,57 @@ void closure_sample(Ctx& c, int64_t attempts, int iteration) {
     const int sl = timer_begin(c);
     const int64_t cap = attempts > 0 ? attempts : 1;
     const int R = (int)std::max<int64_t>(1, std::min<int64_t>(c.closure_rounds, cap));
-    const int64_t rcap = (cap + R - 1) / R + 1;   // attempts per block (at most)
-    uint64_t* k1 = ensure<uint64_t>(c.mkey, rcap);
-    int64_t* v1 = ensure<int64_t>(c.midx, rcap);
-    uint64_t* k2 = ensure<uint64_t>(c.mkey2, rcap);
-    int64_t* v2 = ensure<int64_t>(c.midx2, rcap);
+    uint64_t hsize = 1024;
+    while (hsize < 2 * (uint64_t)((cap + R - 1) / R)) hsize <<= 1;   // one block's pairs, load <= 1/2
+    uint64_t* hkey = ensure<uint64_t>(c.clo_hkey, hsize);
+    uint32_t* hval = ensure<uint32_t>(c.clo_hval, hsize);
+    int64_t* list = ensure<int64_t>(c.clo_list, cap);
     uint64_t* akey = ensure<uint64_t>(c.clo_akey, cap);
     int64_t* aval = ensure<int64_t>(c.clo_aval, cap);
-    const int64_t fcap = std::max<int64_t>(rcap + 1, 2 * (c.g.m + 1) + 1);
-    int64_t* fl = ensure<int64_t>(c.flag, fcap);
-    int64_t* ps = ensure<int64_t>(c.pos, fcap);
     int64_t* crow = ensure<int64_t>(c.clo_rowptr, c.N + 1);
+    unsigned long long* nlist = (unsigned long long*)ensure<int64_t>(c.clo_cnt, 1);
+    FC_HIP(hipMemsetAsync(nlist, 0, sizeof(int64_t), c.stream));
     const uint64_t s = mix64(c.seed ^ 0xC105u);
     const int bits = c.key_bits;
-    int64_t nacc = 0;
+    int64_t nacc = 0, nbuilt = 0;
     for (int r = 0; r < R; ++r) {
         const int64_t t0 = attempts * r / R, t1 = attempts * (r + 1) / R, n = t1 - t0;
         if (n <= 0) continue;
-        const bool have_c = nacc > 0;
+        const bool have_c = nbuilt > 0;
+        FC_HIP(hipMemsetAsync(hkey, 0xff, sizeof(uint64_t) * hsize, c.stream));
+        FC_HIP(hipMemsetAsync(hval, 0xff, sizeof(uint32_t) * hsize, c.stream));
         k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
                                                       c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
                                                       have_c ? crow : nullptr,
-                                                      have_c ? c.clo_col.as<int32_t>() : nullptr, bits, k1, v1);
-        // this block's candidates: sorted, first sample of each pair (stable sort keeps sample order)
-        sort_pairs_public(c, (const uint64_t*)k1, k2, (const int64_t*)v1, v2, n, 2 * bits);
-        k_first_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, k2, bits, fl);
-        exclusive_scan(c, fl, ps, n + 1);
-        k_append_cand<<<nblk(n), TB, 0, c.stream>>>(n, fl, ps, k2, v2, nacc, akey, aval);
-        nacc += read_i64(c, ps + n);
-        if (r + 1 == R || nacc == 0) continue;
-        // C graph of every candidate so far (symmetric, sorted rows) for the next block
-        uint64_t* dk = ensure<uint64_t>(c.clo_dkey, 2 * nacc);
-        uint64_t* dk2 = ensure<uint64_t>(c.clo_dkey2, 2 * nacc);
-        int32_t* ccol = ensure<int32_t>(c.clo_col, 2 * nacc);
-        k_cgraph_keys<<<nblk(nacc), TB, 0, c.stream>>>(nacc, akey, bits, dk);
-        sort_keys_public(c, (const uint64_t*)dk, dk2, 2 * nacc, 2 * bits);
-        k_cgraph_csr<<<nblk(2 * nacc + 1), TB, 0, c.stream>>>(2 * nacc, dk2, bits, c.N, crow, ccol);
+                                                      have_c ? c.clo_col.as<int32_t>() : nullptr, bits, hkey, hval,
+                                                      hsize - 1, list, nlist);
+        const int64_t total = read_i64(c, (const int64_t*)nlist);   // slots listed so far (all blocks)
+        if (total > nacc)
+            k_append_cand<<<nblk(total - nacc), TB, 0, c.stream>>>(total - nacc, list + nacc, hkey, hval, t0,
+                                                                  akey + nacc, aval + nacc);
+        nacc = total;
+        if (r + 1 == R || nacc == nbuilt) continue;
+        // the C graph grows by this block's candidates (rows ascending), for the next block
+        const int64_t kn = nacc - nbuilt;
+        int32_t* nrow = (int32_t*)ensure<int32_t>(c.clo_nrow, 2 * (c.N + 1));
+        int32_t* ncur = nrow + (c.N + 1);
+        int32_t* ncol = ensure<int32_t>(c.clo_ncol, 2 * kn);
+        FC_HIP(hipMemsetAsync(nrow, 0, sizeof(int32_t) * 2 * (c.N + 1), c.stream));
+        k_cgraph_ndeg<<<nblk(kn), TB, 0, c.stream>>>(kn, akey + nbuilt, bits, ncur);
+        exclusive_scan(c, ncur, nrow, c.N + 1);
+        FC_HIP(hipMemsetAsync(ncur, 0, sizeof(int32_t) * (c.N + 1), c.stream));
+        k_cgraph_nfill<<<nblk(kn), TB, 0, c.stream>>>(kn, akey + nbuilt, bits, nrow, ncur, ncol);
+        if (nbuilt == 0) FC_HIP(hipMemsetAsync(crow, 0, sizeof(int64_t) * (c.N + 1), c.stream));
+        int64_t* crow2 = ensure<int64_t>(c.clo_rowptr2, c.N + 1);
+        int32_t* col2 = ensure<int32_t>(c.clo_col2, 2 * nacc);
+        k_cgraph_merge<<<nblk(c.N + 1), TB, 0, c.stream>>>(c.N, crow, nbuilt ? c.clo_col.as<int32_t>() : nullptr, nrow,
+                                                           ncol, crow2, col2);
+        std::swap(c.clo_rowptr, c.clo_rowptr2);
+        std::swap(c.clo_col, c.clo_col2);
+        crow = c.clo_rowptr.as<int64_t>();
+        nbuilt = nacc;
     }
-    // the blocks' candidate sets are disjoint: one key sort (first-sample ages ride along)
+    // candidates in key order (first-sample ages ride along; the keys are distinct)
     finish_candidates(c, nacc, akey, aval, iteration);
     timer_end(c, 2, sl);
 }

@@ -124,10 +124,12 @@ struct Ctx {
     DevBuf deg_next, iso, isoflag, target, tw, active, active2, hit;
     int64_t n_iso = 0;
     DevBuf mkey, mkey2, midx, midx2;  // merge sort
-    // closure over closure_rounds blocks of attempts (closure_sample): accumulated candidates
-    // (uint64 key, int64 first sample), the C graph of the earlier blocks' closure edges
-    // (sorted directed keys, CSR rowptr int64 [N+1] / col int32)
-    DevBuf clo_akey, clo_aval, clo_dkey, clo_dkey2, clo_rowptr, clo_col;
+    // closure over closure_rounds blocks of attempts (closure_sample): candidate table (uint64
+    // key, u64 first attempt), listed slots and their count, accumulated candidates (key,
+    // first attempt), the C graph of the earlier blocks' closure edges (CSR rowptr int64
+    // [N+1] / col int32, ping-pong), a block's new entries (int32 row offsets + cursors, cols)
+    DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
+        clo_nrow, clo_ncol;
     int closure_rounds = 16;        // FC_OPT_CLOSURE_ROUNDS
     DevBuf sort_tmp;                // hipcub temporary storage
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
