@@ -101,7 +101,8 @@ struct CDArgs {
     unsigned long long* red;
     // pruning (list mode): per sweep >= 1 only vertices whose neighbour moved are visited
     uint8_t* aff;                // [n_r][N] affected flags (set by moves, read+cleared by list build)
-    int own_bal;                 // 1: own-label entries summed by wave ballots, not inserted in the LDS table
+    int own_bal;                 // 1: own-label entries of weight w0 summed by wave ballots, not inserted in the LDS table
+    int w0;                      // that weight: 1 on unit-weight graphs, n_p on consensus graphs (their typical weight)
     int wbits;                   // bits of the largest edge weight (LPA: 1)
     int track_div, push_div;     // pruning starts after a sweep moving < N/track_div; pull -> push after < N/push_div (0: never)
     int unitw;                   // every weight is 1: no weight loads
@@ -380,22 +381,24 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         }
         if (a.own_bal) {                         // wave-uniform
             // Entries carrying their vertex's OWN label skip the table: in a settled pull sweep
-            // about half of a row does (its in-community neighbours), and those same-address
-            // LDS atomics serialise.  With 0/1 weights (LPA, the input graph; a.own_bal is set
-            // only then) their weight sum per vertex is a count: lane t (< 8) counts its lanes
-            // [ex - base, inc - base) of each load in one ballot.
+            // about half of a row does (its in-community neighbours; nearly all of it on a
+            // consensus graph), and those same-address LDS atomics serialise.  Those of weight
+            // w0 (1 on unit graphs -- LPA, the input graph -- n_p on consensus graphs, where
+            // agreement made most weights n_p) sum to w0 * count: lane t (< 8) counts its
+            // lanes [ex - base, inc - base) of each load in one ballot.  Own entries of any
+            // other weight still go to the table; kown adds both.
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 int32_t ow = own_s[0];
 #pragma unroll
                 for (int q = 1; q < WNT; ++q) ow = tq[u] == q ? own_s[q] : ow;
-                const bool isown = kq[u] >= 0 && kq[u] == ow;
+                const bool isown = kq[u] >= 0 && kq[u] == ow && wq[u] == a.w0;
                 if (isown) kq[u] = -2;
                 const int base = c * 256 + u * 64;
                 const int lo = min(max(ex - base, 0), 64), hi = min(max(inc - base, 0), 64);
                 const unsigned long long msk = (hi == 64 ? ~0ull : ((1ull << hi) - 1ull)) &
                                                ~(lo == 64 ? ~0ull : ((1ull << lo) - 1ull));
-                const unsigned long long bal = __ballot(isown && (wq[u] & 1));
+                const unsigned long long bal = __ballot(isown);
                 if (bal && lane < WNT) kacc += (int)__popcll(bal & msk);
             }
         }
@@ -425,7 +428,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         }
         PST(4);
     }
-    if (a.own_bal && lane < WNT) ws.kown[lane] = kacc;   // read after the barrier below
+    if (a.own_bal && lane < WNT) ws.kown[lane] = kacc * a.w0;   // the table's own slot adds to it below
     wave_sync();
     // ---- candidates: own-community weight; max val over the foreign ones (Louvain) or over
     // all labels (LPA)
@@ -435,7 +438,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
         const int32_t key = ws.key[sl], val = ws.val[sl];
         if (key == ws.own[t]) {
-            ws.kown[t] = val;
+            ws.kown[t] += val;                   // one owner per slot; the ballot sum landed before the barrier
             if (LOUV) { rec[it] = -1; continue; }   // LPA: the own label competes
         }
         if (LOUV) atomicMax(&ws.vm[t], val);
@@ -1297,10 +1300,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.unitw = (!louv || (g.max_w == 1 && g.M2 == 2 * g.m)) ? 1 : 0;
     a.wbits = 1;
     if (louv) while (a.wbits < 31 && (g.max_w >> a.wbits) != 0) ++a.wbits;
-    // own-label register sums: with 0/1 weights (one ballot per load); weighted rows keep the
-    // table, where the sums were measured cheaper than the wave scan (LFR-1M consensus graph
-    // decide 29.0 vs 32.7 ms per batch)
-    a.own_bal = (c.own_ballot && a.wbits == 1) ? 1 : 0;
+    // own-label register sums (one ballot per load) for the entries of the graph's typical
+    // weight w0; the rest of a weighted row keeps the table (a full wave scan of weighted own
+    // sums measured slower: LFR-1M consensus graph decide 32.7 vs 29.0 ms per batch)
+    a.own_bal = c.own_ballot ? 1 : 0;
+    a.w0 = a.wbits == 1 ? 1 : std::max(1, n_p_total);
 
     // One host round trip per sweep, after the visit lists are planned: it returns the number
     // of rounds (coarse buckets) and the largest per-replica round (decide item slots), so
