@@ -243,9 +243,10 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
                                                         const int64_t* __restrict__ crowptr,
                                                         const int32_t* __restrict__ ccol, int bits,
                                                         uint64_t* hkey, uint32_t* hval, uint64_t hmask,
-                                                        int64_t* list, unsigned long long* nlist) {
+                                                        int64_t* slot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cnt) return;
+    slot[i] = -1;
     const int64_t t = t0 + i;
     U4 ctr = {(uint32_t)t, (uint32_t)(t >> 32), iter, 0x5eedu};
     const U4 r = philox(ctr, k0, k1);
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
             k = atomicCAS((unsigned long long*)&hkey[h], (unsigned long long)CLO_EMPTY, (unsigned long long)key);
             if (k == CLO_EMPTY) {                 // created: a candidate of this block
                 atomicMin(&hval[h], (uint32_t)i);
-                list[atomicAdd(nlist, 1ull)] = (int64_t)h;
+                slot[i] = (int64_t)h;            // dense: no shared counter (one hot address serialised the block)
                 return;
             }
         }
@@ -279,30 +280,39 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
         h = (h + 1) & hmask;
     }
 }
-// This block's candidates (listed slots) appended to the accumulated list.
-__global__ void k_append_cand(int64_t k, const int64_t* list, const uint64_t* hkey, const uint32_t* hval, int64_t t0,
-                              uint64_t* akey, int64_t* aval) {
+// This block's candidates (the attempts that created a slot, in attempt order) appended to
+// the accumulated list at the device-side count *nacc (no host round trip per block).
+__global__ void k_slot_flags(int64_t n, const int64_t* slot, int64_t* flag) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
-    const int64_t h = list[i];
-    akey[i] = hkey[h];
-    aval[i] = t0 + (int64_t)hval[h];
+    if (i > n) return;
+    flag[i] = (i < n && slot[i] >= 0) ? 1 : 0;
+}
+__global__ void k_append_cand(int64_t n, const int64_t* slot, const int64_t* pos, const uint64_t* hkey,
+                              const uint32_t* hval, int64_t t0, int64_t* nacc, uint64_t* akey, int64_t* aval) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t base = nacc[0];
+    if (i < n && slot[i] >= 0) {
+        const int64_t h = slot[i];
+        akey[base + pos[i]] = hkey[h];
+        aval[base + pos[i]] = t0 + (int64_t)hval[h];
+    }
+    if (i == n) { nacc[1] = base; nacc[0] = base + pos[n]; }   // [1]: the block's first entry
 }
 // C graph, grown block by block: the new block's entries (both directions) are counted and
 // scattered per node (int32 atomics), then every node merges its old row with its sorted new
 // entries into the other buffer: row x starts at crow[x] + nrow[x] (both exclusive prefix
 // sums), rows stay ascending.  Work per block: O(new entries) atomics + one pass over N and
 // the rows; no sort of the whole C graph.
-__global__ void k_cgraph_ndeg(int64_t k, const uint64_t* akey, int bits, int32_t* ndeg) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
+__global__ void k_cgraph_ndeg(const int64_t* nacc, const uint64_t* akey, int bits, int32_t* ndeg) {
+    const int64_t i = nacc[1] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // this block's candidates
+    if (i >= nacc[0]) return;
     atomicAdd(&ndeg[akey[i] >> bits], 1);
     atomicAdd(&ndeg[akey[i] & ((1ull << bits) - 1ull)], 1);
 }
-__global__ void k_cgraph_nfill(int64_t k, const uint64_t* akey, int bits, const int32_t* nrow, int32_t* cur,
+__global__ void k_cgraph_nfill(const int64_t* nacc, const uint64_t* akey, int bits, const int32_t* nrow, int32_t* cur,
                                int32_t* ncol) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= k) return;
+    const int64_t i = nacc[1] + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nacc[0]) return;
     const int32_t u = (int32_t)(akey[i] >> bits), v = (int32_t)(akey[i] & ((1ull << bits) - 1ull));
     ncol[nrow[u] + atomicAdd(&cur[u], 1)] = v;
     ncol[nrow[v] + atomicAdd(&cur[v], 1)] = u;
@@ -387,58 +397,56 @@ void closure_sample(Ctx& c, int64_t attempts, int iteration) {
     const int sl = timer_begin(c);
     const int64_t cap = attempts > 0 ? attempts : 1;
     const int R = (int)std::max<int64_t>(1, std::min<int64_t>(c.closure_rounds, cap));
+    const int64_t rcap = (cap + R - 1) / R + 1;                   // attempts per block (at most)
+    const int64_t N = c.N;
     uint64_t hsize = 1024;
-    while (hsize < 2 * (uint64_t)((cap + R - 1) / R)) hsize <<= 1;   // one block's pairs, load <= 1/2
+    while (hsize < 2 * (uint64_t)rcap) hsize <<= 1;                // one block's pairs, load <= 1/2
     uint64_t* hkey = ensure<uint64_t>(c.clo_hkey, hsize);
     uint32_t* hval = ensure<uint32_t>(c.clo_hval, hsize);
-    int64_t* list = ensure<int64_t>(c.clo_list, cap);
+    int64_t* slot = ensure<int64_t>(c.clo_list, rcap);
+    int64_t* fl = ensure<int64_t>(c.nodetmp, std::max<int64_t>(rcap + 1, N + 1));
+    int64_t* ps = ensure<int64_t>(c.nodetmp2, std::max<int64_t>(rcap + 1, N + 1));
     uint64_t* akey = ensure<uint64_t>(c.clo_akey, cap);
     int64_t* aval = ensure<int64_t>(c.clo_aval, cap);
-    int64_t* crow = ensure<int64_t>(c.clo_rowptr, c.N + 1);
-    unsigned long long* nlist = (unsigned long long*)ensure<int64_t>(c.clo_cnt, 1);
-    FC_HIP(hipMemsetAsync(nlist, 0, sizeof(int64_t), c.stream));
+    int64_t* nacc = ensure<int64_t>(c.clo_cnt, 2);                 // [0] candidates so far, [1] this block's first
+    FC_HIP(hipMemsetAsync(nacc, 0, 2 * sizeof(int64_t), c.stream));
+    // the C graph (ping-pong; sized for every candidate: no reallocation inside the loop)
+    int32_t* nrow = ensure<int32_t>(c.clo_nrow, 2 * (N + 1));      // a block's new-entry offsets | cursors
+    int32_t* ncur = nrow + (N + 1);
+    int32_t* ncol = ensure<int32_t>(c.clo_ncol, 2 * rcap);
+    if (R > 1)
+        for (DevBuf* b : {&c.clo_col, &c.clo_col2}) ensure<int32_t>(*b, 2 * cap);
+    for (DevBuf* b : {&c.clo_rowptr, &c.clo_rowptr2}) ensure<int64_t>(*b, N + 1);
+    FC_HIP(hipMemsetAsync(c.clo_rowptr.p, 0, sizeof(int64_t) * (N + 1), c.stream));   // empty C graph
     const uint64_t s = mix64(c.seed ^ 0xC105u);
     const int bits = c.key_bits;
-    int64_t nacc = 0, nbuilt = 0;
     for (int r = 0; r < R; ++r) {
         const int64_t t0 = attempts * r / R, t1 = attempts * (r + 1) / R, n = t1 - t0;
         if (n <= 0) continue;
-        const bool have_c = nbuilt > 0;
         FC_HIP(hipMemsetAsync(hkey, 0xff, sizeof(uint64_t) * hsize, c.stream));
         FC_HIP(hipMemsetAsync(hval, 0xff, sizeof(uint32_t) * hsize, c.stream));
-        k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
+        k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
                                                       c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
-                                                      have_c ? crow : nullptr,
-                                                      have_c ? c.clo_col.as<int32_t>() : nullptr, bits, hkey, hval,
-                                                      hsize - 1, list, nlist);
-        const int64_t total = read_i64(c, (const int64_t*)nlist);   // slots listed so far (all blocks)
-        if (total > nacc)
-            k_append_cand<<<nblk(total - nacc), TB, 0, c.stream>>>(total - nacc, list + nacc, hkey, hval, t0,
-                                                                  akey + nacc, aval + nacc);
-        nacc = total;
-        if (r + 1 == R || nacc == nbuilt) continue;
+                                                      r > 0 ? c.clo_rowptr.as<int64_t>() : nullptr,
+                                                      r > 0 ? c.clo_col.as<int32_t>() : nullptr, bits, hkey, hval,
+                                                      hsize - 1, slot);
+        k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, fl);
+        exclusive_scan(c, fl, ps, n + 1);
+        k_append_cand<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, ps, hkey, hval, t0, nacc, akey, aval);
+        if (r + 1 == R) continue;
         // the C graph grows by this block's candidates (rows ascending), for the next block
-        const int64_t kn = nacc - nbuilt;
-        int32_t* nrow = (int32_t*)ensure<int32_t>(c.clo_nrow, 2 * (c.N + 1));
-        int32_t* ncur = nrow + (c.N + 1);
-        int32_t* ncol = ensure<int32_t>(c.clo_ncol, 2 * kn);
-        FC_HIP(hipMemsetAsync(nrow, 0, sizeof(int32_t) * 2 * (c.N + 1), c.stream));
-        k_cgraph_ndeg<<<nblk(kn), TB, 0, c.stream>>>(kn, akey + nbuilt, bits, ncur);
-        exclusive_scan(c, ncur, nrow, c.N + 1);
-        FC_HIP(hipMemsetAsync(ncur, 0, sizeof(int32_t) * (c.N + 1), c.stream));
-        k_cgraph_nfill<<<nblk(kn), TB, 0, c.stream>>>(kn, akey + nbuilt, bits, nrow, ncur, ncol);
-        if (nbuilt == 0) FC_HIP(hipMemsetAsync(crow, 0, sizeof(int64_t) * (c.N + 1), c.stream));
-        int64_t* crow2 = ensure<int64_t>(c.clo_rowptr2, c.N + 1);
-        int32_t* col2 = ensure<int32_t>(c.clo_col2, 2 * nacc);
-        k_cgraph_merge<<<nblk(c.N + 1), TB, 0, c.stream>>>(c.N, crow, nbuilt ? c.clo_col.as<int32_t>() : nullptr, nrow,
-                                                           ncol, crow2, col2);
+        FC_HIP(hipMemsetAsync(nrow, 0, sizeof(int32_t) * 2 * (N + 1), c.stream));
+        k_cgraph_ndeg<<<nblk(n), TB, 0, c.stream>>>(nacc, akey, bits, ncur);
+        exclusive_scan(c, ncur, nrow, N + 1);
+        FC_HIP(hipMemsetAsync(ncur, 0, sizeof(int32_t) * (N + 1), c.stream));
+        k_cgraph_nfill<<<nblk(n), TB, 0, c.stream>>>(nacc, akey, bits, nrow, ncur, ncol);
+        k_cgraph_merge<<<nblk(N + 1), TB, 0, c.stream>>>(N, c.clo_rowptr.as<int64_t>(), c.clo_col.as<int32_t>(), nrow,
+                                                         ncol, c.clo_rowptr2.as<int64_t>(), c.clo_col2.as<int32_t>());
         std::swap(c.clo_rowptr, c.clo_rowptr2);
         std::swap(c.clo_col, c.clo_col2);
-        crow = c.clo_rowptr.as<int64_t>();
-        nbuilt = nacc;
     }
     // candidates in key order (first-sample ages ride along; the keys are distinct)
-    finish_candidates(c, nacc, akey, aval, iteration);
+    finish_candidates(c, read_i64(c, nacc), akey, aval, iteration);
     timer_end(c, 2, sl);
 }
 

@@ -130,7 +130,7 @@ struct Ctx {
     // [N+1] / col int32, ping-pong), a block's new entries (int32 row offsets + cursors, cols)
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
-    int closure_rounds = 16;        // FC_OPT_CLOSURE_ROUNDS
+    int closure_rounds = 8;         // FC_OPT_CLOSURE_ROUNDS
     DevBuf sort_tmp;                // hipcub temporary storage
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)

@@ -2,7 +2,7 @@
 
 The reference samples its L = m attempts SEQUENTIALLY from the growing graph
 (fast_consensus.py:175-190 louvain, :292-304 lpm): a closure edge added by attempt t is a
-neighbour for attempt t+1 and `has_edge` sees it.  The device runs the L attempts in 16
+neighbour for attempt t+1 and `has_edge` sees it.  The device runs the L attempts in 8
 consecutive blocks; a block draws in parallel from the post-threshold graph plus every
 closure edge the earlier blocks found (consensus.hip k_closure_sample, restated bit-exactly
 by the twin; tests/test_gpu_cd_parity.py checks the device against it).
@@ -10,9 +10,10 @@ by the twin; tests/test_gpu_cd_parity.py checks the device against it).
 For every golden iteration the reference ran, the reference's own closure (its recorded
 samples on its kept graph) is compared with the device sampler on the SAME kept graph over
 8 seeds.  Measured (this file prints it): LFR-1k louvain it 0 (the kept graph of 5,252 edges
-more than doubles during closure) 5,951 reference candidates vs 6,070 +- 40 device (+2.0 %;
-a sequential restatement averages 6,124 over 6 seeds: the reference's one sample is low);
-LFR-1k lpm 12,417 vs 12,414 +- 34; mean closure weight 19.61 vs 19.59.  With ONE block
+more than doubles during closure) 5,951 reference candidates vs 6,065 +- 42 device (+1.9 %;
+a sequential restatement averages 6,124 over 6 seeds: the reference's one sample is low;
+16 blocks give 6,070, LFR-1M shows no difference from 2 blocks up); LFR-1k lpm 12,417 vs
+12,401 +- 44; mean closure weight 19.61 vs 19.60.  With ONE block
 (every attempt from the post-threshold graph, round 1's sampler) the count was 5,647 (-5.1 %)
 and the whole consensus lost ~0.025 NMI against the reference loop on LFR-1k
 (tests/test_engine_semantics.py).  Tolerances: candidate count within 4 % of the reference

@@ -1,4 +1,5 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 600 python tools/cd_ab.py --reps 2 base base@FC_TRACK_DIV=1 base@FC_TRACK_DIV=1,FC_PUSH_DIV=1 > gpurun_out/ab_trk.out 2>&1; rc=$?
-cat gpurun_out/ab_trk.out; exit $rc
+bash tools/gpu_r2.sh pytest bench1m_fast || exit $?
+timeout -k 10 300 python bench.py --n-p 8 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/np8.out 2> gpurun_out/np8.err || exit $?
+grep -o '"ms_per_step": [0-9.]*\|"phase_ms_per_step_rank0": {[^}]*}' gpurun_out/np8.out
