@@ -24,7 +24,7 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
     for r in stats:
         summary["kernels"].append({k: r[k] for k in r})
     counters = defaultdict(lambda: defaultdict(list))
-    for name in ("fetch", "write", "l2", "sq"):
+    for name in ("fetch", "write", "l2", "sq", "sq1", "sq2"):
         for r in rows(os.path.join(prof_dir, name, "**", "*counter_collection.csv")):
             kern = r.get("Kernel_Name", "?")
             short = kern.split("(")[0].split("<")[0].strip()
@@ -36,7 +36,10 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
     for kern, cs in counters.items():
         per[kern] = {c: (sum(v) / len(v), len(v)) for c, v in cs.items()}
     summary["counters_mean_per_launch"] = {k: {c: v[0] for c, v in d.items()} for k, d in per.items()}
-    dec = [k for k in per if k.startswith("k_decide_light<louvain")] or [k for k in per if k.startswith("k_decide")]
+    # the consensus runs' decide kernel: LPA for lpm workloads, else Louvain (<true,int>; the
+    # load-time ordering pass runs <true,long> and is not counted)
+    lpa = "lpm" in config or "sbm" in config
+    dec = [k for k in per if k.startswith("k_decide_light<lpa" if lpa else "k_decide_light<louvain")]
     if dec:
         d = per[dec[0]]
         fetch = d.get("FETCH_SIZE", (None,))[0]
