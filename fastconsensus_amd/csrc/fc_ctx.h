@@ -146,7 +146,7 @@ struct Ctx {
     int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
     int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 4;   // sweeps of that pass
     DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
-    int coarsen = 0;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
+    int coarsen = 8;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     // CD kernel variant that leaves every decision unchanged (A/B switch, default on):
     // own-label entries summed in registers (ballots / wave scan) instead of the LDS table

@@ -93,10 +93,11 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_TAIL_VISITS 7 /* once no replica visits more than this many vertices in a sweep,
                                 the remaining sweeps run in one workgroup per replica (default
                                 16384; 0 = off).  Same results either way.                      */
-#define FC_OPT_COARSEN 8    /* 0 (default): one bucket per round.  gmax > 0: a filtered sweep of V
-                                vertices runs its buckets in rounds of g (largest power of two <= gmax,
-                                <= buckets, with V*g <= n).  Experimental: coarse rounds decide more
-                                neighbouring vertices simultaneously and can need many more sweeps. */
+#define FC_OPT_COARSEN 8    /* gmax (default 8; 0 = off): a filtered sweep of V vertices runs its buckets in
+                                rounds of g (the largest power of two <= gmax, <= buckets, with V*g <= n),
+                                so a small sweep is not 32 latency-bound rounds.  Measured neutral on
+                                quality (LFR-100k CD modularity/NMI equal at 0/4/8; LFR-1k consensus NMI
+                                0.9035 vs 0.9034 at 0/8) and -18 ms on the LFR-1M run.              */
 #define FC_OPT_STORE 9       /* label storage order (set it before fc_load_graph).  1 (default): the
                                 replicas' label rows are stored in community order (a one-replica
                                 Louvain run at load orders the vertices), so the neighbour-label

@@ -217,7 +217,7 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     return lab, sw
 
 
-def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=0):
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels); defaults = the
     engine's defaults (fc_ctx.h)."""
     rowptr, col, cw = g.csr()

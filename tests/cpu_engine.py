@@ -12,7 +12,7 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=0):
+    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8):
         """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity."""
         self.seed = int(seed)
         self.buckets = buckets

@@ -160,7 +160,7 @@ def _lfr1k_graph():
 TAILS = [0, 1 << 40]
 
 
-@pytest.mark.parametrize("coarsen", [0, 4])
+@pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("buckets,chunk,prune", [(32, 0, 0), (5, 0, 0), (32, 16, 0), (7, 16, 0), (32, 0, 1),
