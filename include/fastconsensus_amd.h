@@ -92,7 +92,7 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 #define FC_OPT_TAIL_VISITS 7 /* once no replica visits more than this many vertices in a sweep,
                                 the remaining sweeps run in one workgroup per replica (default
-                                16384; 0 = off).  Same results either way.                      */
+                                4096; 0 = off).  Same results either way.                       */
 #define FC_OPT_COARSEN 8    /* gmax (default 8; 0 = off): a filtered sweep of V vertices runs its buckets in
                                 rounds of g (the largest power of two <= gmax, <= buckets, with V*g <= n),
                                 so a small sweep is not 32 latency-bound rounds.  Measured neutral on
