@@ -553,6 +553,38 @@ __global__ void k_iso_update(int64_t k, const int32_t* hit, int32_t* active, int
     const int32_t a = hit[i] ? 0 : 1;
     if (a != active[i]) { active[i] = a; *changed = 1; }
 }
+// The same fixpoint in ONE workgroup with the state in LDS (k <= ISO_LDS isolates): no host
+// round trip per Jacobi sweep (round 1 synchronised the host once per sweep, unbounded in the
+// DAG depth).
+constexpr int ISO_LDS = 16384;
+__global__ __launch_bounds__(1024) void k_iso_resolve(int64_t k, const int32_t* npos, const int32_t* iso,
+                                                      const int64_t* isoidx, const int32_t* target, int32_t* active) {
+    __shared__ uint8_t s_act[ISO_LDS], s_hit[ISO_LDS];
+    __shared__ int s_changed;
+    for (int64_t i = threadIdx.x; i < k; i += blockDim.x) s_act[i] = 0;   // all-zero start: the first pass flips all
+    for (int64_t it = 0; it <= k + 1; ++it) {
+        for (int64_t i = threadIdx.x; i < k; i += blockDim.x) s_hit[i] = 0;
+        if (threadIdx.x == 0) s_changed = 0;
+        __syncthreads();
+        if (it > 0)
+            for (int64_t i = threadIdx.x; i < k; i += blockDim.x) {
+                if (!s_act[i]) continue;
+                const int32_t y = target[i];
+                const int64_t j = isoidx[y];
+                if (j >= 0 && npos[y] > npos[iso[i]]) s_hit[j] = 1;
+            }
+        __syncthreads();
+        for (int64_t i = threadIdx.x; i < k; i += blockDim.x) {
+            const uint8_t a = s_hit[i] ? 0 : 1;
+            if (a != s_act[i]) { s_act[i] = a; s_changed = 1; }
+        }
+        __syncthreads();
+        const bool done = !s_changed && it > 0;   // block-uniform
+        __syncthreads();
+        if (done) break;
+    }
+    for (int64_t i = threadIdx.x; i < k; i += blockDim.x) active[i] = s_act[i];
+}
 __global__ void k_iso_flag64(int64_t k, const int32_t* active, int64_t* f) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < k) f[i] = active[i];
@@ -597,15 +629,24 @@ static int64_t repair(Ctx& c, int iteration) {
     int32_t* active = ensure<int32_t>(c.active, k);
     int32_t* hit = ensure<int32_t>(c.hit, k + 1);
     int32_t* changed = hit + k;
-    FC_HIP(hipMemsetAsync(active, 0, sizeof(int32_t) * k, c.stream));  // all-zero start: first pass flips all
-    for (int64_t it = 0; it <= k + 1; ++it) {
-        FC_HIP(hipMemsetAsync(hit, 0, sizeof(int32_t) * (k + 1), c.stream));
-        if (it > 0) k_iso_hit<<<nblk(k), TB, 0, c.stream>>>(k, npos, iso, isoidx, target, active, hit);
-        k_iso_update<<<nblk(k), TB, 0, c.stream>>>(k, hit, active, changed);
-        int32_t ch = 0;
-        FC_HIP(hipMemcpyAsync(&ch, changed, sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
-        sync(c);
-        if (!ch && it > 0) break;
+    if (k <= ISO_LDS) {
+        k_iso_resolve<<<1, 1024, 0, c.stream>>>(k, npos, iso, isoidx, target, active);
+    } else {
+        // many isolates: multi-block Jacobi sweeps, the host checking for a fixpoint every 8
+        FC_HIP(hipMemsetAsync(active, 0, sizeof(int32_t) * k, c.stream));  // all-zero start: first pass flips all
+        for (int64_t it = 0; it <= k + 8; ) {
+            FC_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), c.stream));
+            for (int s = 0; s < 8; ++s, ++it) {
+                FC_HIP(hipMemsetAsync(hit, 0, sizeof(int32_t) * k, c.stream));
+                if (it > 0) k_iso_hit<<<nblk(k), TB, 0, c.stream>>>(k, npos, iso, isoidx, target, active, hit);
+                if (s == 7) FC_HIP(hipMemsetAsync(changed, 0, sizeof(int32_t), c.stream));   // the last sweep decides
+                k_iso_update<<<nblk(k), TB, 0, c.stream>>>(k, hit, active, changed);
+            }
+            int32_t ch = 0;
+            FC_HIP(hipMemcpyAsync(&ch, changed, sizeof(int32_t), hipMemcpyDeviceToHost, c.stream));
+            sync(c);
+            if (!ch) break;
+        }
     }
     int64_t* f = ensure<int64_t>(c.nodetmp, k + 1);   // fl no longer needed
     int64_t* p = ensure<int64_t>(c.nodetmp2, k + 1);

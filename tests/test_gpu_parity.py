@@ -453,3 +453,44 @@ def test_c4_run_properties_full_size(fcmod, lfr1m):
     for row in l1[:4]:
         assert row.min() == 0 and row[0] == 0 and row.max() + 1 == len(np.unique(row))
     assert nmi(planted, l1[0]) > 0.8
+
+
+def test_repair_many_isolates_bit_exact(fcmod):
+    """Isolate repair (fast_consensus.py:193-195) with more isolates than the single-workgroup
+    fixpoint holds (k > 16384: the multi-block Jacobi path) and with few (LDS path): one
+    consensus iteration through the step API on a sparse random graph, device == CPU model
+    (graph, weights, ages)."""
+    from tests.cpu_engine import OracleEngine
+    for N, m in ((60_000, 45_000), (6_000, 4_500)):
+        rng = np.random.default_rng(N)
+        u = rng.integers(0, N, m).astype(np.int32)
+        v = rng.integers(0, N, m).astype(np.int32)
+        lab = rng.integers(0, 3, (4, N)).astype(np.int32)
+        eng = fcmod.Engine(seed=9)
+        eng.set_option("relabel", 0)
+        eng.load_graph(N, u, v)
+        cpu = OracleEngine(seed=9)
+        cpu.load_graph(N, u, v)
+        eng.set_labels(lab)
+        cpu.lab = lab.copy()
+        cpu.r0 = 0
+        part = dev_i32(eng.m)
+        eng.consensus_partial(0, part)
+        eng.consensus_apply(0, 4, 0.8, 0.02, part)
+        cpart = torch.zeros(cpu.m + 1, dtype=torch.int32)
+        cpu.consensus_partial(0, cpart)
+        cpu.consensus_apply(0, 4, 0.8, 0.02, cpart)
+        nc = eng.closure_sample(m, 0)
+        assert nc == cpu.closure_sample(m, 0)
+        cnt = dev_i32(nc)
+        eng.closure_partial(cnt)
+        ccnt = torch.zeros(max(nc, 1), dtype=torch.int32)
+        cpu.closure_partial(ccnt)
+        _, m1 = eng.closure_apply(0, 4, 0.02, cnt, 0)
+        _, cm1 = cpu.closure_apply(0, 4, 0.02, ccnt, 0)
+        assert m1 == cm1
+        deg = np.bincount(np.concatenate([cpu.kept.u, cpu.kept.v]), minlength=N)
+        print("N %d: kept %d, isolated after threshold %d, closure %d, graph %d" % (N, cpu.kept.m, int((deg == 0).sum()), nc, m1))
+        for a, b in zip(eng.get_graph(), cpu.get_graph()):
+            np.testing.assert_array_equal(a, b)
+        eng.close()
