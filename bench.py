@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "consensus wall time + partition·edges/sec, LFR 1M nodes n_p=64, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s peak (spec)
+GATHER_LINE_CEILING_GBS = 7168.0   # measured: 56 G L2-miss requests/s x 128 B (profiles/r02_micro_gather.json)
 
 CONFIGS = {
     # BASELINE.json configs[3] (C4): the metric's workload
@@ -258,6 +259,10 @@ def main():
     else:
         import fastconsensus_amd as fc
         eng = fc.Engine(device=local, seed=args.seed)
+        from fastconsensus_amd.core import store_order_pays
+        from fastconsensus_amd.distributed import shard
+        r0, r1 = shard(cfg["n_p"], rank, world)
+        eng.set_option("store", store_order_pays(r1 - r0))   # --store overrides below
         if args.buckets:
             eng.set_params(buckets=args.buckets)
         for name in ("chunk", "prune", "relabel", "store", "coarsen"):
@@ -346,11 +351,17 @@ def main():
         avg_s = tim["decide_ms"] / launches / 1e3
         bytes_per_launch = tim["decide_bytes"] / launches
         achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        traffic = load_traffic(args.config)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(args.config),
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": "k_decide_light<%s>" % ("true" if algo != 1 else "false"),
                 "launches": tim["decide_launches"], "avg_us": avg_s * 1e6,
-                "algorithmic_bytes_per_launch": bytes_per_launch}
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                # line traffic (PMC, L2 misses x 128 B) per second of decide time, against the
+                # measured ceiling of random 4-B gathers that miss L2 (tools/micro/gather.hip:
+                # ~56 G requests/s x 128 B, whether or not the Infinity Cache holds the line)
+                "traffic_rate_gbs": (traffic / avg_s / 1e9) if (traffic and avg_s > 0) else None,
+                "gather_line_ceiling_gbs": GATHER_LINE_CEILING_GBS}
         phases = {k: tim[k] / args.steps for k in ("cd_ms", "consensus_ms", "closure_ms", "rebuild_ms", "decide_ms")}
 
     if rank == 0:

@@ -311,6 +311,14 @@ def labels_to_output(algorithm, node_labels, labels):
     return out
 
 
+def store_order_pays(replicas):
+    """Label storage order (FC_OPT_STORE) for a GPU that will hold `replicas` replicas: the
+    one-replica ordering pass at load costs ~4 ms on LFR-1M and saves gather misses in
+    proportion to the replicas (measured: n_p=8 61.7 ms without vs 63.0 with, n_p=16 89.0 vs
+    87.0, n_p=64 saves ~20 ms)."""
+    return 1 if replicas >= 12 else 0
+
+
 def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, seed=None, device=0,
                    return_stats=False, rule="fast_consensus"):
     """Drop-in for fast_consensus.py:129 ``fast_consensus(G, algorithm, n_p, thresh, delta)``.
@@ -333,6 +341,7 @@ def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, se
         algo = FC_ALGO_LOUVAIN_NC
     g = G if isinstance(G, IdGraph) else IdGraph.from_networkx(G)
     with Engine(device=device, seed=seed) as eng:
+        eng.set_option("store", store_order_pays(n_p))
         eng.load_graph(g.n, g.u, g.v)
         labels, stats = eng.run(algo, int(n_p), float(thresh), float(delta))
     out = labels_to_output(algorithm, g.labels, labels)
