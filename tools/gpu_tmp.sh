@@ -1,5 +1,6 @@
 set -u
 mkdir -p gpurun_out
-bash tools/pmc_cd.sh r02b_louv fastconsensus_amd/lib/libfastconsensus_amd.so lfr1m 0 || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/stats2_lfr1m -o stats --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/stats2_lfr1m.log 2>&1 || exit $?
-grep '"metric"' gpurun_out/stats2_lfr1m.log | head -c 300
+bash tools/gpu_r2.sh pytest smoke bench1m || exit $?
+timeout -k 10 300 python bench.py --n-p 8 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/np8.out 2> gpurun_out/np8.err || exit $?
+grep -o '"ms_per_step": [0-9.]*' gpurun_out/np8.out
+bash tools/gpu_r2.sh bench100k bench100k_lpm benchsbm
