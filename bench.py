@@ -351,7 +351,7 @@ def main():
         avg_s = tim["decide_ms"] / launches / 1e3
         bytes_per_launch = tim["decide_bytes"] / launches
         achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-        traffic = load_traffic(args.config)
+        traffic = load_traffic(args.config) if args.n_p <= 0 else None   # the PMC summary is for the config's n_p
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": "k_decide_light<%s>" % ("true" if algo != 1 else "false"),

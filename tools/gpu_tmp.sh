@@ -1,6 +1,5 @@
 set -u
 mkdir -p gpurun_out
-bash tools/gpu_r2.sh pytest smoke bench1m || exit $?
-timeout -k 10 300 python bench.py --n-p 8 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/np8.out 2> gpurun_out/np8.err || exit $?
-grep -o '"ms_per_step": [0-9.]*' gpurun_out/np8.out
-bash tools/gpu_r2.sh bench100k bench100k_lpm benchsbm
+timeout -k 10 600 python -u -m pytest -p no:cacheprovider --timeout 300 --timeout-method thread -q -x tests/test_gpu_parity.py -k "twin or heavy or full_run" > gpurun_out/t_ro.log 2>&1; rc=$?; tail -1 gpurun_out/t_ro.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python tools/cd_ab.py --reps 3 old base old base > gpurun_out/ab_ro.out 2>&1; rc=$?
+cat gpurun_out/ab_ro.out; exit $rc
