@@ -15,7 +15,8 @@ FC_ALGO_LOUVAIN = 0
 FC_ALGO_LPM = 1
 FC_ALGO_LOUVAIN_NC = 2   # louvain with new_consensus.py's weight rule (:155-163)
 OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6, "tail_visits": 7,
-           "coarsen": 8, "store": 9, "seed": 10, "closure_rounds": 11}
+           "coarsen": 8, "store": 9, "seed": 10, "closure_rounds": 11,
+           "prune_mark": 12}
 ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 
 # Every symbol declared in include/fastconsensus_amd.h (checked by tests/test_capi_symbols.py)

@@ -132,7 +132,7 @@ void fc_destroy(fc_ctx* ctx) {
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
                       &c.hit, &c.mkey, &c.mkey2, &c.midx, &c.midx2, &c.sort_tmp, &c.nodetmp, &c.nodetmp2,
                       &c.nodetmp3, &c.part, &c.ccount, &c.tailbuf, &c.tailmark, &c.sigma, &c.npos, &c.spos, &c.sinv, &c.tpos, &c.snpos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
-                      &c.st_lab, &c.clo_hkey, &c.clo_hval, &c.clo_list, &c.clo_cnt, &c.clo_akey, &c.clo_aval, &c.clo_rowptr, &c.clo_col, &c.clo_rowptr2, &c.clo_col2, &c.clo_nrow, &c.clo_ncol};
+                      &c.st_lab, &c.clo_hkey, &c.clo_hval, &c.clo_list, &c.clo_cnt, &c.clo_akey, &c.clo_aval, &c.clo_rowptr, &c.clo_col, &c.clo_rowptr2, &c.clo_col2, &c.clo_nrow, &c.clo_ncol, &c.mvf};
     for (auto* b : bufs) b->release();
     for (auto e : c.timer.pool) (void)hipEventDestroy(e);
     for (auto e : c.sweep_ev) (void)hipEventDestroy(e);
@@ -189,6 +189,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
         case FC_OPT_SEED: c.seed = (uint64_t)value; break;
         case FC_OPT_CLOSURE_ROUNDS: FC_REQUIRE(value >= 1, FC_EINVAL, "closure_rounds >= 1"); c.closure_rounds = (int)value; break;
+        case FC_OPT_PRUNE_MARK: FC_REQUIRE(value == 0 || value == 1, FC_EINVAL, "prune_mark must be 0 or 1"); c.prune_mark = (int)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }

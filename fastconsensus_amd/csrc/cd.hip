@@ -111,6 +111,11 @@ struct CDArgs {
                                  // [3n_r..4n_r) transition sweep: decide writes the nlab rows it gathers,
                                  // moves push (every vertex is visited), push mode from the next sweep
     int prune;
+    // Leiden-style marking (FC_OPT_PRUNE_MARK, weighted Louvain graphs): tracking starts at
+    // sweep 1, and a tracked sweep's movers mark, at the sweep's end, only the neighbours
+    // whose label differs from theirs (k_mark_lm); k_apply just flags the movers in mvf
+    int lm;
+    uint8_t* mvf;                // [n_r][N] moved this (tracked) sweep
     const int32_t* list;         // [n_r][PN] vertices to visit, grouped by round (offsets loff)
     const int32_t* loff;         // [n_r][B+1] round offsets into a replica's list
     int B;                       // buckets per sweep
@@ -340,6 +345,9 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
 #pragma unroll
     for (int s = 0; s < WNT; ++s) o[s] = __shfl(ex, s);
     const int E = __shfl(inc, WNT - 1);
+    // loads of 64 entries the wave holds (scalar): every loop over loads / owned slots stops
+    // there instead of walking all 8 with per-lane exec masks (a consensus-graph wave has 3)
+    const int nl = __builtin_amdgcn_readfirstlane((E + 63) >> 6);
     wave_sync();
     PST(1);
     // own labels of the 8 vertices (wave-uniform) and, on lane t, vertex t's own-label weight
@@ -434,6 +442,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     // all labels (LPA)
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
+        if (it >= nl) break;                     // scalar: slots past the wave's loads are empty
         if (rec[it] < 0) continue;
         const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
         const int32_t key = ws.key[sl], val = ws.val[sl];
@@ -467,6 +476,8 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         return max(b1, ws.best2[t]);
     };
     TT tg[8];                                    // gathered Sigma (-1: not evaluated)
+#pragma unroll
+    for (int it = 0; it < 8; ++it) tg[it] = (TT)-1;
     // int32 Sigma (Louvain): among the max-val candidates score = vm*2M - k_v*Sigma, so the
     // best one and its tie key come from ONE packed atomicMin per candidate,
     // (Sigma << 32) | ~hash (smallest Sigma, then largest hash; Sigma taken as 0 when k_v = 0,
@@ -479,7 +490,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         // among the max-val candidates the score is vm*2M - k_v*Sigma: the smallest Sigma wins
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
-            tg[it] = (TT)-1;
+            if (it >= nl) break;
             if (rec[it] < 0) continue;
             const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
             if (ws.val[sl] == ws.vm[t]) tg[it] = totr[ws.key[sl]];
@@ -487,6 +498,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         if constexpr (PK) {
 #pragma unroll
             for (int it = 0; it < 8; ++it) {
+                if (it >= nl) break;
                 if (tg[it] < 0) continue;
                 ++ncand;
                 const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
@@ -502,14 +514,17 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             wave_sync();
         } else {
 #pragma unroll
-            for (int it = 0; it < 8; ++it)
+            for (int it = 0; it < 8; ++it) {
+                if (it >= nl) break;
                 if (tg[it] >= 0) { ++ncand; atomicMin(&ws.tmin[rec[it] >> 8], (long long)tg[it]); }
+            }
             wave_sync();
         }
         // a lower val whose bound val*2M still reaches that score (rare: k_v*Sigma >= 2M)
         bool need = false;
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
+            if (it >= nl) break;
             if (rec[it] < 0 || tg[it] >= 0) continue;
             const int t = rec[it] >> 8;
             const long long b1 = PK ? ws.b1[t] : score(ws.vm[t], ws.tmin[t], ws.kv[t]);
@@ -519,6 +534,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             slow = true;
 #pragma unroll
             for (int it = 0; it < 8; ++it) {
+                if (it >= nl) break;
                 if (rec[it] < 0 || tg[it] >= 0) continue;
                 const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
                 const int32_t val = ws.val[sl];
@@ -532,7 +548,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     } else {
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
-            tg[it] = (TT)-1;
+            if (it >= nl) break;
             if (rec[it] >= 0) { tg[it] = 0; ++ncand; }
         }
     }
@@ -541,6 +557,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     if (slow) {                                  // wave-uniform
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
+            if (it >= nl) break;
             if (tg[it] < 0) continue;
             const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
             const int32_t key = ws.key[sl], val = ws.val[sl];
@@ -580,7 +597,8 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
 }
 
 template <bool LOUV, typename TT>
-__global__ __launch_bounds__(DTB) void k_decide_light(CDArgs a, int bucket, int sweep, int X) {
+__global__ __launch_bounds__(DTB) __attribute__((amdgpu_waves_per_eu(8))) void k_decide_light(CDArgs a, int bucket, int sweep,
+                                                                                         int X) {
     __shared__ WaveShared s_ws[DTB / 64];
     __shared__ unsigned long long s_red[2][DTB / 64][5];   // by item parity (no second barrier)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -783,10 +801,15 @@ __global__ __launch_bounds__(ATB) void k_apply(CDArgs a, int bucket) {
     const int4* decr = a.dec + (int64_t)r * a.dstride;
     const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
     int moved = 0;
-    if (!push && !trk) {
+    if (!push && (!trk || a.lm)) {               // lm: a tracked move only flags the mover
+        uint8_t* mv = a.mvf + (int64_t)r * a.N;
         for (int64_t di = (int64_t)blockIdx.x * ATB + threadIdx.x; di < len; di += (int64_t)gridDim.x * ATB) {
             const int4 dv = decr[di];
-            if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]); ++moved; }
+            if (dv.x >= 0) {
+                apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]);
+                ++moved;
+                if (trk) mv[dv.y] = 1;
+            }
         }
     } else {
         const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
@@ -819,6 +842,27 @@ __global__ __launch_bounds__(ATB) void k_apply(CDArgs a, int bucket) {
     if (threadIdx.x == 0 && s_mv) atomicAdd(red_slot(a, r, 2), (unsigned long long)s_mv);
 }
 
+// End of a tracked sweep in lm mode: each mover v marks the neighbours whose label now
+// differs from v's (Traag et al.'s fast local moving rule: a neighbour that ended in v's
+// community is not revisited), comparing the labels the sweep left -- deterministic, unlike a
+// mark at move time, which would race with the round's other moves.
+__global__ __launch_bounds__(256) void k_mark_lm(CDArgs a) {
+    const int r = blockIdx.y;
+    if (!a.active[r] || !a.track[r]) return;     // block-uniform: this sweep was not tracked
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.N) return;
+    uint8_t* mv = a.mvf + (int64_t)r * a.N;
+    if (!mv[v]) return;
+    mv[v] = 0;
+    const int32_t* labr = a.lab + (int64_t)r * a.N;
+    uint8_t* aff = a.aff + (int64_t)r * a.N;
+    const int4 vr = a.vrec[v];
+    const int32_t d = labr[vr.w];
+    const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
+    for (int64_t j = rb; j < re; ++j)
+        if (labr[a.colp[j]] != d) aff[a.col[j]] = 1;
+}
+
 // End of sweep: python-louvain stops a level when the pass gained < 1e-7 modularity or
 // moved nothing; igraph LPA stops when no visited vertex was unstable.
 template <bool LOUV>
@@ -837,7 +881,7 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         atomicAdd(&vis, f[3]);
         if (a.prune) {   // lists filter next sweep iff moves were tracked this sweep
             a.track[a.n_r + r] = a.track[r];
-            if (f[2] * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
+            if (a.lm || f[2] * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
         }
         // pull -> push once a sweep moved < N/4 vertices (push pays d writes per MOVE,
         // pull d gathers per VISIT), through one transition sweep that builds nlab
@@ -902,7 +946,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
     __shared__ WaveShared s_ws[NTH / 64];
     __shared__ HeavyShared<NTH> sh;
     __shared__ int s_off[TAIL_MAXB + 1], s_cur[TAIL_MAXB];
-    __shared__ int s_n, s_nnext, s_nheavy, s_stop;
+    __shared__ int s_n, s_nnext, s_nheavy, s_stop, s_nmv;
     __shared__ unsigned long long s_acc[6];   // dq, unstable, moves, verts, entries, cands
     const int r = blockIdx.x;
     if (!a.active[r]) return;                 // block-uniform
@@ -929,7 +973,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         const int32_t stamp = sweep + 1;
         for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
         if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
-        if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; s_nheavy = 0; }
+        if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; s_nheavy = 0; s_nmv = 0; }
         __syncthreads();
         const int n = s_n;
         const int32_t* blp = bl;
@@ -1000,10 +1044,15 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             if (threadIdx.x == 0) s_nheavy = 0;   // read above; next bucket's decide appends after the barrier below
             // apply the bucket's moves; while tracking, neighbours join the next worklist
             int moved = 0;
-            if (!push && !trk) {
+            if (!push && (!trk || a.lm)) {       // lm: a tracked move joins the sweep's mover list
                 for (int64_t di = threadIdx.x; di < nk; di += NTH) {
                     const int4 dv = decr[di];
-                    if (dv.x >= 0) { apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]); ++moved; }
+                    if (dv.x >= 0) {
+                        apply_move<LOUV, TT>(a, r, dv, a.spos[dv.y]);
+                        ++moved;
+                        // wl (this sweep's unbucketed worklist) is free once bucketed
+                        if (trk) wl[atomicAdd(&s_nmv, 1)] = dv.y;
+                    }
                 }
             } else {
                 const int t16 = threadIdx.x / TILE, l16 = threadIdx.x % TILE;
@@ -1027,6 +1076,22 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             if (moved) atomicAdd(&s_acc[2], (unsigned long long)moved);
             __syncthreads();
         }
+        if (trk && a.lm) {                       // block-uniform: k_mark_lm for this replica
+            const int t16 = threadIdx.x / TILE, l16 = threadIdx.x % TILE;
+            const int32_t* labr = a.lab + (int64_t)r * a.N;
+            const int nmv = s_nmv;
+            for (int i = t16; i < nmv; i += NTH / TILE) {
+                const int4 vr = a.vrec[wl[i]];
+                const int32_t d = labr[vr.w];
+                const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
+                for (int64_t j = rb + l16; j < re; j += TILE) {
+                    if (labr[a.colp[j]] == d) continue;
+                    const int32_t u = a.col[j];
+                    if (atomicMax(&mark[u], stamp) < stamp) wl2[atomicAdd(&s_nnext, 1)] = u;
+                }
+            }
+            __syncthreads();
+        }
         // end of sweep: the same bookkeeping as k_sweep_end, for this replica
         if (threadIdx.x == 0) {
             const unsigned long long moves = s_acc[2];
@@ -1034,7 +1099,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             atomicAdd((unsigned long long*)(n_active_out + 4), 1ull);
             if (a.prune) {
                 a.track[a.n_r + r] = a.track[r];
-                if (moves * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
+                if (a.lm || moves * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
             }
             if (a.track[3 * a.n_r + r]) { a.track[3 * a.n_r + r] = 0; a.track[2 * a.n_r + r] = 1; }
             else if (a.push_div && !a.track[2 * a.n_r + r] && !a.track[a.n_r + r] &&
@@ -1305,6 +1370,17 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // faster (LFR-1M weighted CD batch 46.1 vs 47.1 ms; input graph 125.7 vs 129.6 with push);
     // the mode never changes a decision
     a.push_div = (louv && g.max_w > 1) ? 0 : c.push_div;
+    // Leiden-style marking on weighted Louvain graphs (the consensus graphs; pull-only above):
+    // after the first sweep few vertices move, and nearly all the later movers have a
+    // neighbour that ended in another community (LFR-100k consensus graph: 1.5 % of the
+    // vertices marked after sweep 1, covering 99.6-100 % of sweep 2's movers, against 85 %
+    // marked by "every neighbour of a mover")
+    a.lm = (louv && g.max_w > 1 && c.prune && c.prune_mark == 1) ? 1 : 0;
+    a.mvf = nullptr;
+    if (a.lm) {
+        a.mvf = ensure<uint8_t>(c.mvf, (size_t)rcount * N);
+        FC_HIP(hipMemsetAsync(a.mvf, 0, (size_t)rcount * N, c.stream));
+    }
     a.unitw = (!louv || (g.max_w == 1 && g.M2 == 2 * g.m)) ? 1 : 0;
     a.wbits = 1;
     if (louv) while (a.wbits < 31 && (g.max_w >> a.wbits) != 0) ++a.wbits;
@@ -1355,6 +1431,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
             else if (tot32) sub_round<true, int32_t>(c, a, k, sweep, hv, X);
             else sub_round<true, int64_t>(c, a, k, sweep, hv, X);
         }
+        if (a.lm) k_mark_lm<<<ig, TB, 0, c.stream>>>(a);
         if (louv) k_sweep_end<true><<<1, TB, 0, c.stream>>>(a, n_active);
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
         if (c.trace) {

@@ -106,6 +106,7 @@ struct Ctx {
     DevBuf lab, tot, dec, labT;     // int32 [n_r][N], int64 [n_r][N], int32 [n_r][S], int32 [N][ldT]
     DevBuf nlab;                    // int32 [n_r][2m]: label of each adjacency entry's neighbour
     DevBuf aff, vlist, vcnt, track; // pruning: affected flags, per-sweep visit lists, list lengths, modes
+    DevBuf mvf;                     // movers of a tracked sweep (prune_mark = 1 on weighted Louvain graphs)
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable
@@ -131,6 +132,7 @@ struct Ctx {
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
     int closure_rounds = 8;         // FC_OPT_CLOSURE_ROUNDS
+    int prune_mark = 1;             // FC_OPT_PRUNE_MARK: 1 Leiden-style marks on weighted Louvain graphs, 0 every neighbour
     DevBuf sort_tmp;                // hipcub temporary storage
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)

@@ -528,7 +528,7 @@ static int tw_coarse(i64 N, i64 V, int B, int gmax) {
 
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
                       u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
-                      int coarsen, i32* lab) {
+                      int coarsen, int lm, i32* lab) {
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
@@ -542,6 +542,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     const i64 S = chunk ? ((NC + B - 1) / B) * chunk : (N + B - 1) / B;
     i32* dec = (i32*)malloc(sizeof(i32) * (size_t)(PN + 1));
     u8* aff = (u8*)calloc((size_t)N, 1);
+    u8* mvf = lm ? (u8*)calloc((size_t)N, 1) : NULL;   /* movers of a tracked sweep (lm) */
     i64* lists = (i64*)malloc(sizeof(i64) * (size_t)(PN + 1));   /* per-bucket visit lists */
     i64* loff = (i64*)malloc(sizeof(i64) * (size_t)(B + 1));
     for (i64 v = 0; v < N; ++v) { lab[v] = (i32)v; tot[v] = kdeg[v]; csz[v] = 1; }
@@ -627,19 +628,29 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
                 const i32 old = lab[v], nw = dec[e];
                 lab[v] = nw;
                 if (louv) { tot[old] -= kdeg[v]; tot[nw] += kdeg[v]; csz[old]--; csz[nw]++; }
-                if (track_now)
+                if (track_now && lm) mvf[v] = 1;
+                else if (track_now)
                     for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) aff[col[j]] = 1;
                 ++moves;
             }
         }
+        /* lm (engine k_mark_lm): at the end of a tracked sweep each mover marks the neighbours
+         * whose label differs from its own, as the sweep left them */
+        if (track_now && lm)
+            for (i64 v = 0; v < N; ++v) {
+                if (!mvf[v]) continue;
+                mvf[v] = 0;
+                for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j)
+                    if (lab[col[j]] != lab[v]) aff[col[j]] = 1;
+            }
         if (prune) {
             prune_now = track_now;
-            if (moves * 4 < (unsigned long long)N) track_now = 1;
+            if (lm || moves * 4 < (unsigned long long)N) track_now = 1;
         }
         if (louv) { if (moves == 0 || ((double)dq / 1099511627776.0) < 1e-7) active = 0; }
         else if (unstable == 0) active = 0;
     }
-    free(tot); free(csz); free(acc); free(seen); free(keys); free(dec); free(aff); free(lists); free(loff);
+    free(tot); free(csz); free(acc); free(seen); free(keys); free(dec); free(aff); free(mvf); free(lists); free(loff);
     return sweep;
 }
 
@@ -647,19 +658,22 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
  * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
 void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
                    int iteration, u64 seed, int buckets, int max_sweeps, int chunk, int prune, int coarsen,
-                   i32* lab, int* sweeps) {
+                   int prune_mark, i32* lab, int* sweeps) {
     i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
     i64 M2 = 0;
+    i32 max_w = 0;
     for (i64 v = 0; v < N; ++v) {
         i64 s = 0;
-        for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) s += cw[j];
+        for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) { s += cw[j]; if (cw[j] > max_w) max_w = cw[j]; }
         kdeg[v] = s;
         M2 += s;
     }
+    /* engine cd_run: Leiden-style marks on weighted Louvain graphs */
+    const int lm = algo == 0 && max_w > 1 && prune && prune_mark == 1;
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
-                            buckets, max_sweeps, chunk, prune, coarsen, lab + (i64)r * N);
+                            buckets, max_sweeps, chunk, prune, coarsen, lm, lab + (i64)r * N);
         if (sweeps) sweeps[r] = sw;
     }
     free(kdeg);

@@ -12,13 +12,14 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8):
+    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1):
         """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity."""
         self.seed = int(seed)
         self.buckets = buckets
         self.chunk = chunk
         self.prune = prune
         self.coarsen = coarsen
+        self.prune_mark = prune_mark
         self.sigma = None if sigma is None else np.asarray(sigma, np.int32)
         self.lab = None
 
@@ -50,7 +51,8 @@ class OracleEngine:
     # steps -----------------------------------------------------------------------------
     def cd(self, algo, r0, count, n_p, iteration):
         self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
-                                    chunk=self.chunk, prune=self.prune, coarsen=self.coarsen)
+                                    chunk=self.chunk, prune=self.prune, coarsen=self.coarsen,
+                                    prune_mark=self.prune_mark)
         self.r0 = r0
 
     def consensus_partial(self, algo, out):

@@ -65,7 +65,7 @@ def test_cpu_twin_defaults_match_engine_defaults():
     from oracle import oracle as orc
     from tests.cpu_engine import OracleEngine
     src = open(os.path.join(ROOT, "fastconsensus_amd", "csrc", "fc_ctx.h")).read()
-    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen")}
+    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen", "prune_mark")}
     twin = inspect.signature(orc.engine_cd).parameters
     model = inspect.signature(OracleEngine.__init__).parameters
     for k, v in eng.items():

@@ -223,6 +223,51 @@ def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune, tail):
     eng.close()
 
 
+def _weighted_consensus_engine(fcmod, seed):
+    """An engine holding a weighted consensus graph (weights 0..n_p): one louvain iteration of
+    the step API on LFR-1k with the reference run's recorded labelings and closure pairs."""
+    case = golden_io.load("lfr1k_louvain_np20")
+    eng = fcmod.Engine(seed=seed)
+    e = case.edges_file
+    eng.load_graph(case.N, e[:, 0], e[:, 1])
+    eng.set_labels(case.cd_batches[0])
+    part = dev_i32(eng.m)
+    eng.consensus_partial(0, part)
+    eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)
+    nc = eng.closure_set_pairs(case.pair_batches[0], 0)
+    cnt = dev_i32(nc)
+    eng.closure_partial(cnt)
+    eng.closure_apply(0, case.n_p, case.delta, cnt, 0)
+    return case, eng
+
+
+@pytest.mark.parametrize("coarsen", [0, 8])
+@pytest.mark.parametrize("tail", TAILS)
+@pytest.mark.parametrize("prune_mark", [0, 1])
+def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, prune_mark, tail, coarsen):
+    """CD on a weighted consensus graph, where FC_OPT_PRUNE_MARK=1 (default) tracks from sweep 1
+    and marks at sweep end only the neighbours that ended in another community (k_mark_lm, and
+    the tail kernel's mover list): bit-exact against the twin in both modes, on the multi-kernel
+    path and the tail kernel, with and without coarse rounds."""
+    case, eng = _weighted_consensus_engine(fcmod, 31)
+    eng.set_option("prune_mark", prune_mark)
+    eng.set_option("tail_visits", tail)
+    eng.set_option("coarsen", coarsen)
+    u, v, w, _ = eng.get_graph()
+    assert w.max() > 1
+    sigma = eng.node_map()
+    a, b = sigma[u], sigma[v]
+    lo, hi = np.minimum(a, b), np.maximum(a, b)
+    o = np.lexsort((hi, lo))
+    g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
+    n_r = 6
+    eng.cd(0, 0, n_r, n_r, 3)
+    got = eng.get_labels(n_r)
+    exp, _ = orc.engine_cd(0, g_int, n_r, 0, 3, 31, coarsen=coarsen, prune_mark=prune_mark)
+    np.testing.assert_array_equal(got, exp[:, sigma])
+    eng.close()
+
+
 def test_louvain_quality_vs_sequential_restatement(fcmod):
     """Statistical parity of Louvain level 0: modularity and NMI within tolerance of the
     python-louvain restatement (tolerances: dQ 0.01 on the mean, NMI 0.03)."""

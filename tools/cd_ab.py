@@ -31,6 +31,10 @@ def child(lib, config, algo, reps):
     n_p = cfg["n_p"]
     out = {"lib": lib}
     with fc.Engine(seed=42) as eng:
+        # FC_AB_OPTS="name=value;...": engine options of this variant (fc_set_option)
+        for kv in filter(None, os.environ.get("FC_AB_OPTS", "").split(";")):
+            k, _, val = kv.partition("=")
+            eng.set_option(k, int(val))
         loads = []
         for _ in range(3):
             t0 = time.perf_counter()
