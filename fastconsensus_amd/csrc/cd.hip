@@ -1370,12 +1370,14 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // faster (LFR-1M weighted CD batch 46.1 vs 47.1 ms; input graph 125.7 vs 129.6 with push);
     // the mode never changes a decision
     a.push_div = (louv && g.max_w > 1) ? 0 : c.push_div;
-    // Leiden-style marking on weighted Louvain graphs (the consensus graphs; pull-only above):
-    // after the first sweep few vertices move, and nearly all the later movers have a
-    // neighbour that ended in another community (LFR-100k consensus graph: 1.5 % of the
-    // vertices marked after sweep 1, covering 99.6-100 % of sweep 2's movers, against 85 %
-    // marked by "every neighbour of a mover")
-    a.lm = (louv && g.max_w > 1 && c.prune && c.prune_mark == 1) ? 1 : 0;
+    // Leiden-style marking on consensus graphs (weights > 1; LPA ignores them but runs on the
+    // same strongly clustered graph): after the first sweep few vertices move, and nearly all
+    // the later movers have a neighbour that ended in another community (LFR-100k consensus
+    // graph: 1.5 % of the vertices marked after sweep 1, covering 99.6-100 % of sweep 2's
+    // movers, against 85 % marked by "every neighbour of a mover").  Sweep 2 is already
+    // filtered, so no unfiltered sweep is left for the pull -> push transition: lm is pull-only.
+    a.lm = (g.max_w > 1 && c.prune && c.prune_mark == 1) ? 1 : 0;
+    if (a.lm) a.push_div = 0;
     a.mvf = nullptr;
     if (a.lm) {
         a.mvf = ensure<uint8_t>(c.mvf, (size_t)rcount * N);

@@ -110,12 +110,12 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 from the post-threshold graph plus the earlier blocks' closure edges.
                                 1 = every attempt from the post-threshold graph only.             */
 #define FC_OPT_PRUNE_MARK 12 /* which neighbours a tracked move marks for the next (filtered) sweep.
-                                1 (default): on weighted Louvain graphs (the consensus graphs)
+                                1 (default): on consensus graphs (weights > 1; Louvain and LPA)
                                 tracking starts at sweep 1 and, at each tracked sweep's end, a
                                 mover marks only the neighbours whose label differs from its own
-                                (fast local moving, Traag et al. 2019); unit-weight graphs and LPA
-                                keep 0.  0: every neighbour of a mover, tracking from the first
-                                sweep that moves < n/4 vertices.                                  */
+                                (fast local moving, Traag et al. 2019); unit-weight graphs keep
+                                0.  0: every neighbour of a mover, tracking from the first sweep
+                                that moves < n/4 vertices.                                       */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

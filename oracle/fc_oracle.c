@@ -668,8 +668,9 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
         kdeg[v] = s;
         M2 += s;
     }
-    /* engine cd_run: Leiden-style marks on weighted Louvain graphs */
-    const int lm = algo == 0 && max_w > 1 && prune && prune_mark == 1;
+    /* engine cd_run: Leiden-style marks on consensus graphs (weights > 1; LPA too) */
+    const int lm = max_w > 1 && prune && prune_mark == 1;
+    (void)algo;
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,

@@ -244,8 +244,9 @@ def _weighted_consensus_engine(fcmod, seed):
 @pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("prune_mark", [0, 1])
-def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, prune_mark, tail, coarsen):
-    """CD on a weighted consensus graph, where FC_OPT_PRUNE_MARK=1 (default) tracks from sweep 1
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, algo, prune_mark, tail, coarsen):
+    """CD (Louvain and LPA) on a weighted consensus graph, where FC_OPT_PRUNE_MARK=1 (default) tracks from sweep 1
     and marks at sweep end only the neighbours that ended in another community (k_mark_lm, and
     the tail kernel's mover list): bit-exact against the twin in both modes, on the multi-kernel
     path and the tail kernel, with and without coarse rounds."""
@@ -261,9 +262,9 @@ def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, prune_mark, tail, coars
     o = np.lexsort((hi, lo))
     g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
     n_r = 6
-    eng.cd(0, 0, n_r, n_r, 3)
+    eng.cd(algo, 0, n_r, n_r, 3)
     got = eng.get_labels(n_r)
-    exp, _ = orc.engine_cd(0, g_int, n_r, 0, 3, 31, coarsen=coarsen, prune_mark=prune_mark)
+    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 31, coarsen=coarsen, prune_mark=prune_mark)
     np.testing.assert_array_equal(got, exp[:, sigma])
     eng.close()
 
