@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("FC_LIB_PATH") or os.path.join(PKG, "lib", "libfastcon
 FC_ALGO_LOUVAIN = 0
 FC_ALGO_LPM = 1
 FC_ALGO_LOUVAIN_NC = 2   # louvain with new_consensus.py's weight rule (:155-163)
+FC_ALGO_LEIDEN = 3       # leiden branch (:204-258, final pass :385-388)
 OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6, "tail_visits": 7,
            "coarsen": 8, "store": 9, "seed": 10, "closure_rounds": 11,
            "prune_mark": 12}

@@ -11,7 +11,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 OUT_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(OUT_DIR, "libfastconsensus_amd.so")
-SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "capi.cpp", "gen.cpp"]
+SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "leiden.hip", "capi.cpp", "gen.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",

@@ -72,6 +72,10 @@ def write_outputs(args, output, root='.'):
             output[i] = part.values()
     for i, partition in enumerate(output, start=1):
         with open(out_dir + '/' + str(i), 'w') as f:
+            if args.alg == 'leiden':   # :463-466 rewrites the file as vertex -> cluster, 1-based
+                for j, mem in enumerate(partition.membership):
+                    f.write(str(j + 1) + "\t" + str(mem[0] + 1) + '\n')
+                continue
             for community in partition:
                 print(*community, file=f)
 

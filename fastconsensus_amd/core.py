@@ -8,13 +8,14 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import FC_ALGO_LOUVAIN, FC_ALGO_LOUVAIN_NC, FC_ALGO_LPM, FastConsensusError, Stats, check, ptr
+from ._lib import (FC_ALGO_LEIDEN, FC_ALGO_LOUVAIN, FC_ALGO_LOUVAIN_NC, FC_ALGO_LPM, FastConsensusError, Stats,
+                   check, ptr)
 
-ALGORITHMS = {"louvain": FC_ALGO_LOUVAIN, "lpm": FC_ALGO_LPM}
+ALGORITHMS = {"louvain": FC_ALGO_LOUVAIN, "lpm": FC_ALGO_LPM, "leiden": FC_ALGO_LEIDEN}
 # consensus weight rules: fast_consensus.py (the named entry point) or the new_consensus.py
 # fork's plain count that keeps converged edges (:155-163); louvain only
 RULES = ("fast_consensus", "new_consensus")
-OUT_OF_SCOPE = ("infomap", "leiden", "cnm")
+OUT_OF_SCOPE = ("infomap", "cnm")
 FINAL_PASS_ITER = 0x40000000  # iteration salt of the final pass (matches capi.cpp fc_run)
 
 
@@ -27,7 +28,7 @@ def algo_id(algorithm):
     if algorithm in ALGORITHMS:
         return ALGORITHMS[algorithm]
     if algorithm in OUT_OF_SCOPE:
-        raise NotImplementedError("algorithm %r is outside this engine's scope (louvain and lpm only)"
+        raise NotImplementedError("algorithm %r is outside this engine's scope (louvain, lpm and leiden only)"
                                   % algorithm)
     return None
 
@@ -294,12 +295,60 @@ class IdGraph:
         return IdGraph(labels, u, v)
 
 
+class Cover:
+    """What ``leidenalg.find_partition(...).as_cover()`` returns (fast_consensus.py:123), as far
+    as the reference uses it: iterating yields the clusters (lists of igraph vertex ids,
+    ascending), ``membership[j]`` is ``[cluster of vertex j]`` (:465-466) and ``len`` is the
+    number of clusters.  igraph vertex j is the j-th smallest node label (``nx_to_igraph``
+    adds ``sorted(G.nodes())``, :47).  Clusters are numbered by decreasing size, as leidenalg
+    renumbers its communities (ties: the cluster holding the smaller vertex first)."""
+
+    def __init__(self, vertex_labels):
+        lab = np.asarray(vertex_labels)
+        k = int(lab.max()) + 1 if lab.size else 0
+        sizes = np.bincount(lab, minlength=k)
+        first = np.full(k, lab.size, np.int64)
+        np.minimum.at(first, lab, np.arange(lab.size))
+        order = np.lexsort((first, -sizes))
+        rank = np.empty(k, np.int64)
+        rank[order] = np.arange(k)
+        self._m = rank[lab] if lab.size else lab.astype(np.int64)
+        self._k = k
+
+    def __len__(self):
+        return self._k
+
+    def __iter__(self):
+        idx = np.argsort(self._m, kind="stable")
+        bounds = np.searchsorted(self._m[idx], np.arange(self._k + 1))
+        for c in range(self._k):
+            yield idx[bounds[c]:bounds[c + 1]].tolist()
+
+    def __getitem__(self, c):
+        return np.flatnonzero(self._m == c).tolist()
+
+    @property
+    def membership(self):
+        return [[int(c)] for c in self._m]
+
+    def sizes(self):
+        return np.bincount(self._m, minlength=self._k).tolist()
+
+
 def labels_to_output(algorithm, node_labels, labels):
     """Engine labelings [n_p][N] -> the reference's return type (fast_consensus.py:383-392):
     louvain: list of dict node -> community (insertion order = node order, as
-    python-louvain builds it); lpm: list of set of frozenset of nodes."""
+    python-louvain builds it); lpm: list of set of frozenset of nodes; leiden: list of
+    ``Cover`` (igraph vertex ids, :385-388)."""
     out = []
     nodes = list(node_labels.tolist())
+    if algorithm == "leiden":
+        vid = np.argsort(np.argsort(np.asarray(node_labels), kind="stable"), kind="stable")   # node -> vertex id
+        for lab in labels:
+            vl = np.empty(len(lab), np.int64)
+            vl[vid] = lab
+            out.append(Cover(vl))
+        return out
     for lab in labels:
         if algorithm == "louvain":
             out.append(dict(zip(nodes, lab.tolist())))
@@ -325,7 +374,8 @@ def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, se
 
     G: an undirected networkx Graph (weights are ignored: the reference resets them to 1,
     :135-136) or an ``IdGraph``.  Returns a list of n_p partitions -- dicts for louvain,
-    sets of frozensets for lpm -- or None for an unknown algorithm (the reference's loop
+    sets of frozensets for lpm, ``Cover`` objects for leiden -- or None for an unknown
+    algorithm (the reference's loop
     ``break``s and returns None, :380-381).  ``seed`` makes the run reproducible (the
     reference is unseeded).  ``rule="new_consensus"`` (louvain only) switches to the
     new_consensus.py fork's weight rule (:155-163).

@@ -252,8 +252,10 @@ int fc_get_nextgraph(fc_ctx* ctx, int64_t* m_out, int32_t* u, int32_t* v, int32_
 int fc_cd(fc_ctx* ctx, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM, FC_EINVAL, "algo must be louvain or lpm");
-    cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
+    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM || algo == FC_ALGO_LEIDEN, FC_EINVAL,
+               "algo must be louvain, lpm or leiden");
+    if (algo == FC_ALGO_LEIDEN) leiden_run(c, rbegin, rcount, n_p_total, iteration);
+    else cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
     FC_API_END
 }
 
@@ -373,8 +375,8 @@ int fc_collect_timing(fc_ctx* ctx, fc_stats* st) {
 int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* labels_out, fc_stats* st) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM, FC_EINVAL,
-               "algorithm must be louvain or lpm (infomap/leiden/cnm are out of scope)");
+    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM || algo == FC_ALGO_LEIDEN, FC_EINVAL,
+               "algorithm must be louvain, lpm or leiden (infomap/cnm are out of scope)");
     FC_REQUIRE(n_p >= 1, FC_EINVAL, "n_p must be >= 1");
     FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
     const bool louv = is_louvain(algo);
@@ -382,6 +384,23 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
     c.acc = fc_stats{};
     fc_stats& a = c.acc;
     a.n_p = n_p;
+    if (algo == FC_ALGO_LEIDEN) {
+        // fast_consensus.py:204-258 on integer node ids: communities_to_dict keys vertices by
+        // str(index) (:97), `node in node_community_lookup` is False for every int node (:217),
+        // so nextgraph keeps weight 0 everywhere, :223-227 removes every edge and check #1
+        // (:229) sees an empty graph (count 0 > delta*0 is false): converged after one
+        // iteration whose CD batch cannot reach the result.  Final pass (:385-388): n_p
+        // Leiden runs on `graph` = G with unit weights.
+        a.iterations = 1;
+        a.exit_check = 1;
+        leiden_run(c, 0, n_p, n_p, 0x40000000);
+        a.partition_edges += (int64_t)n_p * c.g.m;
+        a.m_final = c.g.m;
+        if (labels_out) labels_to_host(c, labels_out, true);
+        sync(c);
+        if (st) *st = a;
+        return FC_OK;
+    }
     int it = 0;
     for (;;) {
         if (it >= c.max_iters) { a.hit_iter_cap = 1; break; }

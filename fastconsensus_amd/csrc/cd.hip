@@ -131,6 +131,8 @@ struct CDArgs {
     int32_t* heavy_scratch;      // global tables when rows exceed the LDS table
     int64_t heavy_slots;         // slots per global table (power of 2)
     unsigned long long* sacc;    // [n_r][4] light-kernel vertices / entries / candidates, summed by k_sweep_end
+    double min_dq;               // Louvain stop: a sweep gaining < min_dq (python-louvain __MIN 1e-7; Leiden's
+                                 // move phase 0: run until a sweep moves nothing)
 };
 
 // Sweep order of replica rg: a random permutation of the vertices, or of chunks of CHUNK
@@ -894,7 +896,7 @@ __global__ void k_sweep_end(CDArgs a, int32_t* n_active_out) {
         if (a.active[r]) {
             atomicAdd(&cnt0, 1);
             bool stop;
-            if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < 1e-7;
+            if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < a.min_dq;
             else stop = f[1] == 0;
             if (stop) a.active[r] = 0;
             else atomicAdd(&cnt, 1);
@@ -1106,7 +1108,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                      moves * (unsigned long long)a.push_div < (unsigned long long)a.N)
                 a.track[3 * a.n_r + r] = 1;
             bool stop;
-            if (LOUV) stop = moves == 0 || ((double)s_acc[0] / DQ_SCALE) < 1e-7;
+            if (LOUV) stop = moves == 0 || ((double)s_acc[0] / DQ_SCALE) < a.min_dq;
             else stop = s_acc[1] == 0;
             if (stop) { a.active[r] = 0; s_stop = 1; }
             s_n = s_nnext;
@@ -1362,6 +1364,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.lab = lab; a.tot = tot; a.dec = dec; a.active = active;
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
+    a.min_dq = c.cd_min_dq;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
     a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
     a.hcap = std::max<int64_t>(n_heavy, 1);

@@ -149,6 +149,8 @@ struct Ctx {
     int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 4;   // sweeps of that pass
     DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
     int coarsen = 8;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
+    double cd_min_dq = 1e-7;        // Louvain sweeps stop below this predicted gain (Leiden's move phase: 0)
+    DevBuf lv[48];                  // Leiden level state (leiden.hip)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     // CD kernel variant that leaves every decision unchanged (A/B switch, default on):
     // own-label entries summed in registers (ballots / wave scan) instead of the LDS table
@@ -179,6 +181,8 @@ void labels_to_host(Ctx& c, int32_t* out, bool renumber);   // node order [n_r][
 void labels_from_host(Ctx& c, int count, const int32_t* in);
 void graph_to_host(Ctx& c, int64_t m, const int32_t* u, const int32_t* v, const int32_t* w, const int64_t* age,
                    int32_t* ou, int32_t* ov, int32_t* ow, int64_t* oage);
+// leiden.hip: replica-batched Leiden (leidenalg ModularityVertexPartition, n_iterations=1)
+void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration);
 // consensus.cpp
 void consensus_partial(Ctx& c, int algo, int32_t* out);
 void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept,

@@ -1,0 +1,862 @@
+// leiden.hip -- replica-batched Leiden on MI355X: the community detection of the reference's
+// `leiden` branch, leidenalg.find_partition(graph, ModularityVertexPartition, weights='weight',
+// seed=i, n_iterations=1) (fast_consensus.py:121-123, called n_p times at :210-211 and :386-387).
+//
+// leidenalg (not vendored, not installed; restated from its published algorithm, Traag,
+// Waltman & van Eck 2019, and the package's documented defaults -- parity unpinned, see
+// oracle/fc_oracle.c orc_leiden) optimises one level at a time:
+//   1. move nodes: a queue of every node in random order; a node moves to the neighbour (or
+//      empty) community of largest modularity gain if that gain is positive, and its
+//      neighbours outside the new community re-enter the queue;
+//   2. refine: every node starts alone; in random order, a node that is still alone joins the
+//      best (gain > 0) refined community among its neighbours inside its own step-1 community;
+//   3. aggregate the graph by the refined communities, each aggregate node starting in the
+//      step-1 community of its members; repeat from 1 while the refinement merged anything.
+//
+// MI355X layout.  All replicas of a level live in ONE union graph: replica r's aggregate
+// nodes occupy a contiguous id range, so one launch serves every replica, and the replicas
+// share 2M (aggregation preserves the total weight).  Level 0 is the input graph itself,
+// addressed implicitly (union vertex x = r*N + v, row of v), and its move phase is the
+// replica-batched Louvain local-moving engine (cd.hip) run to exhaustion (no 1e-7 cut).
+// Levels >= 1 are explicit CSRs built here with LDS hash tables (global tables for long
+// rows).  A sweep is B buckets: bucket(x) = hash(replica stream key, local id) mod B; a
+// bucket's vertices decide against the state left by the earlier buckets, then apply.
+// Integer weights: gains are exact int64 (w_vc*2M - k_v*Sigma_c).  Randomness is keyed by
+// (seed, GLOBAL replica index, local vertex id), so results do not depend on the sharding.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <vector>
+
+#include "fc_ctx.h"
+#include "fc_device.h"
+
+namespace fc {
+
+template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
+
+namespace {
+
+constexpr int LTB = 256;          // threads per block (4 waves)
+constexpr int LWS = 256;          // LDS hash slots per wave
+constexpr int LIGHT = 128;        // rows / member-row sums above this go to the block-per-vertex kernels
+constexpr int MODE_MOVE = 0, MODE_REFINE = 1;
+constexpr int MSH = 256;          // move-counter shards
+constexpr int MAX_LEVELS = 64;
+
+inline unsigned nb(int64_t n, int tb = LTB) { return (unsigned)std::max<int64_t>(1, (n + tb - 1) / tb); }
+
+// Level graph: explicit CSR over the union, or (IMPL) the input graph addressed per replica.
+struct LvArgs {
+    int64_t nU;               // union vertices
+    int64_t N0;               // IMPL: vertices per replica
+    const int64_t* rowptr;
+    const int32_t* col;
+    const int32_t* w;         // nullptr: unit weights
+    const int64_t* kv;        // weighted degrees ([N0] when IMPL)
+    const int32_t* rep;       // explicit: local replica of every union vertex
+    const int32_t* roff;      // [n_r] first union id of each replica at this level
+    const uint32_t* rkey;     // [n_r] stream key of this sweep per replica
+    const uint8_t* done;      // [n_r] replica finished
+    int64_t M2;
+    int B;
+    int32_t* P;               // move-phase community
+    int32_t* R;               // refined community
+    int64_t* tot;             // Sigma of the communities the mode works on (ptot or rtot)
+    int32_t* rsize;           // refined community sizes
+    uint8_t* act;             // move queue flags
+    int32_t* blist;           // [nblk][LTB] movers of each decide block (vertex)
+    int32_t* btgt;            // [nblk][LTB] their targets
+    int32_t* bcnt;            // [nblk]
+    int32_t* heavy;           // heavy vertices of this bucket
+    int32_t* heavy_cnt;
+    int32_t* htgt;            // their decisions (-1: stay)
+    int32_t* hkey;            // [LHB][hslots] global tables (kept cleared)
+    int32_t* hval;
+    int32_t* hlst;            // [LHB][hslots] created slots
+    int64_t hslots;
+    unsigned long long* moves;   // [MSH]
+};
+
+template <bool IMPL> __device__ __forceinline__ int32_t rep_of(const LvArgs& a, int64_t x) {
+    return IMPL ? (int32_t)(x / a.N0) : a.rep[x];
+}
+template <bool IMPL> __device__ __forceinline__ int64_t kv_of(const LvArgs& a, int64_t x) {
+    return IMPL ? a.kv[x % a.N0] : a.kv[x];
+}
+__device__ __forceinline__ bool in_bucket(const LvArgs& a, int32_t r, int64_t x, int bucket) {
+    const uint32_t xl = (uint32_t)(x - a.roff[r]);
+    return (int)(hash32(a.rkey[r] ^ hash32(xl)) % (uint32_t)a.B) == bucket;
+}
+__device__ __forceinline__ uint32_t tie_of(const LvArgs& a, int32_t r, int64_t x, int32_t c) {
+    return hash32(hash32(a.rkey[r] ^ 0x5bd1e995u ^ (uint32_t)(x - a.roff[r])) ^ (uint32_t)(c - a.roff[r]));
+}
+// larger score, then larger tie hash, then smaller id; c < 0 = none
+__device__ __forceinline__ bool lv_better(long long s1, uint32_t h1, int32_t c1, long long s2, uint32_t h2, int32_t c2) {
+    if (c1 < 0) return false;
+    if (c2 < 0) return true;
+    if (s1 != s2) return s1 > s2;
+    if (h1 != h2) return h1 > h2;
+    return c1 < c2;
+}
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+// insert (k, w); returns the slot if this call created it, else -1
+__device__ __forceinline__ int tins(int32_t* keys, int32_t* vals, uint32_t nslots, bool pow2, int32_t k, int32_t w) {
+    uint32_t h = hash32((uint32_t)k);
+    h = pow2 ? (h & (nslots - 1)) : (h % nslots);
+    while (true) {
+        const int32_t prev = atomicCAS(&keys[h], -1, k);
+        if (prev == -1) { atomicAdd(&vals[h], w); return (int)h; }
+        if (prev == k) { atomicAdd(&vals[h], w); return -1; }
+        h = (h + 1 == nslots) ? 0 : h + 1;
+    }
+}
+
+// Candidate evaluation shared by the light and heavy deciders.  Returns the target or -1.
+// stay = w_v,own*2M - k_v*(Sigma_own - k_v); a candidate c scores w_vc*2M - k_v*Sigma_c.
+// Move iff the best score beats stay; move phase only: an empty community (score 0, taken
+// as v's own id when that community is empty) when both are negative (leidenalg considers
+// the empty community, ModularityVertexPartition).
+template <int MODE>
+__device__ __forceinline__ int32_t lv_final(const LvArgs& a, int64_t x, int32_t own, long long kvx, long long wown,
+                                            long long bs, int32_t bc) {
+    const long long stay = wown * a.M2 - kvx * (a.tot[own] - kvx);
+    int32_t t = -1;
+    if (bc >= 0 && bs > stay) t = bc;
+    if (MODE == MODE_MOVE && stay < 0 && (t < 0 || bs < 0) && own != (int32_t)x && a.tot[x] == 0) t = (int32_t)x;
+    return t;
+}
+
+// One bucket's decisions.  Each lane owns one union vertex; a wave ballots the eligible
+// ones and decides them one at a time cooperatively (row over the 64 lanes, 256-slot LDS
+// table).  Rows longer than LIGHT go to k_lv_heavy.  Movers are listed per block.
+template <bool IMPL, int MODE>
+__global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket) {
+    __shared__ int32_t skey[LTB / 64][LWS], sval[LTB / 64][LWS];
+    __shared__ int s_cnt;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    bool elig = false;
+    if (x0 < a.nU) {
+        const int32_t r = rep_of<IMPL>(a, x0);
+        if (!a.done[r] && in_bucket(a, r, x0, bucket)) {
+            if (MODE == MODE_MOVE) {
+                elig = a.act[x0] != 0;
+                if (elig) a.act[x0] = 0;   // popped from the queue
+            } else {
+                elig = a.rsize[a.R[x0]] == 1;   // only nodes still alone in their refined community
+            }
+        }
+    }
+    unsigned long long mask = __ballot(elig);
+    int32_t* keys = skey[wv];
+    int32_t* vals = sval[wv];
+    while (mask) {
+        const int l = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        const int64_t x = __shfl(x0, l);
+        const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
+        const int64_t xr = IMPL ? x - base : x;
+        const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
+        if (re - rb > LIGHT) {
+            if (lane == 0) a.heavy[atomicAdd(a.heavy_cnt, 1)] = (int32_t)x;
+            continue;
+        }
+        for (int s = lane; s < LWS; s += 64) { keys[s] = -1; vals[s] = 0; }
+        wsync();
+        const int32_t own = MODE == MODE_MOVE ? a.P[x] : a.R[x];
+        const int32_t pc = a.P[x];
+        for (int64_t j = rb + lane; j < re; j += 64) {
+            const int64_t y = base + a.col[j];
+            const int32_t wy = a.w ? a.w[j] : 1;
+            if (MODE == MODE_REFINE && a.P[y] != pc) continue;
+            tins(keys, vals, LWS, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
+        }
+        wsync();
+        const long long kvx = kv_of<IMPL>(a, x);
+        const int32_t r = rep_of<IMPL>(a, x);
+        long long bs = LLONG_MIN, wown = 0;
+        uint32_t bh = 0;
+        int32_t bc = -1;
+        for (int s = lane; s < LWS; s += 64) {
+            const int32_t k = keys[s];
+            if (k < 0) continue;
+            const long long val = vals[s];
+            if (k == own) { wown = val; continue; }
+            const long long sc = val * a.M2 - kvx * a.tot[k];
+            const uint32_t h = tie_of(a, r, x, k);
+            if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
+        }
+        for (int off = 32; off; off >>= 1) {
+            const long long s2 = __shfl_xor(bs, off);
+            const uint32_t h2 = __shfl_xor(bh, off);
+            const int32_t c2 = __shfl_xor(bc, off);
+            wown += __shfl_xor(wown, off);
+            if (lv_better(s2, h2, c2, bs, bh, bc)) { bs = s2; bh = h2; bc = c2; }
+        }
+        if (lane == 0) {
+            const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
+            if (t >= 0) {
+                const int p = atomicAdd(&s_cnt, 1);
+                a.blist[(int64_t)blockIdx.x * LTB + p] = (int32_t)x;
+                a.btgt[(int64_t)blockIdx.x * LTB + p] = t;
+            }
+        }
+        wsync();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) a.bcnt[blockIdx.x] = s_cnt;
+}
+
+// Block reduction of (score, tie, community) candidates; thread 0 ends with the best.
+struct BRed {
+    long long s[LTB / 64];
+    uint32_t h[LTB / 64];
+    int32_t c[LTB / 64];
+    long long wown[LTB / 64];
+};
+__device__ __forceinline__ void block_best(BRed& red, long long& bs, uint32_t& bh, int32_t& bc, long long& wown) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int off = 32; off; off >>= 1) {
+        const long long s2 = __shfl_xor(bs, off);
+        const uint32_t h2 = __shfl_xor(bh, off);
+        const int32_t c2 = __shfl_xor(bc, off);
+        wown += __shfl_xor(wown, off);
+        if (lv_better(s2, h2, c2, bs, bh, bc)) { bs = s2; bh = h2; bc = c2; }
+    }
+    if (lane == 0) { red.s[wv] = bs; red.h[wv] = bh; red.c[wv] = bc; red.wown[wv] = wown; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < LTB / 64; ++k) {
+            wown += red.wown[k];
+            if (lv_better(red.s[k], red.h[k], red.c[k], bs, bh, bc)) { bs = red.s[k]; bh = red.h[k]; bc = red.c[k]; }
+        }
+    }
+    __syncthreads();
+}
+
+// Long rows: one block per vertex over a global hash table (one table per block, cleared
+// through the list of slots it created).
+template <bool IMPL, int MODE>
+__global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a) {
+    __shared__ int s_n;
+    __shared__ BRed red;
+    const int n = *a.heavy_cnt;
+    int32_t* keys = a.hkey + (int64_t)blockIdx.x * a.hslots;
+    int32_t* vals = a.hval + (int64_t)blockIdx.x * a.hslots;
+    int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
+    const uint32_t ns = (uint32_t)a.hslots;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t x = a.heavy[i];
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
+        const int64_t xr = IMPL ? x - base : x;
+        const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
+        const int32_t own = MODE == MODE_MOVE ? a.P[x] : a.R[x];
+        const int32_t pc = a.P[x];
+        for (int64_t j = rb + threadIdx.x; j < re; j += LTB) {
+            const int64_t y = base + a.col[j];
+            const int32_t wy = a.w ? a.w[j] : 1;
+            if (MODE == MODE_REFINE && a.P[y] != pc) continue;
+            const int s = tins(keys, vals, ns, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
+            if (s >= 0) lst[atomicAdd(&s_n, 1)] = s;
+        }
+        __syncthreads();
+        const long long kvx = kv_of<IMPL>(a, x);
+        const int32_t r = rep_of<IMPL>(a, x);
+        long long bs = LLONG_MIN, wown = 0;
+        uint32_t bh = 0;
+        int32_t bc = -1;
+        const int cnt = s_n;
+        for (int q = threadIdx.x; q < cnt; q += LTB) {
+            const int s = lst[q];
+            const int32_t k = keys[s];
+            const long long val = vals[s];
+            keys[s] = -1; vals[s] = 0;   // clear for the next vertex (read before)
+            if (k == own) { wown = val; continue; }
+            const long long sc = val * a.M2 - kvx * a.tot[k];
+            const uint32_t h = tie_of(a, r, x, k);
+            if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
+        }
+        block_best(red, bs, bh, bc, wown);
+        if (threadIdx.x == 0) a.htgt[i] = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
+        __syncthreads();
+    }
+}
+
+// Apply one bucket's moves: blocks [0, nblk) take the decide blocks' lists, the rest the
+// heavy decisions.  Move phase: P, Sigma, and the queue (neighbours outside the new
+// community); refine: R, Sigma and sizes.
+template <bool IMPL, int MODE>
+__device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, unsigned long long& mv) {
+    const long long kvx = kv_of<IMPL>(a, x);
+    if (MODE == MODE_MOVE) {
+        const int32_t old = a.P[x];
+        a.P[x] = t;
+        atomicAdd((unsigned long long*)&a.tot[t], (unsigned long long)kvx);
+        atomicAdd((unsigned long long*)&a.tot[old], (unsigned long long)(-kvx));
+        const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
+        const int64_t xr = IMPL ? x - base : x;
+        for (int64_t j = a.rowptr[xr]; j < a.rowptr[xr + 1]; ++j) {
+            const int64_t y = base + a.col[j];
+            if (a.P[y] != t) a.act[y] = 1;
+        }
+    } else {
+        const int32_t old = a.R[x];
+        a.R[x] = t;
+        atomicAdd((unsigned long long*)&a.tot[t], (unsigned long long)kvx);
+        atomicAdd((unsigned long long*)&a.tot[old], (unsigned long long)(-kvx));
+        atomicAdd(&a.rsize[t], 1);
+        atomicAdd(&a.rsize[old], -1);
+    }
+    ++mv;
+}
+template <bool IMPL, int MODE>
+__global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk) {
+    unsigned long long mv = 0;
+    if ((int)blockIdx.x < nblk) {
+        const int n = a.bcnt[blockIdx.x];
+        if ((int)threadIdx.x < n) {
+            const int64_t q = (int64_t)blockIdx.x * LTB + threadIdx.x;
+            lv_move<IMPL, MODE>(a, a.blist[q], a.btgt[q], mv);
+        }
+    } else {
+        const int n = *a.heavy_cnt;
+        for (int i = (blockIdx.x - nblk) * LTB + threadIdx.x; i < n; i += hblk * LTB) {
+            const int32_t t = a.htgt[i];
+            if (t >= 0) lv_move<IMPL, MODE>(a, a.heavy[i], t, mv);
+        }
+    }
+    for (int off = 32; off; off >>= 1) mv += __shfl_xor(mv, off);
+    if ((threadIdx.x & 63) == 0 && mv) atomicAdd(&a.moves[blockIdx.x & (MSH - 1)], mv);
+}
+
+// ---------------------------------------------------------------- level bookkeeping kernels
+__global__ void k_lv_init0(int64_t N, int n_r, const int32_t* lab, const int32_t* spos, int32_t* P, int32_t* R,
+                           int64_t* rtot, int32_t* rsize, const int64_t* kdeg, int32_t* memb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n_r * N) return;
+    const int64_t r = i / N, v = i - r * N;
+    P[i] = (int32_t)(r * N + lab[r * N + spos[v]]);
+    R[i] = (int32_t)i;
+    rtot[i] = kdeg[v];
+    rsize[i] = 1;
+    memb[i] = (int32_t)i;
+}
+// singleton refined partition of an explicit level
+__global__ void k_lv_rinit(int64_t nU, const int64_t* kv, int32_t* R, int64_t* rtot, int32_t* rsize) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nU) return;
+    R[i] = (int32_t)i;
+    rtot[i] = kv[i];
+    rsize[i] = 1;
+}
+template <bool IMPL>
+__global__ void k_ag_flags(LvArgs a, int32_t* flag) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > a.nU) return;
+    flag[c] = (c < a.nU && a.rsize[c] > 0 && !a.done[rep_of<IMPL>(a, c)]) ? 1 : 0;
+}
+// per replica: refined communities (from the scan) at the replica's first/last union id
+__global__ void k_ag_counts(int n_r, const uint8_t* done, const int32_t* roff, const int32_t* rend, const int32_t* nid,
+                            int32_t* out) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n_r) out[r] = done[r] ? 0 : nid[rend[r]] - nid[roff[r]];   // finished: ranges are stale
+}
+template <bool IMPL>
+__global__ void k_ag_nodes(LvArgs a, const int32_t* nid, int32_t* nrep, int64_t* nkv, int32_t* mcnt) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.nU || nid[c + 1] == nid[c]) return;
+    const int32_t xn = nid[c];
+    nrep[xn] = rep_of<IMPL>(a, c);
+    nkv[xn] = a.tot[c];   // rtot: the refined community's weighted degree
+    mcnt[xn] = a.rsize[c];
+}
+// pofR[R[x]] = P[x] (every member agrees: R refines P); prep[P] = min new id over members;
+// ub[new id] += deg(x)
+template <bool IMPL>
+__global__ void k_ag_members(LvArgs a, const int32_t* nid, int32_t* pofR, int32_t* prep, int64_t* ub) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= a.nU) return;
+    if (a.done[rep_of<IMPL>(a, x)]) return;
+    const int32_t rc = a.R[x];
+    pofR[rc] = a.P[x];
+    const int32_t xn = nid[rc];
+    atomicMin(&prep[a.P[x]], xn);
+    const int64_t xr = IMPL ? x % a.N0 : x;
+    atomicAdd((unsigned long long*)&ub[xn], (unsigned long long)(a.rowptr[xr + 1] - a.rowptr[xr]));
+}
+template <bool IMPL>
+__global__ void k_ag_fill(LvArgs a, const int32_t* nid, const int32_t* moff, int32_t* mcur, int32_t* mlist) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= a.nU) return;
+    if (a.done[rep_of<IMPL>(a, x)]) return;
+    const int32_t xn = nid[a.R[x]];
+    mlist[moff[xn] + atomicAdd(&mcur[xn], 1)] = (int32_t)x;
+}
+__global__ void k_ag_part(int64_t nU, const int32_t* nid, const int32_t* pofR, const int32_t* prep, int32_t* nP) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nU || nid[c + 1] == nid[c]) return;
+    nP[nid[c]] = prep[pofR[c]];
+}
+__global__ void k_ag_ptot(int64_t nU, const int32_t* P, const int64_t* kv, int64_t* ptot) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < nU) atomicAdd((unsigned long long*)&ptot[P[x]], (unsigned long long)kv[x]);
+}
+__global__ void k_ag_memb(int64_t total, int64_t N, const uint8_t* done, const int32_t* R, const int32_t* nid,
+                          int32_t* memb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total || done[i / N]) return;
+    memb[i] = nid[R[memb[i]]];
+}
+
+// Aggregate rows: new vertex xn = refined community; its row = the members' rows mapped
+// through nid[R[.]], self loops dropped, weights summed.  One wave per light new vertex
+// (LDS table), heavy ones (member-row sum > LIGHT) are listed for k_ag_rows_heavy.  Rows
+// are written at their upper-bound offsets ubo and compacted afterwards.
+template <bool IMPL>
+__global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const int32_t* nid, const int32_t* moff,
+                                                 const int32_t* mlist, const int64_t* ubo, int32_t* ocol, int32_t* ow,
+                                                 int32_t* olen, int32_t* hlist, int32_t* hcnt) {
+    __shared__ int32_t skey[LTB / 64][LWS], sval[LTB / 64][LWS];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t xn = (int64_t)blockIdx.x * (LTB / 64) + wv;
+    if (xn >= nUn) return;
+    if (ubo[xn + 1] - ubo[xn] > LIGHT) {
+        if (lane == 0) hlist[atomicAdd(hcnt, 1)] = (int32_t)xn;
+        return;
+    }
+    int32_t* keys = skey[wv];
+    int32_t* vals = sval[wv];
+    for (int s = lane; s < LWS; s += 64) { keys[s] = -1; vals[s] = 0; }
+    wsync();
+    for (int32_t q = moff[xn]; q < moff[xn + 1]; ++q) {
+        const int64_t x = mlist[q];
+        const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
+        const int64_t xr = IMPL ? x - base : x;
+        for (int64_t j = a.rowptr[xr] + lane; j < a.rowptr[xr + 1]; j += 64) {
+            const int32_t yn = nid[a.R[base + a.col[j]]];
+            if (yn != (int32_t)xn) tins(keys, vals, LWS, true, yn, a.w ? a.w[j] : 1);
+        }
+    }
+    wsync();
+    int32_t cnt = 0;
+    const int64_t o = ubo[xn];
+    for (int s0 = 0; s0 < LWS; s0 += 64) {
+        const int32_t k = keys[s0 + lane];
+        const unsigned long long bal = __ballot(k >= 0);
+        if (k >= 0) {
+            const int p = cnt + __popcll(bal & ((1ull << lane) - 1));
+            ocol[o + p] = k;
+            ow[o + p] = vals[s0 + lane];
+        }
+        cnt += __popcll(bal);
+    }
+    if (lane == 0) olen[xn] = cnt;
+}
+template <bool IMPL>
+__global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* nid, const int32_t* moff,
+                                                       const int32_t* mlist, const int64_t* ubo, int32_t* ocol,
+                                                       int32_t* ow, int32_t* olen, const int32_t* hlist,
+                                                       const int32_t* hcnt) {
+    __shared__ int s_n;
+    const int n = *hcnt;
+    int32_t* keys = a.hkey + (int64_t)blockIdx.x * a.hslots;
+    int32_t* vals = a.hval + (int64_t)blockIdx.x * a.hslots;
+    int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
+    const uint32_t ns = (uint32_t)a.hslots;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t xn = hlist[i];
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        for (int32_t q = moff[xn]; q < moff[xn + 1]; ++q) {
+            const int64_t x = mlist[q];
+            const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
+            const int64_t xr = IMPL ? x - base : x;
+            for (int64_t j = a.rowptr[xr] + threadIdx.x; j < a.rowptr[xr + 1]; j += LTB) {
+                const int32_t yn = nid[a.R[base + a.col[j]]];
+                if (yn == (int32_t)xn) continue;
+                const int s = tins(keys, vals, ns, true, yn, a.w ? a.w[j] : 1);
+                if (s >= 0) lst[atomicAdd(&s_n, 1)] = s;
+            }
+        }
+        __syncthreads();
+        const int cnt = s_n;
+        const int64_t o = ubo[xn];
+        for (int q = threadIdx.x; q < cnt; q += LTB) {
+            const int s = lst[q];
+            ocol[o + q] = keys[s];
+            ow[o + q] = vals[s];
+            keys[s] = -1; vals[s] = 0;
+        }
+        if (threadIdx.x == 0) olen[xn] = cnt;
+        __syncthreads();
+    }
+}
+__global__ void k_ag_len64(int64_t n, const int32_t* len, int64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) out[i] = i < n ? len[i] : 0;
+}
+// compact rows (sorted by column, so rows are canonical and deterministic)
+__global__ __launch_bounds__(LTB) void k_ag_compact(int64_t nUn, const int64_t* ubo, const int64_t* rp,
+                                                    const int32_t* icol, const int32_t* iw, int32_t* ocol,
+                                                    int32_t* ow) {
+    const int lane = threadIdx.x & 63;
+    const int64_t xn = (int64_t)blockIdx.x * (LTB / 64) + (threadIdx.x >> 6);
+    if (xn >= nUn) return;
+    const int64_t o = ubo[xn], d = rp[xn + 1] - rp[xn], q = rp[xn];
+    for (int64_t k = lane; k < d; k += 64) { ocol[q + k] = icol[o + k]; ow[q + k] = iw[o + k]; }
+}
+__global__ void k_ag_roff(int64_t nU, const int32_t* rep, int32_t* roff, int32_t* rend) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= nU) return;
+    if (x == 0 || rep[x - 1] != rep[x]) roff[rep[x]] = (int32_t)x;
+    if (x == nU - 1 || rep[x + 1] != rep[x]) rend[rep[x]] = (int32_t)(x + 1);
+}
+// final labels of replica r (fin[r] = 1): lab[r][spos[v]] = P[memb[r*N+v]] - roff[r]
+__global__ void k_lv_final(int64_t N, int n_r, const uint8_t* fin, const int32_t* memb, const int32_t* P,
+                           const int32_t* roff, const int32_t* spos, int32_t* lab) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n_r * N) return;
+    const int64_t r = i / N, v = i - r * N;
+    if (!fin[r]) return;
+    lab[r * N + spos[v]] = P[memb[i]] - roff[r];
+}
+__global__ void k_lv_fill_i32(int64_t n, int32_t* p, int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_lv_fill_u8(int64_t n, uint8_t* p, const uint8_t* done, const int32_t* rep) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = done[rep[i]] ? 0 : 1;
+}
+
+// Buffers (Ctx::lv).
+enum {
+    B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
+    B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC,
+    // aggregation scratch
+    B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
+    // explicit level graphs, ping-pong: rowptr, col, w, kv, rep (x2)
+    B_G0, B_G1 = B_G0 + 5, B_END = B_G1 + 5
+};
+static_assert(B_END <= (int)(sizeof(((Ctx*)nullptr)->lv) / sizeof(DevBuf)), "Ctx::lv too small");
+
+// device max of ubo[i+1]-ubo[i] (int64) or of len[i] (int32): one atomic per block
+__global__ void k_max_row(int64_t n, const int64_t* ubo, const int32_t* len, unsigned long long* out) {
+    __shared__ unsigned long long sm[LTB / 64];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long v = 0;
+    if (i < n) v = ubo ? (unsigned long long)(ubo[i + 1] - ubo[i]) : (unsigned long long)len[i];
+    for (int off = 32; off; off >>= 1) { const unsigned long long o = __shfl_xor(v, off); v = o > v ? o : v; }
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < LTB / 64; ++k) v = sm[k] > v ? sm[k] : v;
+        if (v) atomicMax(out, v);
+    }
+}
+
+struct LvGraph {
+    int64_t nU = 0, E = 0;
+    int64_t* rowptr = nullptr;
+    int32_t* col = nullptr;
+    int32_t* w = nullptr;
+    int64_t* kv = nullptr;
+    int32_t* rep = nullptr;
+    int32_t max_deg = 0;
+};
+
+}  // namespace
+
+// One Leiden run per local replica on the working graph c.g; labels -> c.lab (slot order,
+// values in [0, N) per replica), exactly like cd_run leaves them.
+void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
+    FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
+    FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
+    const int64_t N = c.N;
+    Graph& g = c.g;
+    FC_REQUIRE(g.M2 < 0x7fffffffll, FC_ELIMIT, "leiden: total edge weight must stay below 2^30");
+    FC_REQUIRE((int64_t)rcount * N < 0x7fffffffll, FC_ELIMIT, "leiden: replicas x nodes must stay below 2^31");
+
+    // ---- level 0, move phase: the replica-batched local-moving engine run to exhaustion
+    const double mdq = c.cd_min_dq;
+    c.cd_min_dq = 0.0;
+    try {
+        cd_run(c, FC_ALGO_LOUVAIN, rbegin, rcount, n_p_total, iteration);
+    } catch (...) {
+        c.cd_min_dq = mdq;
+        throw;
+    }
+    c.cd_min_dq = mdq;
+    const int sl0 = timer_begin(c);   // cd_run timed itself; this span covers refinement and the levels
+
+    const int n_r = rcount;
+    const int64_t nU0 = (int64_t)n_r * N;
+    const int B = std::max(1, c.buckets);
+    auto I32 = [&](int k, int64_t n) { return ensure<int32_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };
+    auto I64 = [&](int k, int64_t n) { return ensure<int64_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };
+    auto U8 = [&](int k, int64_t n) { return ensure<uint8_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };
+
+    int32_t* P = I32(B_P, nU0);
+    int32_t* R = I32(B_R, nU0);
+    int64_t* rtot = I64(B_RTOT, nU0);
+    int32_t* rsize = I32(B_RSIZE, nU0);
+    int32_t* memb = I32(B_MEMB, nU0);
+    uint8_t* done = U8(B_DONE, n_r);
+    int32_t* roff = I32(B_ROFF, n_r);
+    int32_t* rend = I32(B_REND, n_r);
+    uint32_t* rkey = (uint32_t*)I32(B_RKEY, n_r);
+    unsigned long long* moves = (unsigned long long*)I64(B_MOVES, MSH);
+    int32_t* hcnt = I32(B_HCNT, 4);
+    // [n_r] refined-community counts | [n_r] finalize flags (u8 view) | 2 u64 maxima
+    int32_t* misc = I32(B_MISC, 2 * (int64_t)n_r + 16);
+    FC_HIP(hipMemsetAsync(done, 0, n_r, c.stream));
+    k_lv_init0<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, c.lab.as<int32_t>(), c.spos.as<int32_t>(), P, R, rtot, rsize,
+                                               g.kdeg.as<int64_t>(), memb);
+    std::vector<int32_t> h_roff(n_r), h_rend(n_r);
+    for (int r = 0; r < n_r; ++r) { h_roff[r] = (int32_t)(r * N); h_rend[r] = (int32_t)((r + 1) * N); }
+    FC_HIP(hipMemcpyAsync(roff, h_roff.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
+    FC_HIP(hipMemcpyAsync(rend, h_rend.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
+    std::vector<uint8_t> h_done(n_r, 0);
+    std::vector<uint32_t> h_rkey(n_r);
+
+    LvArgs a{};
+    a.N0 = N; a.M2 = g.M2; a.B = B;
+    a.roff = roff; a.rkey = rkey; a.done = done; a.moves = moves;
+    a.heavy_cnt = hcnt;
+
+    LvGraph cur;            // explicit level (level >= 1)
+    int pp = 0;             // ping-pong slot of the next explicit level
+    int64_t nU = nU0;
+    bool impl = true;
+    int32_t max_deg = g.max_deg;
+
+    auto set_keys = [&](int level, int sweep, uint32_t salt) {
+        for (int r = 0; r < n_r; ++r)
+            h_rkey[r] = stream_key(c.seed, (uint32_t)(rbegin + r), (uint32_t)iteration,
+                                   (uint32_t)(level * 4096 + sweep), 16 + salt);
+        FC_HIP(hipMemcpyAsync(rkey, h_rkey.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
+    };
+    auto set_graph = [&]() {
+        a.nU = nU;
+        if (impl) {
+            a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>();
+            a.w = (g.max_w == 1) ? nullptr : g.cw.as<int32_t>();
+            a.kv = g.kdeg.as<int64_t>(); a.rep = nullptr;
+        } else {
+            a.rowptr = cur.rowptr; a.col = cur.col; a.w = cur.w; a.kv = cur.kv; a.rep = cur.rep;
+        }
+        const int64_t nblk = nb(nU);
+        a.blist = I32(B_BLIST, nblk * LTB);
+        a.btgt = I32(B_BTGT, nblk * LTB);
+        a.bcnt = I32(B_BCNT, nblk);
+        a.heavy = I32(B_HEAVY, nU);
+        a.htgt = I32(B_HTGT, nU);
+        int64_t hs = 1;
+        while (hs < 2 * (int64_t)std::max(max_deg, 1)) hs <<= 1;
+        a.hslots = hs;
+    };
+    // heavy-kernel grid: one global table per block, bounded to ~2 GB of tables
+    auto heavy_grid = [&](int64_t slots) {
+        int64_t gr = std::min<int64_t>(256, std::max<int64_t>(1, ((int64_t)2 << 30) / (12 * slots)));
+        const size_t need = (size_t)(gr * slots);
+        const bool grow = c.lv[B_HKEY].bytes < need * 4 + 16;
+        a.hkey = I32(B_HKEY, gr * slots);
+        a.hval = I32(B_HVAL, gr * slots);
+        a.hlst = I32(B_HLST, gr * slots);
+        if (grow) {   // tables are kept cleared by their users; a fresh allocation is cleared once
+            FC_HIP(hipMemsetAsync(a.hkey, 0xff, c.lv[B_HKEY].bytes, c.stream));
+            FC_HIP(hipMemsetAsync(a.hval, 0, c.lv[B_HVAL].bytes, c.stream));
+        }
+        return (int)gr;
+    };
+
+    // one bucketed sweep; returns moves
+    auto sweep = [&](int MODE, int level, int sw) -> unsigned long long {
+        set_keys(level, sw, (uint32_t)MODE);
+        FC_HIP(hipMemsetAsync(moves, 0, 8 * MSH, c.stream));
+        const int nblk = (int)nb(nU);
+        const int hg = heavy_grid(a.hslots);
+        const int hblk = 64;
+        for (int b = 0; b < B; ++b) {
+            FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
+#define LV_LAUNCH(IM, MD)                                                                        \
+    do {                                                                                         \
+        k_lv_decide<IM, MD><<<nblk, LTB, 0, c.stream>>>(a, b);                                   \
+        if (max_deg > LIGHT) k_lv_heavy<IM, MD><<<hg, LTB, 0, c.stream>>>(a);                    \
+        k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk); \
+    } while (0)
+            if (impl && MODE == MODE_MOVE) LV_LAUNCH(true, MODE_MOVE);
+            else if (impl) LV_LAUNCH(true, MODE_REFINE);
+            else if (MODE == MODE_MOVE) LV_LAUNCH(false, MODE_MOVE);
+            else LV_LAUNCH(false, MODE_REFINE);
+#undef LV_LAUNCH
+        }
+        std::vector<unsigned long long> hm(MSH);
+        FC_HIP(hipMemcpyAsync(hm.data(), moves, 8 * MSH, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        unsigned long long t = 0;
+        for (auto v : hm) t += v;
+        return t;
+    };
+
+    int level = 0;
+    int64_t lv_sweeps = 0;
+    for (;; ++level) {
+        // ---- refine: singletons inside the move-phase communities, one sweep
+        set_graph();
+        if (!impl) k_lv_rinit<<<nb(nU), LTB, 0, c.stream>>>(nU, cur.kv, R, rtot, rsize);
+        a.P = P; a.R = R; a.tot = rtot; a.rsize = rsize;
+        sweep(MODE_REFINE, level, 0);
+        ++lv_sweeps;
+        // ---- which replicas still aggregate: refined communities < level nodes
+        int32_t* nid = I32(B_NID, nU + 1);
+        int32_t* fl = I32(B_FL, nU + 1);
+        if (impl) k_ag_flags<true><<<nb(nU + 1), LTB, 0, c.stream>>>(a, fl);
+        else k_ag_flags<false><<<nb(nU + 1), LTB, 0, c.stream>>>(a, fl);
+        exclusive_scan(c, fl, nid, nU + 1);
+        k_ag_counts<<<nb(n_r), LTB, 0, c.stream>>>(n_r, done, roff, rend, nid, misc);
+        std::vector<int32_t> rc(n_r);
+        FC_HIP(hipMemcpyAsync(rc.data(), misc, 4 * (size_t)n_r, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        std::vector<uint8_t> fin(n_r, 0);
+        bool any_fin = false, any_left = false;
+        for (int r = 0; r < n_r; ++r) {
+            if (h_done[r]) continue;
+            if (rc[r] == h_rend[r] - h_roff[r] || level + 1 >= MAX_LEVELS) { fin[r] = 1; any_fin = true; }
+            else any_left = true;
+        }
+        if (any_fin) {
+            uint8_t* dfin = (uint8_t*)(misc + n_r);
+            FC_HIP(hipMemcpyAsync(dfin, fin.data(), n_r, hipMemcpyHostToDevice, c.stream));
+            k_lv_final<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, dfin, memb, P, roff, c.spos.as<int32_t>(),
+                                                      c.lab.as<int32_t>());
+            for (int r = 0; r < n_r; ++r) h_done[r] |= fin[r];
+            FC_HIP(hipMemcpyAsync(done, h_done.data(), n_r, hipMemcpyHostToDevice, c.stream));
+            sync(c);
+        }
+        if (!any_left) break;
+        if (any_fin) {   // drop the finished replicas from the next level
+            if (impl) k_ag_flags<true><<<nb(nU + 1), LTB, 0, c.stream>>>(a, fl);
+            else k_ag_flags<false><<<nb(nU + 1), LTB, 0, c.stream>>>(a, fl);
+            exclusive_scan(c, fl, nid, nU + 1);
+        }
+        // ---- aggregate by the refined partition
+        int64_t nUn = 0;
+        {
+            int32_t t32;
+            FC_HIP(hipMemcpyAsync(&t32, nid + nU, 4, hipMemcpyDeviceToHost, c.stream));
+            sync(c);
+            nUn = t32;
+        }
+        const int gs = pp ? B_G1 : B_G0;
+        LvGraph nx;
+        nx.nU = nUn;
+        nx.rowptr = I64(gs + 0, nUn + 1);
+        nx.kv = I64(gs + 3, nUn);
+        nx.rep = I32(gs + 4, nUn);
+        int32_t* mcnt = I32(B_MCNT, nUn + 1);
+        if (impl) k_ag_nodes<true><<<nb(nU), LTB, 0, c.stream>>>(a, nid, nx.rep, nx.kv, mcnt);
+        else k_ag_nodes<false><<<nb(nU), LTB, 0, c.stream>>>(a, nid, nx.rep, nx.kv, mcnt);
+        FC_HIP(hipMemsetAsync(mcnt + nUn, 0, 4, c.stream));
+        int32_t* moff = I32(B_MOFF, nUn + 1);
+        exclusive_scan(c, mcnt, moff, nUn + 1);
+        int32_t* pofR = I32(B_HTGT, nU);   // free between sweeps
+        int32_t* prep = I32(B_HEAVY, nU);
+        int64_t* ub = I64(B_UB, nUn + 1);
+        int64_t* ubo = I64(B_UBO, nUn + 1);
+        k_lv_fill_i32<<<nb(nU), LTB, 0, c.stream>>>(nU, prep, INT_MAX);
+        FC_HIP(hipMemsetAsync(ub, 0, 8 * ((size_t)nUn + 1), c.stream));
+        if (impl) k_ag_members<true><<<nb(nU), LTB, 0, c.stream>>>(a, nid, pofR, prep, ub);
+        else k_ag_members<false><<<nb(nU), LTB, 0, c.stream>>>(a, nid, pofR, prep, ub);
+        exclusive_scan(c, ub, ubo, nUn + 1);
+        int32_t* mcur = I32(B_MCUR, nUn + 1);
+        int32_t* mlist = I32(B_MLIST, nU + 1);
+        FC_HIP(hipMemsetAsync(mcur, 0, 4 * (size_t)nUn, c.stream));
+        if (impl) k_ag_fill<true><<<nb(nU), LTB, 0, c.stream>>>(a, nid, moff, mcur, mlist);
+        else k_ag_fill<false><<<nb(nU), LTB, 0, c.stream>>>(a, nid, moff, mcur, mlist);
+        // [0] member-row sum total, [1] the longest one (bounds the heavy tables), [2] longest new row
+        int64_t* hx = (int64_t*)c.hpin + 40;
+        unsigned long long* dmax = (unsigned long long*)(misc + 2 * (int64_t)n_r + 2 + ((2 * n_r) & 1));
+        FC_HIP(hipMemsetAsync(dmax, 0, 16, c.stream));
+        k_max_row<<<nb(nUn), LTB, 0, c.stream>>>(nUn, ubo, nullptr, dmax);
+        FC_HIP(hipMemcpyAsync(hx, ubo + nUn, 8, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hx + 1, dmax, 8, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        const int64_t ubtot = hx[0], ubmax = hx[1];
+        int32_t* tcol = I32(B_TCOL, ubtot + 1);
+        int32_t* tw = I32(B_TW, ubtot + 1);
+        int32_t* olen = I32(B_OLEN, nUn + 1);
+        int32_t* agh = I32(B_AGH, nUn + 1);
+        FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
+        const unsigned agb = nb(nUn, LTB / 64);
+        if (impl) k_ag_rows<true><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+        else k_ag_rows<false><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+        if (ubmax > LIGHT) {
+            int64_t hs = 1;
+            while (hs < 2 * ubmax) hs <<= 1;
+            a.hslots = hs;
+            const int hg = heavy_grid(hs);
+            if (impl) k_ag_rows_heavy<true><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+            else k_ag_rows_heavy<false><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+        }
+        int64_t* len64 = I64(B_LEN64, nUn + 1);
+        k_ag_len64<<<nb(nUn + 1), LTB, 0, c.stream>>>(nUn, olen, len64);
+        exclusive_scan(c, len64, nx.rowptr, nUn + 1);
+        k_max_row<<<nb(nUn), LTB, 0, c.stream>>>(nUn, nullptr, olen, dmax + 1);
+        FC_HIP(hipMemcpyAsync(hx, nx.rowptr + nUn, 8, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hx + 2, dmax + 1, 8, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        nx.E = hx[0];
+        nx.max_deg = (int32_t)hx[2];
+        nx.col = I32(gs + 1, nx.E);
+        nx.w = I32(gs + 2, nx.E);
+        k_ag_compact<<<agb, LTB, 0, c.stream>>>(nUn, ubo, nx.rowptr, tcol, tw, nx.col, nx.w);
+        // P of the new level: each new vertex starts in its members' move-phase community
+        int32_t* nP = I32(B_PTOT, nUn);   // staged in the (free) ptot buffer, then swapped into P
+        k_ag_part<<<nb(nU), LTB, 0, c.stream>>>(nU, nid, pofR, prep, nP);
+        k_ag_memb<<<nb(nU0), LTB, 0, c.stream>>>(nU0, N, done, R, nid, memb);
+        std::swap(c.lv[B_P], c.lv[B_PTOT]);
+        P = c.lv[B_P].as<int32_t>();
+        // replica ranges of the new level
+        k_ag_roff<<<nb(nUn), LTB, 0, c.stream>>>(nUn, nx.rep, roff, rend);
+        FC_HIP(hipMemcpyAsync(h_roff.data(), roff, 4 * (size_t)n_r, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(h_rend.data(), rend, 4 * (size_t)n_r, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        cur = nx;
+        pp ^= 1;
+        impl = false;
+        nU = nUn;
+        max_deg = nx.max_deg;
+        // ---- move phase on the new level, from the inherited partition, until no move
+        int64_t* ptot = I64(B_PTOT, nU);
+        R = I32(B_R, nU); rtot = I64(B_RTOT, nU); rsize = I32(B_RSIZE, nU);
+        FC_HIP(hipMemsetAsync(ptot, 0, 8 * (size_t)nU, c.stream));
+        k_ag_ptot<<<nb(nU), LTB, 0, c.stream>>>(nU, P, cur.kv, ptot);
+        uint8_t* act = U8(B_ACT, nU);
+        k_lv_fill_u8<<<nb(nU), LTB, 0, c.stream>>>(nU, act, done, cur.rep);
+        set_graph();
+        a.P = P; a.R = R; a.tot = ptot; a.rsize = rsize; a.act = act;
+        for (int sw = 0; sw < c.max_sweeps; ++sw) {
+            ++lv_sweeps;
+            if (sweep(MODE_MOVE, level + 1, sw + 1) == 0) break;
+        }
+    }
+    if (c.trace) fprintf(stderr, "[fc] leiden it=%d: %d levels, %lld level sweeps\n", iteration, level + 1,
+                         (long long)lv_sweeps);
+    c.acc.cd_sweeps += lv_sweeps * n_r;
+    c.prof.cd_sweeps += lv_sweeps * n_r;
+    c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
+    c.labT_valid = false;
+    timer_end(c, 0, sl0);
+}
+
+}  // namespace fc

@@ -22,7 +22,7 @@ import torch.distributed as dist
 
 from .core import FINAL_PASS_ITER
 
-LOUVAIN, LPM, LOUVAIN_NC = 0, 1, 2
+LOUVAIN, LPM, LOUVAIN_NC, LEIDEN = 0, 1, 2, 3
 
 
 def on_device(t):
@@ -79,7 +79,12 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
     n, _, L = engine.graph_info()
     st = {"iterations": 0, "exit_check": 0, "hit_iter_cap": 0, "partition_edges": 0, "n_p": n_p}
     it = 0
-    while True:
+    if algo == LEIDEN:
+        # fast_consensus.py:204-258 on integer node ids: the str-keyed lookups (:97, :217) never
+        # match, every weight stays 0 and check #1 (:229) converges on the emptied graph; the
+        # loop's CD batch cannot reach the result (capi.cpp fc_run does the same)
+        st["exit_check"] = 1
+    while algo != LEIDEN:
         if it >= max_iters:
             st["hit_iter_cap"] = 1
             break

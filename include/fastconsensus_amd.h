@@ -40,6 +40,14 @@ extern "C" {
 #define FC_ALGO_LOUVAIN_NC 2 /* louvain with new_consensus.py's weight rule (:155-163): an edge of
                                 weight w not in {0,n_p} gets the plain co-membership count,
                                 others keep w; everything else as FC_ALGO_LOUVAIN */
+#define FC_ALGO_LEIDEN 3  /* fast_consensus.py:204-258 (+ final pass :385-388): n_p Leiden runs
+                             (leidenalg ModularityVertexPartition, n_iterations=1, :121-123).  On the
+                             integer-labelled graphs the CLI reads (:434) the loop's membership
+                             lookups are keyed by str(vertex) (:97) and never match an int node
+                             (:217), so every consensus weight stays 0, :223-227 removes every
+                             edge and check #1 (:229) converges on the empty graph: the result is
+                             the final pass on G.  fc_run reports that one iteration (exit 1)
+                             without running its discarded CD batch.   */
 
 typedef struct fc_ctx fc_ctx;
 
@@ -145,7 +153,8 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
 
 /* ---- fine-grained steps (distributed driver; parity tests) ------------------------ */
 /* Community detection on the working graph for replicas [replica_begin,
- * replica_begin+replica_count) of n_p_total (:148 / :384 louvain level 0, :270 / :392 LPA).
+ * replica_begin+replica_count) of n_p_total (:148 / :384 louvain level 0, :270 / :392 LPA,
+ * :210-211 / :386-387 Leiden).
  * Randomness depends on (seed, global replica index, iteration), not on the sharding. */
 int fc_cd(fc_ctx* ctx, int algo, int replica_begin, int replica_count, int n_p_total,
           int iteration);

@@ -392,8 +392,216 @@ int orc_lpa(i64 N, const i64* rowptr, const i32* col, u64 seed, i32* lab, int ma
     return sweeps;
 }
 
+/* ------------------------------------------------------------------ leidenalg Leiden
+ * Restatement of leidenalg.find_partition(G, ModularityVertexPartition, weights='weight',
+ * seed=i, n_iterations=1) as called at fast_consensus.py:121-123 (n_p times, :210-211 and
+ * :386-387).  leidenalg is not vendored and not installed here, so this follows its
+ * published algorithm (Traag, Waltman & van Eck, Sci. Rep. 9:5233, 2019) and the package's
+ * documented defaults -- parity unpinned (statistical comparisons only):
+ *   move_nodes: a queue holding every node in random order; the popped node moves to the
+ *     neighbour community -- or an empty one -- of largest modularity gain when that gain
+ *     is positive; its neighbours outside the new community re-enter the queue.
+ *   refine: singletons; in random order a node still alone joins the neighbour refined
+ *     community inside its own move-phase community of largest positive gain.
+ *   aggregate by the refined partition, every aggregate node starting in the move-phase
+ *     community of its members; repeat while the refinement merged anything.
+ * Gains in exact int64 (w_vc*2M - k_v*Sigma_c): integer weights.  Output labels are
+ * renumbered 0..k-1 by first node (leidenalg orders communities by size; the host layer
+ * does that for both the oracle and the engine).  Returns the number of levels. */
+typedef struct { i64 n; i64* rp; i32* col; i64* w; i64* kv; } ld_graph;
+
+static void ld_free(ld_graph* g) { free(g->rp); free(g->col); free(g->w); free(g->kv); }
+
+static void ld_move(const ld_graph* g, i64 M2, i32* P, i64* tot, i32* csize, u64* s, i64* nw, u8* seen,
+                    i32* cands) {
+    const i64 n = g->n;
+    i32* q = (i32*)malloc(sizeof(i32) * (size_t)(n ? n : 1));
+    u8* inq = (u8*)calloc((size_t)n + 1, 1);
+    i32* empt = (i32*)malloc(sizeof(i32) * (size_t)(n ? n : 1));
+    i64 ne = 0;
+    for (i64 c = 0; c < n; ++c) if (csize[c] == 0) empt[ne++] = (i32)c;
+    for (i64 i = 0; i < n; ++i) { q[i] = (i32)i; inq[i] = 1; }
+    shuffle_i32(q, n, s);
+    i64 head = 0, len = n;
+    while (len > 0) {
+        const i32 v = q[head];
+        head = (head + 1 == n) ? 0 : head + 1;
+        --len;
+        inq[v] = 0;
+        const i32 own = P[v];
+        const i64 kv = g->kv[v];
+        i64 nc = 0;
+        for (i64 j = g->rp[v]; j < g->rp[v + 1]; ++j) {
+            const i32 c = P[g->col[j]];
+            if (!seen[c]) { seen[c] = 1; nw[c] = 0; cands[nc++] = c; }
+            nw[c] += g->w[j];
+        }
+        const i64 wown = seen[own] ? nw[own] : 0;
+        i32 best = own;
+        long long bs = (long long)wown * M2 - (long long)kv * (tot[own] - kv);
+        shuffle_i32(cands, nc, s);
+        for (i64 k = 0; k < nc; ++k) {
+            const i32 c = cands[k];
+            if (c == own) continue;
+            const long long sc = (long long)nw[c] * M2 - (long long)kv * tot[c];
+            if (sc > bs) { bs = sc; best = c; }
+        }
+        for (i64 k = 0; k < nc; ++k) seen[cands[k]] = 0;
+        if (csize[own] > 1 && bs < 0 && ne > 0) { best = empt[ne - 1]; bs = 0; }   /* the empty community */
+        if (best == own) continue;
+        if (csize[best] == 0) --ne;   /* best was the empty community on the stack top */
+        tot[own] -= kv; tot[best] += kv;
+        csize[own]--; csize[best]++;
+        P[v] = best;
+        if (csize[own] == 0) empt[ne++] = own;
+        for (i64 j = g->rp[v]; j < g->rp[v + 1]; ++j) {
+            const i32 u = g->col[j];
+            if (P[u] != best && !inq[u]) {
+                i64 tail = head + len;
+                if (tail >= n) tail -= n;
+                q[tail] = u; inq[u] = 1; ++len;
+            }
+        }
+    }
+    free(q); free(inq); free(empt);
+}
+
+/* one refinement pass; returns the number of refined communities */
+static i64 ld_refine(const ld_graph* g, i64 M2, const i32* P, i32* R, i64* rtot, i32* rsize, u64* s, i64* nw,
+                     u8* seen, i32* cands, i32* order) {
+    const i64 n = g->n;
+    for (i64 v = 0; v < n; ++v) { R[v] = (i32)v; rtot[v] = g->kv[v]; rsize[v] = 1; order[v] = (i32)v; }
+    shuffle_i32(order, n, s);
+    i64 ncom = n;
+    for (i64 t = 0; t < n; ++t) {
+        const i32 v = order[t];
+        if (rsize[R[v]] != 1) continue;
+        const i64 kv = g->kv[v];
+        i64 nc = 0;
+        for (i64 j = g->rp[v]; j < g->rp[v + 1]; ++j) {
+            const i32 u = g->col[j];
+            if (P[u] != P[v]) continue;
+            const i32 c = R[u];
+            if (!seen[c]) { seen[c] = 1; nw[c] = 0; cands[nc++] = c; }
+            nw[c] += g->w[j];
+        }
+        i32 best = -1;
+        long long bs = 0;
+        shuffle_i32(cands, nc, s);
+        for (i64 k = 0; k < nc; ++k) {
+            const i32 c = cands[k];
+            if (c == R[v]) continue;
+            const long long sc = (long long)nw[c] * M2 - (long long)kv * rtot[c];
+            if (sc > bs) { bs = sc; best = c; }
+        }
+        for (i64 k = 0; k < nc; ++k) seen[cands[k]] = 0;
+        if (best < 0) continue;
+        const i32 old = R[v];
+        rtot[old] -= kv; rsize[old]--;
+        rtot[best] += kv; rsize[best]++;
+        R[v] = best;
+        --ncom;
+    }
+    return ncom;
+}
+
+int orc_leiden(i64 N, const i64* rowptr, const i32* col, const i32* w, u64 seed, i32* lab) {
+    u64 s = seed ^ 0x2545F4914F6CDD1Dull;
+    ld_graph g;
+    g.n = N;
+    g.rp = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    const i64 E = rowptr[N];
+    g.col = (i32*)malloc(sizeof(i32) * (size_t)(E ? E : 1));
+    g.w = (i64*)malloc(sizeof(i64) * (size_t)(E ? E : 1));
+    g.kv = (i64*)calloc((size_t)(N ? N : 1), sizeof(i64));
+    i64 M2 = 0;
+    for (i64 v = 0; v <= N; ++v) g.rp[v] = rowptr[v];
+    for (i64 v = 0; v < N; ++v)
+        for (i64 j = rowptr[v]; j < rowptr[v + 1]; ++j) {
+            g.col[j] = col[j]; g.w[j] = w ? w[j] : 1; g.kv[v] += g.w[j]; M2 += g.w[j];
+        }
+    const size_t nn = (size_t)(N ? N : 1);
+    i32* P = (i32*)malloc(sizeof(i32) * nn);
+    i32* R = (i32*)malloc(sizeof(i32) * nn);
+    i64* tot = (i64*)malloc(sizeof(i64) * nn);
+    i64* rtot = (i64*)malloc(sizeof(i64) * nn);
+    i32* csize = (i32*)malloc(sizeof(i32) * nn);
+    i32* rsize = (i32*)malloc(sizeof(i32) * nn);
+    i64* nw = (i64*)malloc(sizeof(i64) * nn);
+    u8* seen = (u8*)calloc(nn, 1);
+    i32* cands = (i32*)malloc(sizeof(i32) * nn);
+    i32* order = (i32*)malloc(sizeof(i32) * nn);
+    i32* memb = (i32*)malloc(sizeof(i32) * nn);
+    i32* nid = (i32*)malloc(sizeof(i32) * nn);
+    i32* prep = (i32*)malloc(sizeof(i32) * nn);
+    for (i64 v = 0; v < N; ++v) { P[v] = (i32)v; tot[v] = g.kv[v]; csize[v] = 1; memb[v] = (i32)v; }
+    int levels = 0;
+    while (1) {
+        ++levels;
+        ld_move(&g, M2, P, tot, csize, &s, nw, seen, cands);
+        const i64 nR = ld_refine(&g, M2, P, R, rtot, rsize, &s, nw, seen, cands, order);
+        if (nR == g.n || levels >= 64) break;
+        /* aggregate by R: new ids in refined-community id order */
+        i64 k = 0;
+        for (i64 c = 0; c < g.n; ++c) nid[c] = rsize[c] > 0 ? (i32)k++ : -1;
+        for (i64 c = 0; c < g.n; ++c) prep[c] = INT32_MAX;
+        for (i64 v = 0; v < g.n; ++v) if (nid[R[v]] < prep[P[v]]) prep[P[v]] = nid[R[v]];
+        ld_graph h;
+        h.n = k;
+        h.rp = (i64*)calloc((size_t)k + 1, sizeof(i64));
+        h.kv = (i64*)calloc((size_t)(k ? k : 1), sizeof(i64));
+        i32* np = (i32*)malloc(sizeof(i32) * (size_t)(k ? k : 1));
+        /* members of each new node (counting sort) */
+        i64* moff = (i64*)calloc((size_t)k + 1, sizeof(i64));
+        i32* ml = (i32*)malloc(sizeof(i32) * (size_t)(g.n ? g.n : 1));
+        for (i64 v = 0; v < g.n; ++v) moff[nid[R[v]] + 1]++;
+        for (i64 x = 0; x < k; ++x) moff[x + 1] += moff[x];
+        i64* cur = (i64*)malloc(sizeof(i64) * (size_t)(k ? k : 1));
+        for (i64 x = 0; x < k; ++x) cur[x] = moff[x];
+        for (i64 v = 0; v < g.n; ++v) ml[cur[nid[R[v]]]++] = (i32)v;
+        i64 cap = g.rp[g.n] ? g.rp[g.n] : 1;
+        h.col = (i32*)malloc(sizeof(i32) * (size_t)cap);
+        h.w = (i64*)malloc(sizeof(i64) * (size_t)cap);
+        i64 e = 0;
+        for (i64 x = 0; x < k; ++x) {
+            i64 nc = 0;
+            for (i64 q = moff[x]; q < moff[x + 1]; ++q) {
+                const i32 v = ml[q];
+                h.kv[x] += g.kv[v];
+                np[x] = prep[P[v]];
+                for (i64 j = g.rp[v]; j < g.rp[v + 1]; ++j) {
+                    const i32 y = nid[R[g.col[j]]];
+                    if (y == x) continue;
+                    if (!seen[y]) { seen[y] = 1; nw[y] = 0; cands[nc++] = y; }
+                    nw[y] += g.w[j];
+                }
+            }
+            /* rows sorted by column (canonical) */
+            for (i64 a = 1; a < nc; ++a) {
+                i32 t = cands[a]; i64 b = a - 1;
+                while (b >= 0 && cands[b] > t) { cands[b + 1] = cands[b]; --b; }
+                cands[b + 1] = t;
+            }
+            for (i64 q = 0; q < nc; ++q) { h.col[e] = cands[q]; h.w[e] = nw[cands[q]]; ++e; seen[cands[q]] = 0; }
+            h.rp[x + 1] = e;
+        }
+        for (i64 v = 0; v < N; ++v) memb[v] = nid[R[memb[v]]];
+        for (i64 x = 0; x < k; ++x) { P[x] = np[x]; tot[x] = 0; csize[x] = 0; }
+        for (i64 x = 0; x < k; ++x) { tot[P[x]] += h.kv[x]; csize[P[x]]++; }
+        free(np); free(moff); free(ml); free(cur);
+        ld_free(&g);
+        g = h;
+    }
+    for (i64 v = 0; v < N; ++v) lab[v] = P[memb[v]];
+    renumber(N, lab, nid);
+    ld_free(&g);
+    free(P); free(R); free(tot); free(rtot); free(csize); free(rsize); free(nw); free(seen); free(cands);
+    free(order); free(memb); free(nid); free(prep);
+    return levels;
+}
+
 /* Batch helper: n_r independent runs (replicas) in parallel over host threads.
- * algo 0 = louvain level 0, 1 = lpa.  lab is [n_r][N]. */
+ * algo 0 = louvain level 0, 1 = lpa, 3 = leiden.  lab is [n_r][N]. */
 void orc_cd_batch(int algo, int n_r, i64 N, const i64* rowptr, const i32* col, const i32* w,
                   u64 seed, i32* lab, int* sweeps, int nthreads) {
 #ifdef _OPENMP
@@ -404,8 +612,9 @@ void orc_cd_batch(int algo, int n_r, i64 N, const i64* rowptr, const i32* col, c
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         u64 sd = seed * 0x9E3779B97F4A7C15ull + (u64)r * 0xC2B2AE3D27D4EB4Full + 1;
-        int sw = algo == 0 ? orc_louvain_level0(N, rowptr, col, w, sd, lab + (i64)r * N)
-                           : orc_lpa(N, rowptr, col, sd, lab + (i64)r * N, 10000);
+        int sw = algo == 0   ? orc_louvain_level0(N, rowptr, col, w, sd, lab + (i64)r * N)
+                 : algo == 3 ? orc_leiden(N, rowptr, col, w, sd, lab + (i64)r * N)
+                             : orc_lpa(N, rowptr, col, sd, lab + (i64)r * N, 10000);
         if (sweeps) sweeps[r] = sw;
     }
 }

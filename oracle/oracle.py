@@ -24,12 +24,12 @@ _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
 _lib = None
 
-LOUVAIN, LPM, LOUVAIN_NC = 0, 1, 2   # LOUVAIN_NC: louvain with new_consensus.py's rule (:155-163)
+LOUVAIN, LPM, LOUVAIN_NC, LEIDEN = 0, 1, 2, 3   # LOUVAIN_NC: louvain with new_consensus.py's rule (:155-163)
 
 
 def _cd_algo(algo):
     """Community-detection algorithm of a loop variant (the new_consensus.py rule runs Louvain)."""
-    return LPM if algo == LPM else LOUVAIN
+    return algo if algo in (LPM, LEIDEN) else LOUVAIN
 AGE_ITER_SHIFT = 40          # closure/repair edges created in iteration b get ages >= (b+1) << 40
 AGE_REPAIR_OFFSET = 1 << 39
 
@@ -64,6 +64,8 @@ def lib():
         L.orc_louvain_level0.argtypes = [i64, _i64p, _i32p, _i32p, u64, _i32p]
         L.orc_louvain_level0.restype = ctypes.c_int
         L.orc_lpa.argtypes = [i64, _i64p, _i32p, u64, _i32p, ctypes.c_int]
+        L.orc_leiden.argtypes = [i64, _i64p, _i32p, ctypes.c_void_p, u64, _i32p]
+        L.orc_leiden.restype = ctypes.c_int
         L.orc_lpa.restype = ctypes.c_int
         L.orc_cd_batch.argtypes = [ctypes.c_int, ctypes.c_int, i64, _i64p, _i32p, _i32p, u64, _i32p, _i32p,
                                    ctypes.c_int]
