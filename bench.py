@@ -45,6 +45,11 @@ CONFIGS = {
     # configs[1] (C2)
     "lfr1k": dict(kind="lfr", n=1_000, mu=0.4, algo="louvain", n_p=20, tau=0.2, delta=0.02,
                   desc="LFR n=1,000 mu=0.4, louvain n_p=20"),
+    # the leiden branch (fast_consensus.py:204-258) on the C4 / C3 graphs
+    "lfr1m_leiden": dict(kind="lfr", n=1_000_000, mu=0.5, algo="leiden", n_p=64, tau=0.2, delta=0.02,
+                         desc="LFR n=1,000,000 mu=0.5, leiden n_p=64"),
+    "lfr100k_leiden": dict(kind="lfr", n=100_000, mu=0.5, algo="leiden", n_p=64, tau=0.2, delta=0.02,
+                           desc="LFR n=100,000 mu=0.5, leiden n_p=64"),
     # configs[4] (C5)
     "sbm4m": dict(kind="sbm", n=4_000_000, algo="lpm", n_p=128, tau=0.8, delta=0.02,
                   desc="SBM n=4,000,000 blocks of 100, ~40M edges, lpm n_p=128"),
@@ -108,10 +113,22 @@ def cpu_baseline(n, u, v, cfg, seed):
     consensus parts by ceil(n_p / threads) and n_p / threads."""
     from oracle import oracle as orc
     threads = host_cpu_share()
-    algo = 0 if cfg["algo"] == "louvain" else 1
     n_p = cfg["n_p"]
     reps = max(1, min(n_p, threads))
     g = orc.EdgeGraph.from_lines(n, np.stack([u, v], 1))
+    if cfg["algo"] == "leiden":
+        # the leiden branch on integer nodes is n_p Leiden runs on G (fc_run, capi.cpp)
+        t0 = time.perf_counter()
+        orc.cd_batch(orc.LEIDEN, reps, g, seed=seed, nthreads=threads)
+        cd_s = time.perf_counter() - t0
+        full_s = cd_s * math.ceil(n_p / reps)
+        return {"value": n_p * g.m / full_s, "unit": "partition·edges/s", "cores": threads, "kind": "port",
+                "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "iteration_s": full_s,
+                "sample_s": cd_s,
+                "sample": "%d sequential Leiden runs (orc_leiden, the leidenalg restatement) in parallel on %d "
+                          "threads (%s) %.2fs; value = n_p*m / (that time x ceil(n_p/threads)=%d) at n_p=%d"
+                          % (reps, threads, cpu_model(), cd_s, math.ceil(n_p / reps), n_p)}
+    algo = 0 if cfg["algo"] == "louvain" else 1
     t = {}
     t0 = time.perf_counter()
     lab, _ = orc.cd_batch(algo, reps, g, seed=seed, nthreads=threads)

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <vector>
 
@@ -39,8 +40,10 @@ template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
 namespace {
 
 constexpr int LTB = 256;          // threads per block (4 waves)
-constexpr int LWS = 256;          // LDS hash slots per wave
-constexpr int LIGHT = 128;        // rows / member-row sums above this go to the block-per-vertex kernels
+constexpr int LWS = 1024;         // LDS hash slots per wave (a table is sized to its row: 64..LWS)
+constexpr int LIGHT = LWS / 2;    // rows / member-row sums above this go to the block-per-vertex kernels
+constexpr int HLS = 8192;         // LDS slots of a block-per-vertex table
+constexpr int HLIGHT = HLS / 2;   // longer rows use a global table
 constexpr int MODE_MOVE = 0, MODE_REFINE = 1;
 constexpr int MSH = 256;          // move-counter shards
 constexpr int MAX_LEVELS = 64;
@@ -77,6 +80,7 @@ struct LvArgs {
     int32_t* hlst;            // [LHB][hslots] created slots
     int64_t hslots;
     unsigned long long* moves;   // [MSH]
+    unsigned long long* mvt;     // [nU] move phase: (bucket stamp << 32) | target of this bucket's movers
 };
 
 template <bool IMPL> __device__ __forceinline__ int32_t rep_of(const LvArgs& a, int64_t x) {
@@ -131,11 +135,45 @@ __device__ __forceinline__ int32_t lv_final(const LvArgs& a, int64_t x, int32_t 
     return t;
 }
 
+// Table size for a row of d entries: the power of two >= 2d, at least 64.
+__device__ __forceinline__ uint32_t tsize(int64_t d) {
+    uint32_t t = 64;
+    while ((int64_t)t < 2 * d) t <<= 1;
+    return t;
+}
+
+// Wave-level candidate scan over table slots [0, ts): best (score, tie, community) and the
+// weight to the own community, reduced over the wave.
+__device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
+                                          int32_t own, long long kvx, int32_t r, int64_t x, long long& bs,
+                                          uint32_t& bh, int32_t& bc, long long& wown) {
+    const int lane = threadIdx.x & 63;
+    bs = LLONG_MIN; bh = 0; bc = -1; wown = 0;
+    for (uint32_t s = lane; s < ts; s += 64) {
+        const int32_t k = keys[s];
+        if (k < 0) continue;
+        const long long val = vals[s];
+        if (k == own) { wown = val; continue; }
+        const long long sc = val * a.M2 - kvx * a.tot[k];
+        const uint32_t h = tie_of(a, r, x, k);
+        if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
+    }
+    for (int off = 32; off; off >>= 1) {
+        const long long s2 = __shfl_xor(bs, off);
+        const uint32_t h2 = __shfl_xor(bh, off);
+        const int32_t c2 = __shfl_xor(bc, off);
+        wown += __shfl_xor(wown, off);
+        if (lv_better(s2, h2, c2, bs, bh, bc)) { bs = s2; bh = h2; bc = c2; }
+    }
+}
+
 // One bucket's decisions.  Each lane owns one union vertex; a wave ballots the eligible
-// ones and decides them one at a time cooperatively (row over the 64 lanes, 256-slot LDS
-// table).  Rows longer than LIGHT go to k_lv_heavy.  Movers are listed per block.
+// ones and decides them one at a time cooperatively: the row over the 64 lanes into an LDS
+// table sized for it (64..LWS slots).  Rows longer than LIGHT go to k_lv_heavy.  Movers are
+// listed per block and stamped in mvt (the apply kernel decides the neighbours' queue
+// flags from the bucket's final state, so the result does not depend on thread timing).
 template <bool IMPL, int MODE>
-__global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket) {
+__global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_t stamp) {
     __shared__ int32_t skey[LTB / 64][LWS], sval[LTB / 64][LWS];
     __shared__ int s_cnt;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -168,7 +206,8 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket) {
             if (lane == 0) a.heavy[atomicAdd(a.heavy_cnt, 1)] = (int32_t)x;
             continue;
         }
-        for (int s = lane; s < LWS; s += 64) { keys[s] = -1; vals[s] = 0; }
+        const uint32_t ts = tsize(re - rb);
+        for (uint32_t s = lane; s < ts; s += 64) { keys[s] = -1; vals[s] = 0; }
         wsync();
         const int32_t own = MODE == MODE_MOVE ? a.P[x] : a.R[x];
         const int32_t pc = a.P[x];
@@ -176,36 +215,21 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket) {
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
-            tins(keys, vals, LWS, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
+            tins(keys, vals, ts, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
         }
         wsync();
         const long long kvx = kv_of<IMPL>(a, x);
-        const int32_t r = rep_of<IMPL>(a, x);
-        long long bs = LLONG_MIN, wown = 0;
-        uint32_t bh = 0;
-        int32_t bc = -1;
-        for (int s = lane; s < LWS; s += 64) {
-            const int32_t k = keys[s];
-            if (k < 0) continue;
-            const long long val = vals[s];
-            if (k == own) { wown = val; continue; }
-            const long long sc = val * a.M2 - kvx * a.tot[k];
-            const uint32_t h = tie_of(a, r, x, k);
-            if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
-        }
-        for (int off = 32; off; off >>= 1) {
-            const long long s2 = __shfl_xor(bs, off);
-            const uint32_t h2 = __shfl_xor(bh, off);
-            const int32_t c2 = __shfl_xor(bc, off);
-            wown += __shfl_xor(wown, off);
-            if (lv_better(s2, h2, c2, bs, bh, bc)) { bs = s2; bh = h2; bc = c2; }
-        }
+        long long bs, wown;
+        uint32_t bh;
+        int32_t bc;
+        wave_scan(a, keys, vals, ts, own, kvx, rep_of<IMPL>(a, x), x, bs, bh, bc, wown);
         if (lane == 0) {
             const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
             if (t >= 0) {
                 const int p = atomicAdd(&s_cnt, 1);
                 a.blist[(int64_t)blockIdx.x * LTB + p] = (int32_t)x;
                 a.btgt[(int64_t)blockIdx.x * LTB + p] = t;
+                if (MODE == MODE_MOVE) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
             }
         }
         wsync();
@@ -241,32 +265,38 @@ __device__ __forceinline__ void block_best(BRed& red, long long& bs, uint32_t& b
     __syncthreads();
 }
 
-// Long rows: one block per vertex over a global hash table (one table per block, cleared
-// through the list of slots it created).
+// Long rows: one block per vertex; an LDS table of up to HLS slots, or (rows > HLIGHT) a
+// global table per block, cleared through the list of slots it created.
 template <bool IMPL, int MODE>
-__global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a) {
+__global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
+    __shared__ int32_t lkey[HLS], lval[HLS];
     __shared__ int s_n;
     __shared__ BRed red;
     const int n = *a.heavy_cnt;
-    int32_t* keys = a.hkey + (int64_t)blockIdx.x * a.hslots;
-    int32_t* vals = a.hval + (int64_t)blockIdx.x * a.hslots;
+    int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
+    int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
     int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
-    const uint32_t ns = (uint32_t)a.hslots;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t x = a.heavy[i];
-        if (threadIdx.x == 0) s_n = 0;
-        __syncthreads();
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
         const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
+        const bool lds = re - rb <= HLIGHT;
+        const uint32_t ts = lds ? tsize(re - rb) : (uint32_t)a.hslots;
+        int32_t* keys = lds ? lkey : gkey;
+        int32_t* vals = lds ? lval : gval;
+        if (threadIdx.x == 0) s_n = 0;
+        if (lds)
+            for (uint32_t s = threadIdx.x; s < ts; s += LTB) { lkey[s] = -1; lval[s] = 0; }
+        __syncthreads();
         const int32_t own = MODE == MODE_MOVE ? a.P[x] : a.R[x];
         const int32_t pc = a.P[x];
         for (int64_t j = rb + threadIdx.x; j < re; j += LTB) {
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
-            const int s = tins(keys, vals, ns, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
-            if (s >= 0) lst[atomicAdd(&s_n, 1)] = s;
+            const int s = tins(keys, vals, ts, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
+            if (!lds && s >= 0) lst[atomicAdd(&s_n, 1)] = s;
         }
         __syncthreads();
         const long long kvx = kv_of<IMPL>(a, x);
@@ -274,67 +304,79 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a) {
         long long bs = LLONG_MIN, wown = 0;
         uint32_t bh = 0;
         int32_t bc = -1;
-        const int cnt = s_n;
+        const int cnt = lds ? (int)ts : s_n;
         for (int q = threadIdx.x; q < cnt; q += LTB) {
-            const int s = lst[q];
+            const int s = lds ? q : lst[q];
             const int32_t k = keys[s];
+            if (k < 0) continue;
             const long long val = vals[s];
-            keys[s] = -1; vals[s] = 0;   // clear for the next vertex (read before)
+            if (!lds) { gkey[s] = -1; gval[s] = 0; }   // clear for the next vertex (read before)
             if (k == own) { wown = val; continue; }
             const long long sc = val * a.M2 - kvx * a.tot[k];
             const uint32_t h = tie_of(a, r, x, k);
             if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
         }
         block_best(red, bs, bh, bc, wown);
-        if (threadIdx.x == 0) a.htgt[i] = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
+        if (threadIdx.x == 0) {
+            const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
+            a.htgt[i] = t;
+            if (MODE == MODE_MOVE && t >= 0) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
+        }
         __syncthreads();
     }
 }
 
-// Apply one bucket's moves: blocks [0, nblk) take the decide blocks' lists, the rest the
-// heavy decisions.  Move phase: P, Sigma, and the queue (neighbours outside the new
-// community); refine: R, Sigma and sizes.
+// Apply one bucket's moves, one wave per mover: blocks [0, nblk) take the decide blocks'
+// lists, the rest the heavy decisions.  Lane 0 moves the vertex (move phase: P and Sigma;
+// refine: R, Sigma and sizes); in the move phase the lanes then queue the neighbours whose
+// community at the END of the bucket differs from the target (a neighbour that moves in
+// this bucket is judged by its stamped target, the others by P, which this bucket leaves
+// alone), so the queue flags do not depend on thread timing.
 template <bool IMPL, int MODE>
-__device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, unsigned long long& mv) {
-    const long long kvx = kv_of<IMPL>(a, x);
-    if (MODE == MODE_MOVE) {
-        const int32_t old = a.P[x];
-        a.P[x] = t;
+__device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, uint32_t stamp, unsigned long long& mv) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        const long long kvx = kv_of<IMPL>(a, x);
+        int32_t* lab = MODE == MODE_MOVE ? a.P : a.R;
+        const int32_t old = lab[x];
+        lab[x] = t;
         atomicAdd((unsigned long long*)&a.tot[t], (unsigned long long)kvx);
         atomicAdd((unsigned long long*)&a.tot[old], (unsigned long long)(-kvx));
+        if (MODE == MODE_REFINE) {
+            atomicAdd(&a.rsize[t], 1);
+            atomicAdd(&a.rsize[old], -1);
+        }
+        ++mv;
+    }
+    if (MODE == MODE_MOVE) {
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
-        for (int64_t j = a.rowptr[xr]; j < a.rowptr[xr + 1]; ++j) {
+        const int64_t re = a.rowptr[xr + 1];
+        for (int64_t j = a.rowptr[xr] + lane; j < re; j += 64) {
             const int64_t y = base + a.col[j];
-            if (a.P[y] != t) a.act[y] = 1;
+            const unsigned long long my = a.mvt[y];
+            const int32_t fin = (uint32_t)(my >> 32) == stamp ? (int32_t)(uint32_t)my : a.P[y];
+            if (fin != t) a.act[y] = 1;
         }
-    } else {
-        const int32_t old = a.R[x];
-        a.R[x] = t;
-        atomicAdd((unsigned long long*)&a.tot[t], (unsigned long long)kvx);
-        atomicAdd((unsigned long long*)&a.tot[old], (unsigned long long)(-kvx));
-        atomicAdd(&a.rsize[t], 1);
-        atomicAdd(&a.rsize[old], -1);
     }
-    ++mv;
 }
 template <bool IMPL, int MODE>
-__global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk) {
+__global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk, uint32_t stamp) {
     unsigned long long mv = 0;
+    const int wv = threadIdx.x >> 6;
     if ((int)blockIdx.x < nblk) {
         const int n = a.bcnt[blockIdx.x];
-        if ((int)threadIdx.x < n) {
-            const int64_t q = (int64_t)blockIdx.x * LTB + threadIdx.x;
-            lv_move<IMPL, MODE>(a, a.blist[q], a.btgt[q], mv);
+        for (int i = wv; i < n; i += LTB / 64) {
+            const int64_t q = (int64_t)blockIdx.x * LTB + i;
+            lv_move<IMPL, MODE>(a, a.blist[q], a.btgt[q], stamp, mv);
         }
     } else {
         const int n = *a.heavy_cnt;
-        for (int i = (blockIdx.x - nblk) * LTB + threadIdx.x; i < n; i += hblk * LTB) {
+        for (int i = (blockIdx.x - nblk) * (LTB / 64) + wv; i < n; i += hblk * (LTB / 64)) {
             const int32_t t = a.htgt[i];
-            if (t >= 0) lv_move<IMPL, MODE>(a, a.heavy[i], t, mv);
+            if (t >= 0) lv_move<IMPL, MODE>(a, a.heavy[i], t, stamp, mv);
         }
     }
-    for (int off = 32; off; off >>= 1) mv += __shfl_xor(mv, off);
     if ((threadIdx.x & 63) == 0 && mv) atomicAdd(&a.moves[blockIdx.x & (MSH - 1)], mv);
 }
 
@@ -435,7 +477,8 @@ __global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const in
     }
     int32_t* keys = skey[wv];
     int32_t* vals = sval[wv];
-    for (int s = lane; s < LWS; s += 64) { keys[s] = -1; vals[s] = 0; }
+    const uint32_t ts = tsize(ubo[xn + 1] - ubo[xn]);
+    for (uint32_t s = lane; s < ts; s += 64) { keys[s] = -1; vals[s] = 0; }
     wsync();
     for (int32_t q = moff[xn]; q < moff[xn + 1]; ++q) {
         const int64_t x = mlist[q];
@@ -443,13 +486,13 @@ __global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const in
         const int64_t xr = IMPL ? x - base : x;
         for (int64_t j = a.rowptr[xr] + lane; j < a.rowptr[xr + 1]; j += 64) {
             const int32_t yn = nid[a.R[base + a.col[j]]];
-            if (yn != (int32_t)xn) tins(keys, vals, LWS, true, yn, a.w ? a.w[j] : 1);
+            if (yn != (int32_t)xn) tins(keys, vals, ts, true, yn, a.w ? a.w[j] : 1);
         }
     }
     wsync();
     int32_t cnt = 0;
     const int64_t o = ubo[xn];
-    for (int s0 = 0; s0 < LWS; s0 += 64) {
+    for (uint32_t s0 = 0; s0 < ts; s0 += 64) {
         const int32_t k = keys[s0 + lane];
         const unsigned long long bal = __ballot(k >= 0);
         if (k >= 0) {
@@ -466,15 +509,22 @@ __global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* 
                                                        const int32_t* mlist, const int64_t* ubo, int32_t* ocol,
                                                        int32_t* ow, int32_t* olen, const int32_t* hlist,
                                                        const int32_t* hcnt) {
+    __shared__ int32_t lkey[HLS], lval[HLS];
     __shared__ int s_n;
     const int n = *hcnt;
-    int32_t* keys = a.hkey + (int64_t)blockIdx.x * a.hslots;
-    int32_t* vals = a.hval + (int64_t)blockIdx.x * a.hslots;
+    int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
+    int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
     int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
-    const uint32_t ns = (uint32_t)a.hslots;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t xn = hlist[i];
+        const int64_t ubn = ubo[xn + 1] - ubo[xn];
+        const bool lds = ubn <= HLIGHT;
+        const uint32_t ts = lds ? tsize(ubn) : (uint32_t)a.hslots;
+        int32_t* keys = lds ? lkey : gkey;
+        int32_t* vals = lds ? lval : gval;
         if (threadIdx.x == 0) s_n = 0;
+        if (lds)
+            for (uint32_t s = threadIdx.x; s < ts; s += LTB) { lkey[s] = -1; lval[s] = 0; }
         __syncthreads();
         for (int32_t q = moff[xn]; q < moff[xn + 1]; ++q) {
             const int64_t x = mlist[q];
@@ -483,20 +533,31 @@ __global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* 
             for (int64_t j = a.rowptr[xr] + threadIdx.x; j < a.rowptr[xr + 1]; j += LTB) {
                 const int32_t yn = nid[a.R[base + a.col[j]]];
                 if (yn == (int32_t)xn) continue;
-                const int s = tins(keys, vals, ns, true, yn, a.w ? a.w[j] : 1);
-                if (s >= 0) lst[atomicAdd(&s_n, 1)] = s;
+                const int s = tins(keys, vals, ts, true, yn, a.w ? a.w[j] : 1);
+                if (!lds && s >= 0) lst[atomicAdd(&s_n, 1)] = s;
             }
         }
         __syncthreads();
-        const int cnt = s_n;
         const int64_t o = ubo[xn];
-        for (int q = threadIdx.x; q < cnt; q += LTB) {
-            const int s = lst[q];
-            ocol[o + q] = keys[s];
-            ow[o + q] = vals[s];
-            keys[s] = -1; vals[s] = 0;
+        if (lds) {   // every slot of the LDS table; output positions from a block counter
+            if (threadIdx.x == 0) s_n = 0;
+            __syncthreads();
+            for (uint32_t q = threadIdx.x; q < ts; q += LTB) {
+                if (lkey[q] < 0) continue;
+                const int p = atomicAdd(&s_n, 1);
+                ocol[o + p] = lkey[q];
+                ow[o + p] = lval[q];
+            }
+        } else {     // the global table through its created-slot list, cleared on the way
+            for (int q = threadIdx.x; q < s_n; q += LTB) {
+                const int s = lst[q];
+                ocol[o + q] = gkey[s];
+                ow[o + q] = gval[s];
+                gkey[s] = -1; gval[s] = 0;
+            }
         }
-        if (threadIdx.x == 0) olen[xn] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) olen[xn] = s_n;
         __syncthreads();
     }
 }
@@ -504,7 +565,8 @@ __global__ void k_ag_len64(int64_t n, const int32_t* len, int64_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) out[i] = i < n ? len[i] : 0;
 }
-// compact rows (sorted by column, so rows are canonical and deterministic)
+// compact rows (entry order inside a row is the hash tables' and may vary between runs; no
+// decision depends on it: table sums commute and candidates are ranked by a total order)
 __global__ __launch_bounds__(LTB) void k_ag_compact(int64_t nUn, const int64_t* ubo, const int64_t* rp,
                                                     const int32_t* icol, const int32_t* iw, int32_t* ocol,
                                                     int32_t* ow) {
@@ -541,7 +603,7 @@ __global__ void k_lv_fill_u8(int64_t n, uint8_t* p, const uint8_t* done, const i
 // Buffers (Ctx::lv).
 enum {
     B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
-    B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC,
+    B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC, B_MVT,
     // aggregation scratch
     B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
     // explicit level graphs, ping-pong: rowptr, col, w, kv, rep (x2)
@@ -626,12 +688,15 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
     FC_HIP(hipMemcpyAsync(roff, h_roff.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
     FC_HIP(hipMemcpyAsync(rend, h_rend.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
     std::vector<uint8_t> h_done(n_r, 0);
+    uint32_t stamp_ctr = 0;
     std::vector<uint32_t> h_rkey(n_r);
 
     LvArgs a{};
     a.N0 = N; a.M2 = g.M2; a.B = B;
     a.roff = roff; a.rkey = rkey; a.done = done; a.moves = moves;
     a.heavy_cnt = hcnt;
+    a.mvt = (unsigned long long*)I64(B_MVT, nU0);
+    FC_HIP(hipMemsetAsync(a.mvt, 0, 8 * (size_t)nU0, c.stream));
 
     LvGraph cur;            // explicit level (level >= 1)
     int pp = 0;             // ping-pong slot of the next explicit level
@@ -660,8 +725,9 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         a.bcnt = I32(B_BCNT, nblk);
         a.heavy = I32(B_HEAVY, nU);
         a.htgt = I32(B_HTGT, nU);
-        int64_t hs = 1;
-        while (hs < 2 * (int64_t)std::max(max_deg, 1)) hs <<= 1;
+        int64_t hs = 64;   // global tables only for rows beyond the block's LDS table
+        if (max_deg > HLIGHT)
+            while (hs < 2 * (int64_t)max_deg) hs <<= 1;
         a.hslots = hs;
     };
     // heavy-kernel grid: one global table per block, bounded to ~2 GB of tables
@@ -687,12 +753,13 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         const int hg = heavy_grid(a.hslots);
         const int hblk = 64;
         for (int b = 0; b < B; ++b) {
+            const uint32_t stamp = ++stamp_ctr;   // unique per bucket launch of this run (mvt)
             FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
 #define LV_LAUNCH(IM, MD)                                                                        \
     do {                                                                                         \
-        k_lv_decide<IM, MD><<<nblk, LTB, 0, c.stream>>>(a, b);                                   \
-        if (max_deg > LIGHT) k_lv_heavy<IM, MD><<<hg, LTB, 0, c.stream>>>(a);                    \
-        k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk); \
+        k_lv_decide<IM, MD><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);                            \
+        if (max_deg > LIGHT) k_lv_heavy<IM, MD><<<hg, LTB, 0, c.stream>>>(a, stamp);             \
+        k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
             if (impl && MODE == MODE_MOVE) LV_LAUNCH(true, MODE_MOVE);
             else if (impl) LV_LAUNCH(true, MODE_REFINE);
@@ -801,8 +868,9 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         if (impl) k_ag_rows<true><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
         else k_ag_rows<false><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
         if (ubmax > LIGHT) {
-            int64_t hs = 1;
-            while (hs < 2 * ubmax) hs <<= 1;
+            int64_t hs = 64;
+            if (ubmax > HLIGHT)
+                while (hs < 2 * ubmax) hs <<= 1;
             a.hslots = hs;
             const int hg = heavy_grid(hs);
             if (impl) k_ag_rows_heavy<true><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
@@ -845,9 +913,19 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         k_lv_fill_u8<<<nb(nU), LTB, 0, c.stream>>>(nU, act, done, cur.rep);
         set_graph();
         a.P = P; a.R = R; a.tot = ptot; a.rsize = rsize; a.act = act;
-        for (int sw = 0; sw < c.max_sweeps; ++sw) {
+        int sw = 0;
+        for (; sw < c.max_sweeps; ++sw) {
             ++lv_sweeps;
             if (sweep(MODE_MOVE, level + 1, sw + 1) == 0) break;
+        }
+        if (c.trace) {
+            sync(c);
+            static auto t_last = std::chrono::steady_clock::now();
+            const auto t_now = std::chrono::steady_clock::now();
+            fprintf(stderr, "[fc] leiden level %d: %lld union vertices, %lld entries, max degree %d, %d move sweeps, "
+                    "%.1f ms since the previous level\n", level + 1, (long long)nU, (long long)cur.E, max_deg, sw + 1,
+                    1e-3 * (double)std::chrono::duration_cast<std::chrono::microseconds>(t_now - t_last).count());
+            t_last = t_now;
         }
     }
     if (c.trace) fprintf(stderr, "[fc] leiden it=%d: %d levels, %lld level sweeps\n", iteration, level + 1,
