@@ -50,6 +50,11 @@ CONFIGS = {
                          desc="LFR n=1,000,000 mu=0.5, leiden n_p=64"),
     "lfr100k_leiden": dict(kind="lfr", n=100_000, mu=0.5, algo="leiden", n_p=64, tau=0.2, delta=0.02,
                            desc="LFR n=100,000 mu=0.5, leiden n_p=64"),
+    # the infomap branch (fast_consensus.py:260-310 with :268) on the C3 graph, default tau 0.6 (:426)
+    "lfr100k_infomap": dict(kind="lfr", n=100_000, mu=0.5, algo="infomap", n_p=64, tau=0.6, delta=0.02,
+                            desc="LFR n=100,000 mu=0.5, infomap n_p=64"),
+    "lfr1m_infomap": dict(kind="lfr", n=1_000_000, mu=0.5, algo="infomap", n_p=64, tau=0.6, delta=0.02,
+                          desc="LFR n=1,000,000 mu=0.5, infomap n_p=64"),
     # configs[4] (C5)
     "sbm4m": dict(kind="sbm", n=4_000_000, algo="lpm", n_p=128, tau=0.8, delta=0.02,
                   desc="SBM n=4,000,000 blocks of 100, ~40M edges, lpm n_p=128"),
@@ -128,10 +133,11 @@ def cpu_baseline(n, u, v, cfg, seed):
                 "sample": "%d sequential Leiden runs (orc_leiden, the leidenalg restatement) in parallel on %d "
                           "threads (%s) %.2fs; value = n_p*m / (that time x ceil(n_p/threads)=%d) at n_p=%d"
                           % (reps, threads, cpu_model(), cd_s, math.ceil(n_p / reps), n_p)}
-    algo = 0 if cfg["algo"] == "louvain" else 1
+    algo = 0 if cfg["algo"] == "louvain" else 1          # the loop: louvain, or lpm (lpm, infomap)
+    cd_algo = orc.INFOMAP if cfg["algo"] == "infomap" else algo
     t = {}
     t0 = time.perf_counter()
-    lab, _ = orc.cd_batch(algo, reps, g, seed=seed, nthreads=threads)
+    lab, _ = orc.cd_batch(cd_algo, reps, g, seed=seed, nthreads=threads)
     t["cd"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     w = orc.consensus(algo, g, lab, reps)
@@ -372,6 +378,9 @@ def main():
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "kernel": "k_decide_light<%s>" % ("true" if algo != 1 else "false"),
+                "note": (None if cfg["algo"] in ("louvain", "lpm") else
+                         "the %s CD runs its own kernels (leiden.hip); this roofline covers the Louvain-engine "
+                         "decide launches only" % cfg["algo"]),
                 "launches": tim["decide_launches"], "avg_us": avg_s * 1e6,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 # line traffic (PMC, L2 misses x 128 B) per second of decide time, against the

@@ -8,14 +8,14 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import (FC_ALGO_LEIDEN, FC_ALGO_LOUVAIN, FC_ALGO_LOUVAIN_NC, FC_ALGO_LPM, FastConsensusError, Stats,
-                   check, ptr)
+from ._lib import (FC_ALGO_INFOMAP, FC_ALGO_LEIDEN, FC_ALGO_LOUVAIN, FC_ALGO_LOUVAIN_NC, FC_ALGO_LPM,
+                   FastConsensusError, Stats, check, ptr)
 
-ALGORITHMS = {"louvain": FC_ALGO_LOUVAIN, "lpm": FC_ALGO_LPM, "leiden": FC_ALGO_LEIDEN}
+ALGORITHMS = {"louvain": FC_ALGO_LOUVAIN, "lpm": FC_ALGO_LPM, "leiden": FC_ALGO_LEIDEN, "infomap": FC_ALGO_INFOMAP}
 # consensus weight rules: fast_consensus.py (the named entry point) or the new_consensus.py
 # fork's plain count that keeps converged edges (:155-163); louvain only
 RULES = ("fast_consensus", "new_consensus")
-OUT_OF_SCOPE = ("infomap", "cnm")
+OUT_OF_SCOPE = ("cnm",)
 FINAL_PASS_ITER = 0x40000000  # iteration salt of the final pass (matches capi.cpp fc_run)
 
 
@@ -28,7 +28,7 @@ def algo_id(algorithm):
     if algorithm in ALGORITHMS:
         return ALGORITHMS[algorithm]
     if algorithm in OUT_OF_SCOPE:
-        raise NotImplementedError("algorithm %r is outside this engine's scope (louvain, lpm and leiden only)"
+        raise NotImplementedError("algorithm %r is outside this engine's scope (louvain, lpm, leiden and infomap only)"
                                   % algorithm)
     return None
 
@@ -338,8 +338,8 @@ class Cover:
 def labels_to_output(algorithm, node_labels, labels):
     """Engine labelings [n_p][N] -> the reference's return type (fast_consensus.py:383-392):
     louvain: list of dict node -> community (insertion order = node order, as
-    python-louvain builds it); lpm: list of set of frozenset of nodes; leiden: list of
-    ``Cover`` (igraph vertex ids, :385-388)."""
+    python-louvain builds it); lpm and infomap: list of set of frozenset of nodes; leiden:
+    list of ``Cover`` (igraph vertex ids, :385-388)."""
     out = []
     nodes = list(node_labels.tolist())
     if algorithm == "leiden":
@@ -374,7 +374,7 @@ def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, se
 
     G: an undirected networkx Graph (weights are ignored: the reference resets them to 1,
     :135-136) or an ``IdGraph``.  Returns a list of n_p partitions -- dicts for louvain,
-    sets of frozensets for lpm, ``Cover`` objects for leiden -- or None for an unknown
+    sets of frozensets for lpm and infomap, ``Cover`` objects for leiden -- or None for an unknown
     algorithm (the reference's loop
     ``break``s and returns None, :380-381).  ``seed`` makes the run reproducible (the
     reference is unseeded).  ``rule="new_consensus"`` (louvain only) switches to the

@@ -59,6 +59,16 @@ void timer_collect(Ctx& c, fc_stats* st) {
 
 static void bind(Ctx& c) { FC_HIP(hipSetDevice(c.device)); }
 
+static bool known_algo(int algo) {
+    return is_louvain(algo) || algo == FC_ALGO_LPM || algo == FC_ALGO_LEIDEN || algo == FC_ALGO_INFOMAP;
+}
+// community detection of a loop variant (:148 / :270 / :210-211 / :268)
+static void run_cd(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+    if (algo == FC_ALGO_LEIDEN) leiden_run(c, rbegin, rcount, n_p_total, iteration);
+    else if (algo == FC_ALGO_INFOMAP) infomap_run(c, rbegin, rcount, n_p_total, iteration);
+    else cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
+}
+
 }  // namespace fc
 
 using namespace fc;
@@ -190,6 +200,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_SEED: c.seed = (uint64_t)value; break;
         case FC_OPT_CLOSURE_ROUNDS: FC_REQUIRE(value >= 1, FC_EINVAL, "closure_rounds >= 1"); c.closure_rounds = (int)value; break;
         case FC_OPT_PRUNE_MARK: FC_REQUIRE(value == 0 || value == 1, FC_EINVAL, "prune_mark must be 0 or 1"); c.prune_mark = (int)value; break;
+        case FC_OPT_INFOMAP_TRIALS: FC_REQUIRE(value >= 1, FC_EINVAL, "infomap trials >= 1"); c.infomap_trials = (int)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }
@@ -252,10 +263,8 @@ int fc_get_nextgraph(fc_ctx* ctx, int64_t* m_out, int32_t* u, int32_t* v, int32_
 int fc_cd(fc_ctx* ctx, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM || algo == FC_ALGO_LEIDEN, FC_EINVAL,
-               "algo must be louvain, lpm or leiden");
-    if (algo == FC_ALGO_LEIDEN) leiden_run(c, rbegin, rcount, n_p_total, iteration);
-    else cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
+    FC_REQUIRE(known_algo(algo), FC_EINVAL, "algo must be louvain, lpm, leiden or infomap");
+    run_cd(c, algo, rbegin, rcount, n_p_total, iteration);
     FC_API_END
 }
 
@@ -375,8 +384,7 @@ int fc_collect_timing(fc_ctx* ctx, fc_stats* st) {
 int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* labels_out, fc_stats* st) {
     FC_CTX(ctx)
     FC_API_BEGIN
-    FC_REQUIRE(is_louvain(algo) || algo == FC_ALGO_LPM || algo == FC_ALGO_LEIDEN, FC_EINVAL,
-               "algorithm must be louvain, lpm or leiden (infomap/cnm are out of scope)");
+    FC_REQUIRE(known_algo(algo), FC_EINVAL, "algorithm must be louvain, lpm, leiden or infomap (cnm is out of scope)");
     FC_REQUIRE(n_p >= 1, FC_EINVAL, "n_p must be >= 1");
     FC_REQUIRE(c.N > 0, FC_ESTATE, "no graph loaded");
     const bool louv = is_louvain(algo);
@@ -404,7 +412,7 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
     int it = 0;
     for (;;) {
         if (it >= c.max_iters) { a.hit_iter_cap = 1; break; }
-        cd_run(c, algo, 0, n_p, n_p, it);                             // :148 / :270
+        run_cd(c, algo, 0, n_p, n_p, it);                             // :148 / :270 / :268
         int32_t* part = ensure<int32_t>(c.part, c.g.m + 1);
         consensus_partial(c, algo, part);                             // :150-159 / :273-280
         a.partition_edges += (int64_t)n_p * c.g.m;
@@ -429,7 +437,7 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
         }
     }
     a.iterations = it + (a.exit_check == 1 ? 1 : 0);
-    cd_run(c, algo, 0, n_p, n_p, 0x40000000 + it);                   // final pass :383-392
+    run_cd(c, algo, 0, n_p, n_p, 0x40000000 + it);                   // final pass :383-392
     a.partition_edges += (int64_t)n_p * c.g.m;
     a.m_final = c.g.m;
     if (labels_out) {

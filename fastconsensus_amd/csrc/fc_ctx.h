@@ -150,7 +150,8 @@ struct Ctx {
     DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
     int coarsen = 8;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
     double cd_min_dq = 1e-7;        // Louvain sweeps stop below this predicted gain (Leiden's move phase: 0)
-    DevBuf lv[48];                  // Leiden level state (leiden.hip)
+    DevBuf lv[64];                  // Leiden level state (leiden.hip)
+    int infomap_trials = 10;        // FC_OPT_INFOMAP_TRIALS (igraph community_infomap default)
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     // CD kernel variant that leaves every decision unchanged (A/B switch, default on):
     // own-label entries summed in registers (ballots / wave scan) instead of the LDS table
@@ -183,6 +184,8 @@ void graph_to_host(Ctx& c, int64_t m, const int32_t* u, const int32_t* v, const 
                    int32_t* ou, int32_t* ov, int32_t* ow, int64_t* oage);
 // leiden.hip: replica-batched Leiden (leidenalg ModularityVertexPartition, n_iterations=1)
 void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration);
+// igraph Infomap core (two-level map equation, best of `trials`), same layout
+void infomap_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration);
 // consensus.cpp
 void consensus_partial(Ctx& c, int algo, int32_t* out);
 void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept,

@@ -44,7 +44,7 @@ constexpr int LWS = 1024;         // LDS hash slots per wave (a table is sized t
 constexpr int LIGHT = LWS / 2;    // rows / member-row sums above this go to the block-per-vertex kernels
 constexpr int HLS = 8192;         // LDS slots of a block-per-vertex table
 constexpr int HLIGHT = HLS / 2;   // longer rows use a global table
-constexpr int MODE_MOVE = 0, MODE_REFINE = 1;
+constexpr int MODE_MOVE = 0, MODE_REFINE = 1, MODE_INFO = 2;   // Leiden move / refine; Infomap move
 constexpr int MSH = 256;          // move-counter shards
 constexpr int MAX_LEVELS = 64;
 
@@ -81,13 +81,45 @@ struct LvArgs {
     int64_t hslots;
     unsigned long long* moves;   // [MSH]
     unsigned long long* mvt;     // [nU] move phase: (bucket stamp << 32) | target of this bucket's movers
+    // Infomap (map equation): module exit weights, the replica's total exit weight, every
+    // vertex's external weight (row sum; its weighted degree kv also counts internal edges),
+    // the two adjacency weights a move changes, 1/2M
+    int64_t* out;
+    int64_t* qrep;
+    const int64_t* sv;
+    int32_t* mvo;                // [nU] Infomap: the old module of this bucket's movers (with mvt)
+    double inv;
 };
+
+__device__ __forceinline__ double plogp2(double p) { return p > 0.0 ? p * log(p) * 1.4426950408889634 : 0.0; }
+// Change of the two-level map equation (bits) when a vertex of flow kv and external weight
+// sv moves from module A (adjacency weight wA) to module B (wB); integer weights, /2M.
+__device__ __forceinline__ double info_delta(double inv, long long Q, long long oA, long long tA, long long oB,
+                                             long long tB, long long kv, long long sv, long long wA, long long wB) {
+    const long long oA2 = oA - sv + 2 * wA, tA2 = tA - kv, oB2 = oB + sv - 2 * wB, tB2 = tB + kv;
+    const long long Q2 = Q + (oA2 - oA) + (oB2 - oB);
+    return (plogp2(Q2 * inv) - plogp2(Q * inv)) -
+           2.0 * (plogp2(oA2 * inv) - plogp2(oA * inv) + plogp2(oB2 * inv) - plogp2(oB * inv)) +
+           (plogp2((oA2 + tA2) * inv) - plogp2((oA + tA) * inv) + plogp2((oB2 + tB2) * inv) - plogp2((oB + tB) * inv));
+}
+// smaller delta, then larger tie hash, then smaller id; c < 0 = none
+__device__ __forceinline__ bool info_better(double d1, uint32_t h1, int32_t c1, double d2, uint32_t h2, int32_t c2) {
+    if (c1 < 0) return false;
+    if (c2 < 0) return true;
+    if (d1 != d2) return d1 < d2;
+    if (h1 != h2) return h1 > h2;
+    return c1 < c2;
+}
+constexpr double INFO_MIN_GAIN = 1e-10;   // igraph's greedy core moves on a codelength decrease > 1e-10
 
 template <bool IMPL> __device__ __forceinline__ int32_t rep_of(const LvArgs& a, int64_t x) {
     return IMPL ? (int32_t)(x / a.N0) : a.rep[x];
 }
 template <bool IMPL> __device__ __forceinline__ int64_t kv_of(const LvArgs& a, int64_t x) {
     return IMPL ? a.kv[x % a.N0] : a.kv[x];
+}
+template <bool IMPL> __device__ __forceinline__ int64_t sv_of(const LvArgs& a, int64_t x) {
+    return IMPL ? a.sv[x % a.N0] : a.sv[x];
 }
 __device__ __forceinline__ bool in_bucket(const LvArgs& a, int32_t r, int64_t x, int bucket) {
     const uint32_t xl = (uint32_t)(x - a.roff[r]);
@@ -103,6 +135,28 @@ __device__ __forceinline__ bool lv_better(long long s1, uint32_t h1, int32_t c1,
     if (s1 != s2) return s1 > s2;
     if (h1 != h2) return h1 > h2;
     return c1 < c2;
+}
+// Infomap candidate scan over table slots [0, ts) (wave): the most negative delta-L
+__device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
+                                               int32_t own, long long kvx, long long svx, long long wown, int32_t r,
+                                               int64_t x, double& bd, uint32_t& bh, int32_t& bc, int32_t& bw) {
+    const int lane = threadIdx.x & 63;
+    bd = 0.0; bh = 0; bc = -1; bw = 0;
+    const long long Q = a.qrep[r], oA = a.out[own], tA = a.tot[own];
+    for (uint32_t s = lane; s < ts; s += 64) {
+        const int32_t k = keys[s];
+        if (k < 0 || k == own) continue;
+        const double d = info_delta(a.inv, Q, oA, tA, a.out[k], a.tot[k], kvx, svx, wown, vals[s]);
+        const uint32_t h = tie_of(a, r, x, k);
+        if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = vals[s]; }
+    }
+    for (int off = 32; off; off >>= 1) {
+        const double d2 = __shfl_xor(bd, off);
+        const uint32_t h2 = __shfl_xor(bh, off);
+        const int32_t c2 = __shfl_xor(bc, off);
+        const int32_t w2 = __shfl_xor(bw, off);
+        if (info_better(d2, h2, c2, bd, bh, bc)) { bd = d2; bh = h2; bc = c2; bw = w2; }
+    }
 }
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_wave_barrier();
@@ -187,8 +241,10 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             if (MODE == MODE_MOVE) {
                 elig = a.act[x0] != 0;
                 if (elig) a.act[x0] = 0;   // popped from the queue
-            } else {
+            } else if (MODE == MODE_REFINE) {
                 elig = a.rsize[a.R[x0]] == 1;   // only nodes still alone in their refined community
+            } else {
+                elig = true;                    // Infomap: full passes
             }
         }
     }
@@ -209,27 +265,41 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         const uint32_t ts = tsize(re - rb);
         for (uint32_t s = lane; s < ts; s += 64) { keys[s] = -1; vals[s] = 0; }
         wsync();
-        const int32_t own = MODE == MODE_MOVE ? a.P[x] : a.R[x];
+        const int32_t own = MODE == MODE_REFINE ? a.R[x] : a.P[x];
         const int32_t pc = a.P[x];
+        long long wl = 0;   // Infomap: weight to the own module
         for (int64_t j = rb + lane; j < re; j += 64) {
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
-            tins(keys, vals, ts, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
+            const int32_t cy = MODE == MODE_REFINE ? a.R[y] : a.P[y];
+            if (MODE == MODE_INFO && cy == own) { wl += wy; continue; }
+            tins(keys, vals, ts, true, cy, wy);
         }
         wsync();
         const long long kvx = kv_of<IMPL>(a, x);
         long long bs, wown;
         uint32_t bh;
-        int32_t bc;
-        wave_scan(a, keys, vals, ts, own, kvx, rep_of<IMPL>(a, x), x, bs, bh, bc, wown);
+        int32_t bc, bw = 0;
+        if (MODE == MODE_INFO) {
+            for (int off = 32; off; off >>= 1) wl += __shfl_xor(wl, off);
+            wown = wl;
+            double bd;
+            wave_scan_info(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rep_of<IMPL>(a, x), x, bd, bh, bc, bw);
+            if (!(bd < -INFO_MIN_GAIN)) bc = -1;
+            bs = 0;
+        } else {
+            wave_scan(a, keys, vals, ts, own, kvx, rep_of<IMPL>(a, x), x, bs, bh, bc, wown);
+        }
         if (lane == 0) {
-            const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
+            const int32_t t = MODE == MODE_INFO ? bc : lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
             if (t >= 0) {
                 const int p = atomicAdd(&s_cnt, 1);
-                a.blist[(int64_t)blockIdx.x * LTB + p] = (int32_t)x;
-                a.btgt[(int64_t)blockIdx.x * LTB + p] = t;
-                if (MODE == MODE_MOVE) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
+                const int64_t q = (int64_t)blockIdx.x * LTB + p;
+                a.blist[q] = (int32_t)x;
+                a.btgt[q] = t;
+                if (MODE != MODE_REFINE) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
+                if (MODE == MODE_INFO) a.mvo[x] = own;
             }
         }
         wsync();
@@ -265,13 +335,40 @@ __device__ __forceinline__ void block_best(BRed& red, long long& bs, uint32_t& b
     __syncthreads();
 }
 
+struct BRedI {
+    double d[LTB / 64];
+    uint32_t h[LTB / 64];
+    int32_t c[LTB / 64];
+    int32_t w[LTB / 64];
+};
+__device__ __forceinline__ void block_best_info(BRedI& red, double& bd, uint32_t& bh, int32_t& bc, int32_t& bw) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int off = 32; off; off >>= 1) {
+        const double d2 = __shfl_xor(bd, off);
+        const uint32_t h2 = __shfl_xor(bh, off);
+        const int32_t c2 = __shfl_xor(bc, off);
+        const int32_t w2 = __shfl_xor(bw, off);
+        if (info_better(d2, h2, c2, bd, bh, bc)) { bd = d2; bh = h2; bc = c2; bw = w2; }
+    }
+    if (lane == 0) { red.d[wv] = bd; red.h[wv] = bh; red.c[wv] = bc; red.w[wv] = bw; }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int k = 1; k < LTB / 64; ++k)
+            if (info_better(red.d[k], red.h[k], red.c[k], bd, bh, bc)) {
+                bd = red.d[k]; bh = red.h[k]; bc = red.c[k]; bw = red.w[k];
+            }
+    __syncthreads();
+}
+
 // Long rows: one block per vertex; an LDS table of up to HLS slots, or (rows > HLIGHT) a
 // global table per block, cleared through the list of slots it created.
 template <bool IMPL, int MODE>
 __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
     __shared__ int32_t lkey[HLS], lval[HLS];
     __shared__ int s_n;
+    __shared__ long long s_wown;
     __shared__ BRed red;
+    __shared__ BRedI redi;
     const int n = *a.heavy_cnt;
     int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
     int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
@@ -285,25 +382,30 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
         const uint32_t ts = lds ? tsize(re - rb) : (uint32_t)a.hslots;
         int32_t* keys = lds ? lkey : gkey;
         int32_t* vals = lds ? lval : gval;
-        if (threadIdx.x == 0) s_n = 0;
+        if (threadIdx.x == 0) { s_n = 0; s_wown = 0; }
         if (lds)
             for (uint32_t s = threadIdx.x; s < ts; s += LTB) { lkey[s] = -1; lval[s] = 0; }
         __syncthreads();
-        const int32_t own = MODE == MODE_MOVE ? a.P[x] : a.R[x];
+        const int32_t own = MODE == MODE_REFINE ? a.R[x] : a.P[x];
         const int32_t pc = a.P[x];
+        long long wl = 0;
         for (int64_t j = rb + threadIdx.x; j < re; j += LTB) {
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
-            const int s = tins(keys, vals, ts, true, MODE == MODE_MOVE ? a.P[y] : a.R[y], wy);
+            const int32_t cy = MODE == MODE_REFINE ? a.R[y] : a.P[y];
+            if (MODE == MODE_INFO && cy == own) { wl += wy; continue; }
+            const int s = tins(keys, vals, ts, true, cy, wy);
             if (!lds && s >= 0) lst[atomicAdd(&s_n, 1)] = s;
         }
+        if (MODE == MODE_INFO && wl) atomicAdd((unsigned long long*)&s_wown, (unsigned long long)wl);
         __syncthreads();
         const long long kvx = kv_of<IMPL>(a, x);
         const int32_t r = rep_of<IMPL>(a, x);
-        long long bs = LLONG_MIN, wown = 0;
+        long long bs = LLONG_MIN, wown = MODE == MODE_INFO ? s_wown : 0;
+        double bd = 0.0;
         uint32_t bh = 0;
-        int32_t bc = -1;
+        int32_t bc = -1, bw = 0;
         const int cnt = lds ? (int)ts : s_n;
         for (int q = threadIdx.x; q < cnt; q += LTB) {
             const int s = lds ? q : lst[q];
@@ -311,16 +413,32 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
             if (k < 0) continue;
             const long long val = vals[s];
             if (!lds) { gkey[s] = -1; gval[s] = 0; }   // clear for the next vertex (read before)
+            if (MODE == MODE_INFO) {
+                const double d = info_delta(a.inv, a.qrep[r], a.out[own], a.tot[own], a.out[k], a.tot[k], kvx,
+                                            sv_of<IMPL>(a, x), wown, val);
+                const uint32_t h = tie_of(a, r, x, k);
+                if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = (int32_t)val; }
+                continue;
+            }
             if (k == own) { wown = val; continue; }
             const long long sc = val * a.M2 - kvx * a.tot[k];
             const uint32_t h = tie_of(a, r, x, k);
             if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
         }
-        block_best(red, bs, bh, bc, wown);
-        if (threadIdx.x == 0) {
-            const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
-            a.htgt[i] = t;
-            if (MODE == MODE_MOVE && t >= 0) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
+        if (MODE == MODE_INFO) {
+            block_best_info(redi, bd, bh, bc, bw);
+            if (threadIdx.x == 0) {
+                const int32_t t = (bc >= 0 && bd < -INFO_MIN_GAIN) ? bc : -1;
+                a.htgt[i] = t;
+                if (t >= 0) { a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t; a.mvo[x] = own; }
+            }
+        } else {
+            block_best(red, bs, bh, bc, wown);
+            if (threadIdx.x == 0) {
+                const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
+                a.htgt[i] = t;
+                if (MODE == MODE_MOVE && t >= 0) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
+            }
         }
         __syncthreads();
     }
@@ -337,7 +455,7 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
     const int lane = threadIdx.x & 63;
     if (lane == 0) {
         const long long kvx = kv_of<IMPL>(a, x);
-        int32_t* lab = MODE == MODE_MOVE ? a.P : a.R;
+        int32_t* lab = MODE == MODE_REFINE ? a.R : a.P;
         const int32_t old = lab[x];
         lab[x] = t;
         atomicAdd((unsigned long long*)&a.tot[t], (unsigned long long)kvx);
@@ -347,6 +465,42 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
             atomicAdd(&a.rsize[old], -1);
         }
         ++mv;
+    }
+    if (MODE == MODE_INFO) {
+        // exact module exit weights under simultaneous moves: every edge at a mover changes the
+        // exits of its ends' modules from the bucket's before-labels to its after-labels (a
+        // neighbour that moves in this bucket is read from its stamped records; an edge between
+        // two movers is counted by the smaller id only)
+        const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
+        const int64_t xr = IMPL ? x - base : x;
+        const int32_t xo = a.mvo[x];
+        const int64_t re = a.rowptr[xr + 1];
+        long long dq = 0;
+        for (int64_t j = a.rowptr[xr] + lane; j < re; j += 64) {
+            const int64_t y = base + a.col[j];
+            const long long w = a.w ? a.w[j] : 1;
+            const unsigned long long my = a.mvt[y];
+            int32_t yo, yn;
+            if ((uint32_t)(my >> 32) == stamp) {
+                if (y < x) continue;
+                yo = a.mvo[y];
+                yn = (int32_t)(uint32_t)my;
+            } else {
+                yo = yn = a.P[y];
+            }
+            if (xo != yo) {
+                atomicAdd((unsigned long long*)&a.out[xo], (unsigned long long)(-w));
+                atomicAdd((unsigned long long*)&a.out[yo], (unsigned long long)(-w));
+                dq -= 2 * w;
+            }
+            if (t != yn) {
+                atomicAdd((unsigned long long*)&a.out[t], (unsigned long long)w);
+                atomicAdd((unsigned long long*)&a.out[yn], (unsigned long long)w);
+                dq += 2 * w;
+            }
+        }
+        for (int off = 32; off; off >>= 1) dq += __shfl_xor(dq, off);
+        if (lane == 0 && dq) atomicAdd((unsigned long long*)&a.qrep[rep_of<IMPL>(a, x)], (unsigned long long)dq);
     }
     if (MODE == MODE_MOVE) {
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
@@ -413,13 +567,14 @@ __global__ void k_ag_counts(int n_r, const uint8_t* done, const int32_t* roff, c
     if (r < n_r) out[r] = done[r] ? 0 : nid[rend[r]] - nid[roff[r]];   // finished: ranges are stale
 }
 template <bool IMPL>
-__global__ void k_ag_nodes(LvArgs a, const int32_t* nid, int32_t* nrep, int64_t* nkv, int32_t* mcnt) {
+__global__ void k_ag_nodes(LvArgs a, const int32_t* nid, int32_t* nrep, int64_t* nkv, int32_t* mcnt, int64_t* nsv) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.nU || nid[c + 1] == nid[c]) return;
     const int32_t xn = nid[c];
     nrep[xn] = rep_of<IMPL>(a, c);
     nkv[xn] = a.tot[c];   // rtot: the refined community's weighted degree
     mcnt[xn] = a.rsize[c];
+    if (nsv) nsv[xn] = a.out[c];   // Infomap: the module's exit weight = the new node's external weight
 }
 // pofR[R[x]] = P[x] (every member agrees: R refines P); prep[P] = min new id over members;
 // ub[new id] += deg(x)
@@ -600,14 +755,71 @@ __global__ void k_lv_fill_u8(int64_t n, uint8_t* p, const uint8_t* done, const i
     if (i < n) p[i] = done[rep[i]] ? 0 : 1;
 }
 
+// ---------------------------------------------------------------- Infomap bookkeeping
+__global__ void k_degree(int64_t N, const int64_t* rowptr, int64_t* deg) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < N) deg[v] = rowptr[v + 1] - rowptr[v];
+}
+// level 0: every vertex its own module (flow = degree, exit = degree)
+__global__ void k_info_init0(int64_t N, int n_r, const int64_t* deg, int32_t* P, int64_t* ptot, int64_t* pout,
+                             int32_t* memb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)n_r * N) return;
+    P[i] = (int32_t)i;
+    ptot[i] = pout[i] = deg[i % N];
+    memb[i] = (int32_t)i;
+}
+// explicit level: singleton modules of the aggregate nodes
+__global__ void k_info_level(int64_t nU, const int64_t* kv, const int64_t* sv, int64_t* ptot, int64_t* pout) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nU) return;
+    ptot[i] = kv[i];
+    pout[i] = sv[i];
+}
+// the modules play the refined communities' part in the aggregation: R = P, sizes, totals
+__global__ void k_info_rclear(int64_t nU, const int64_t* ptot, int32_t* rsize, int64_t* rtot) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nU) return;
+    rsize[c] = 0;
+    rtot[c] = ptot[c];
+}
+template <bool IMPL>
+__global__ void k_info_modules(LvArgs a) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= a.nU || a.done[rep_of<IMPL>(a, x)]) return;
+    const int32_t m = a.P[x];
+    a.R[x] = m;
+    atomicAdd(&a.rsize[m], 1);
+}
+// codelength (bits, without the constant node-entropy term) of replica r's modules: one
+// block per finishing replica, fixed-order reduction (deterministic)
+__global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const int32_t* roff, const int32_t* rend,
+                                                      const int64_t* ptot, const int64_t* pout, const int64_t* qrep,
+                                                      double inv, double* cl) {
+    __shared__ double sm[LTB];
+    const int r = blockIdx.x;
+    if (!fin[r]) return;
+    double acc = 0.0;
+    for (int64_t c = roff[r] + threadIdx.x; c < rend[r]; c += LTB)
+        acc += -2.0 * plogp2(pout[c] * inv) + plogp2((pout[c] + ptot[c]) * inv);
+    sm[threadIdx.x] = acc;
+    __syncthreads();
+    for (int k = LTB / 2; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) sm[threadIdx.x] += sm[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cl[r] = plogp2(qrep[r] * inv) + sm[0];
+}
+
 // Buffers (Ctx::lv).
 enum {
     B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
     B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC, B_MVT,
+    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB,
     // aggregation scratch
     B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
-    // explicit level graphs, ping-pong: rowptr, col, w, kv, rep (x2)
-    B_G0, B_G1 = B_G0 + 5, B_END = B_G1 + 5
+    // explicit level graphs, ping-pong: rowptr, col, w, kv, rep, sv (x2)
+    B_G0, B_G1 = B_G0 + 6, B_END = B_G1 + 6
 };
 static_assert(B_END <= (int)(sizeof(((Ctx*)nullptr)->lv) / sizeof(DevBuf)), "Ctx::lv too small");
 
@@ -633,32 +845,45 @@ struct LvGraph {
     int32_t* w = nullptr;
     int64_t* kv = nullptr;
     int32_t* rep = nullptr;
+    int64_t* sv = nullptr;
     int32_t max_deg = 0;
 };
 
 }  // namespace
 
-// One Leiden run per local replica on the working graph c.g; labels -> c.lab (slot order,
-// values in [0, N) per replica), exactly like cd_run leaves them.
-void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
+// One multi-level run per local replica on the working graph c.g; labels -> lab_out (slot
+// order, values in [0, N) per replica), exactly like cd_run leaves c.lab.
+//   info = false: Leiden (level-0 move on the Louvain engine, refine, aggregate by R);
+//   info = true:  one Infomap trial (map-equation passes at every level, aggregate by the
+//                 modules); cl_out[r] = the replica's codelength (without the constant
+//                 node-entropy term) for the best-of-trials choice.
+static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total, int iteration, int trial,
+                       int32_t* lab_out, double* cl_out) {
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
     FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
     const int64_t N = c.N;
     Graph& g = c.g;
-    FC_REQUIRE(g.M2 < 0x7fffffffll, FC_ELIMIT, "leiden: total edge weight must stay below 2^30");
-    FC_REQUIRE((int64_t)rcount * N < 0x7fffffffll, FC_ELIMIT, "leiden: replicas x nodes must stay below 2^31");
+    // Infomap runs on the topology (community_infomap() without weights, :268 / :390)
+    const int64_t M2 = info ? 2 * g.m : g.M2;
+    FC_REQUIRE(M2 < 0x7fffffffll, FC_ELIMIT, "leiden/infomap: total edge weight must stay below 2^30");
+    FC_REQUIRE((int64_t)rcount * N < 0x7fffffffll, FC_ELIMIT, "leiden/infomap: replicas x nodes must stay below 2^31");
 
-    // ---- level 0, move phase: the replica-batched local-moving engine run to exhaustion
-    const double mdq = c.cd_min_dq;
-    c.cd_min_dq = 0.0;
-    try {
-        cd_run(c, FC_ALGO_LOUVAIN, rbegin, rcount, n_p_total, iteration);
-    } catch (...) {
+    if (!info) {
+        // ---- level 0, move phase: the replica-batched local-moving engine run to exhaustion
+        const double mdq = c.cd_min_dq;
+        c.cd_min_dq = 0.0;
+        try {
+            cd_run(c, FC_ALGO_LOUVAIN, rbegin, rcount, n_p_total, iteration);
+        } catch (...) {
+            c.cd_min_dq = mdq;
+            throw;
+        }
         c.cd_min_dq = mdq;
-        throw;
     }
-    c.cd_min_dq = mdq;
-    const int sl0 = timer_begin(c);   // cd_run timed itself; this span covers refinement and the levels
+    // lab_out == nullptr: c.lab, read only now (cd_run above may have (re)allocated it)
+    if (!lab_out) lab_out = ensure<int32_t>(c.lab, (size_t)rcount * (size_t)N);
+    const int sl0 = timer_begin(c);   // (cd_run timed itself) refinement, Infomap passes and the levels
+    const char* name = info ? "infomap" : "leiden";
 
     const int n_r = rcount;
     const int64_t nU0 = (int64_t)n_r * N;
@@ -681,8 +906,26 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
     // [n_r] refined-community counts | [n_r] finalize flags (u8 view) | 2 u64 maxima
     int32_t* misc = I32(B_MISC, 2 * (int64_t)n_r + 16);
     FC_HIP(hipMemsetAsync(done, 0, n_r, c.stream));
-    k_lv_init0<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, c.lab.as<int32_t>(), c.spos.as<int32_t>(), P, R, rtot, rsize,
-                                               g.kdeg.as<int64_t>(), memb);
+    int64_t* deg = nullptr;
+    int64_t* ptot = nullptr;
+    int64_t* pout = nullptr;
+    int64_t* qrep = nullptr;
+    double* dcl = nullptr;
+    if (info) {
+        deg = I64(B_DEG, N);
+        ptot = I64(B_PTOT, nU0);
+        pout = I64(B_POUT, nU0);
+        qrep = I64(B_QREP, n_r);
+        dcl = (double*)I64(B_CL, n_r);
+        k_degree<<<nb(N), LTB, 0, c.stream>>>(N, g.rowptr.as<int64_t>(), deg);
+        k_info_init0<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, deg, P, ptot, pout, memb);
+        std::vector<int64_t> q0(n_r, M2);   // singletons: total exit weight = every edge end
+        FC_HIP(hipMemcpyAsync(qrep, q0.data(), 8 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
+        sync(c);
+    } else {
+        k_lv_init0<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, c.lab.as<int32_t>(), c.spos.as<int32_t>(), P, R, rtot,
+                                                   rsize, g.kdeg.as<int64_t>(), memb);
+    }
     std::vector<int32_t> h_roff(n_r), h_rend(n_r);
     for (int r = 0; r < n_r; ++r) { h_roff[r] = (int32_t)(r * N); h_rend[r] = (int32_t)((r + 1) * N); }
     FC_HIP(hipMemcpyAsync(roff, h_roff.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
@@ -692,7 +935,9 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
     std::vector<uint32_t> h_rkey(n_r);
 
     LvArgs a{};
-    a.N0 = N; a.M2 = g.M2; a.B = B;
+    a.N0 = N; a.M2 = M2; a.B = B;
+    a.inv = M2 > 0 ? 1.0 / (double)M2 : 0.0;
+    a.out = pout; a.qrep = qrep;
     a.roff = roff; a.rkey = rkey; a.done = done; a.moves = moves;
     a.heavy_cnt = hcnt;
     a.mvt = (unsigned long long*)I64(B_MVT, nU0);
@@ -707,18 +952,20 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
     auto set_keys = [&](int level, int sweep, uint32_t salt) {
         for (int r = 0; r < n_r; ++r)
             h_rkey[r] = stream_key(c.seed, (uint32_t)(rbegin + r), (uint32_t)iteration,
-                                   (uint32_t)(level * 4096 + sweep), 16 + salt);
+                                   (uint32_t)(level * 4096 + sweep), 16 + salt + 8 * (uint32_t)trial);
         FC_HIP(hipMemcpyAsync(rkey, h_rkey.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
     };
     auto set_graph = [&]() {
         a.nU = nU;
         if (impl) {
             a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>();
-            a.w = (g.max_w == 1) ? nullptr : g.cw.as<int32_t>();
-            a.kv = g.kdeg.as<int64_t>(); a.rep = nullptr;
+            a.w = (info || g.max_w == 1) ? nullptr : g.cw.as<int32_t>();
+            a.kv = info ? deg : g.kdeg.as<int64_t>(); a.rep = nullptr;
+            a.sv = deg;
         } else {
-            a.rowptr = cur.rowptr; a.col = cur.col; a.w = cur.w; a.kv = cur.kv; a.rep = cur.rep;
+            a.rowptr = cur.rowptr; a.col = cur.col; a.w = cur.w; a.kv = cur.kv; a.rep = cur.rep; a.sv = cur.sv;
         }
+        if (info) a.mvo = I32(B_BWA, nU);
         const int64_t nblk = nb(nU);
         a.blist = I32(B_BLIST, nblk * LTB);
         a.btgt = I32(B_BTGT, nblk * LTB);
@@ -762,9 +1009,11 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
             if (impl && MODE == MODE_MOVE) LV_LAUNCH(true, MODE_MOVE);
-            else if (impl) LV_LAUNCH(true, MODE_REFINE);
+            else if (impl && MODE == MODE_REFINE) LV_LAUNCH(true, MODE_REFINE);
+            else if (impl) LV_LAUNCH(true, MODE_INFO);
             else if (MODE == MODE_MOVE) LV_LAUNCH(false, MODE_MOVE);
-            else LV_LAUNCH(false, MODE_REFINE);
+            else if (MODE == MODE_REFINE) LV_LAUNCH(false, MODE_REFINE);
+            else LV_LAUNCH(false, MODE_INFO);
 #undef LV_LAUNCH
         }
         std::vector<unsigned long long> hm(MSH);
@@ -778,12 +1027,51 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
     int level = 0;
     int64_t lv_sweeps = 0;
     for (;; ++level) {
-        // ---- refine: singletons inside the move-phase communities, one sweep
         set_graph();
-        if (!impl) k_lv_rinit<<<nb(nU), LTB, 0, c.stream>>>(nU, cur.kv, R, rtot, rsize);
-        a.P = P; a.R = R; a.tot = rtot; a.rsize = rsize;
-        sweep(MODE_REFINE, level, 0);
-        ++lv_sweeps;
+        if (info) {
+            // ---- Infomap: greedy passes (at most 10, until one moves nothing), then the
+            // modules are the units the level aggregates
+            a.P = P; a.tot = ptot; a.out = pout; a.qrep = qrep;
+            for (int sw = 0; sw < 10; ++sw) {
+                ++lv_sweeps;
+                if (sweep(MODE_INFO, level, sw) == 0) break;
+            }
+            if (getenv("FC_INFOMAP_DEBUG") && nU < 100000) {   // invariants: sum tot = 2M, sum out = Q per replica
+                sync(c);
+                std::vector<int64_t> ht(nU), ho(nU), hq(n_r);
+                std::vector<int32_t> hr0(n_r), hr1(n_r);
+                FC_HIP(hipMemcpy(ht.data(), ptot, 8 * nU, hipMemcpyDeviceToHost));
+                FC_HIP(hipMemcpy(ho.data(), pout, 8 * nU, hipMemcpyDeviceToHost));
+                FC_HIP(hipMemcpy(hq.data(), qrep, 8 * n_r, hipMemcpyDeviceToHost));
+                FC_HIP(hipMemcpy(hr0.data(), roff, 4 * n_r, hipMemcpyDeviceToHost));
+                FC_HIP(hipMemcpy(hr1.data(), rend, 4 * n_r, hipMemcpyDeviceToHost));
+                for (int r = 0; r < std::min(n_r, 4); ++r) {
+                    if (h_done[r]) continue;
+                    long long st = 0, so = 0;
+                    double Lh = 0;
+                    auto pl = [](double p) { return p > 0 ? p * log(p) * 1.4426950408889634 : 0.0; };
+                    for (int64_t x = hr0[r]; x < hr1[r]; ++x) {
+                        st += ht[x]; so += ho[x];
+                        Lh += -2 * pl(ho[x] * a.inv) + pl((ho[x] + ht[x]) * a.inv);
+                    }
+                    Lh += pl(hq[r] * a.inv);
+                    fprintf(stderr, "[fc] infomap dbg host L %.6f\n", Lh);
+                    fprintf(stderr, "[fc] infomap dbg trial %d level %d replica %d range [%d,%d) sum tot %lld (2M %lld) sum out %lld Q %lld\n",
+                            trial, level, r, hr0[r], hr1[r], st, (long long)M2, so, (long long)hq[r]);
+                }
+            }
+            a.R = R; a.rsize = rsize;
+            k_info_rclear<<<nb(nU), LTB, 0, c.stream>>>(nU, ptot, rsize, rtot);
+            if (impl) k_info_modules<true><<<nb(nU), LTB, 0, c.stream>>>(a);
+            else k_info_modules<false><<<nb(nU), LTB, 0, c.stream>>>(a);
+            a.tot = rtot;
+        } else {
+            // ---- refine: singletons inside the move-phase communities, one sweep
+            if (!impl) k_lv_rinit<<<nb(nU), LTB, 0, c.stream>>>(nU, cur.kv, R, rtot, rsize);
+            a.P = P; a.R = R; a.tot = rtot; a.rsize = rsize;
+            sweep(MODE_REFINE, level, 0);
+            ++lv_sweeps;
+        }
         // ---- which replicas still aggregate: refined communities < level nodes
         int32_t* nid = I32(B_NID, nU + 1);
         int32_t* fl = I32(B_FL, nU + 1);
@@ -804,8 +1092,8 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         if (any_fin) {
             uint8_t* dfin = (uint8_t*)(misc + n_r);
             FC_HIP(hipMemcpyAsync(dfin, fin.data(), n_r, hipMemcpyHostToDevice, c.stream));
-            k_lv_final<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, dfin, memb, P, roff, c.spos.as<int32_t>(),
-                                                      c.lab.as<int32_t>());
+            if (info) k_info_codelen<<<n_r, LTB, 0, c.stream>>>(dfin, roff, rend, ptot, pout, qrep, a.inv, dcl);
+            k_lv_final<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, dfin, memb, P, roff, c.spos.as<int32_t>(), lab_out);
             for (int r = 0; r < n_r; ++r) h_done[r] |= fin[r];
             FC_HIP(hipMemcpyAsync(done, h_done.data(), n_r, hipMemcpyHostToDevice, c.stream));
             sync(c);
@@ -830,9 +1118,10 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         nx.rowptr = I64(gs + 0, nUn + 1);
         nx.kv = I64(gs + 3, nUn);
         nx.rep = I32(gs + 4, nUn);
+        nx.sv = info ? I64(gs + 5, nUn) : nullptr;
         int32_t* mcnt = I32(B_MCNT, nUn + 1);
-        if (impl) k_ag_nodes<true><<<nb(nU), LTB, 0, c.stream>>>(a, nid, nx.rep, nx.kv, mcnt);
-        else k_ag_nodes<false><<<nb(nU), LTB, 0, c.stream>>>(a, nid, nx.rep, nx.kv, mcnt);
+        if (impl) k_ag_nodes<true><<<nb(nU), LTB, 0, c.stream>>>(a, nid, nx.rep, nx.kv, mcnt, nx.sv);
+        else k_ag_nodes<false><<<nb(nU), LTB, 0, c.stream>>>(a, nid, nx.rep, nx.kv, mcnt, nx.sv);
         FC_HIP(hipMemsetAsync(mcnt + nUn, 0, 4, c.stream));
         int32_t* moff = I32(B_MOFF, nUn + 1);
         exclusive_scan(c, mcnt, moff, nUn + 1);
@@ -904,8 +1193,20 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         impl = false;
         nU = nUn;
         max_deg = nx.max_deg;
+        if (info) {   // singleton modules of the aggregate nodes; the next loop trip optimises them
+            ptot = I64(B_PTOT, nU);
+            pout = I64(B_POUT, nU);
+            R = I32(B_R, nU); rtot = I64(B_RTOT, nU); rsize = I32(B_RSIZE, nU);
+            k_info_level<<<nb(nU), LTB, 0, c.stream>>>(nU, cur.kv, cur.sv, ptot, pout);
+            if (c.trace) {
+                sync(c);
+                fprintf(stderr, "[fc] infomap level %d: %lld union vertices, %lld entries, max degree %d\n", level + 1,
+                        (long long)nU, (long long)cur.E, max_deg);
+            }
+            continue;
+        }
         // ---- move phase on the new level, from the inherited partition, until no move
-        int64_t* ptot = I64(B_PTOT, nU);
+        ptot = I64(B_PTOT, nU);
         R = I32(B_R, nU); rtot = I64(B_RTOT, nU); rsize = I32(B_RSIZE, nU);
         FC_HIP(hipMemsetAsync(ptot, 0, 8 * (size_t)nU, c.stream));
         k_ag_ptot<<<nb(nU), LTB, 0, c.stream>>>(nU, P, cur.kv, ptot);
@@ -928,13 +1229,45 @@ void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
             t_last = t_now;
         }
     }
-    if (c.trace) fprintf(stderr, "[fc] leiden it=%d: %d levels, %lld level sweeps\n", iteration, level + 1,
+    if (c.trace) fprintf(stderr, "[fc] %s it=%d: %d levels, %lld level sweeps\n", name, iteration, level + 1,
                          (long long)lv_sweeps);
+    if (info) FC_HIP(hipMemcpyAsync(cl_out, dcl, 8 * (size_t)n_r, hipMemcpyDeviceToHost, c.stream));
     c.acc.cd_sweeps += lv_sweeps * n_r;
     c.prof.cd_sweeps += lv_sweeps * n_r;
     c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
     c.labT_valid = false;
     timer_end(c, 0, sl0);
+    sync(c);
+}
+
+void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
+    multilevel(c, false, rbegin, rcount, n_p_total, iteration, 0, nullptr, nullptr);   // -> c.lab
+}
+
+// igraph community_infomap(trials=10) (fast_consensus.py:268, :390): the best of `trials`
+// independent runs per replica, by codelength.
+void infomap_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
+    const int64_t N = c.N;
+    const int T = std::max(1, c.infomap_trials);
+    int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * (size_t)std::max<int64_t>(N, 1));
+    int32_t* tlab = T > 1 ? ensure<int32_t>(c.lv[B_TLAB], (size_t)rcount * (size_t)std::max<int64_t>(N, 1)) : lab;
+    std::vector<double> best(rcount, 1e300), cl(rcount);
+    for (int t = 0; t < T; ++t) {
+        multilevel(c, true, rbegin, rcount, n_p_total, iteration, t, t == 0 ? lab : tlab, cl.data());
+        if (getenv("FC_INFOMAP_DEBUG"))
+            for (int r = 0; r < std::min(rcount, 4); ++r)
+                fprintf(stderr, "[fc] infomap trial %d replica %d codelength %.6f (best %.6f)\n", t, r, cl[r], best[r]);
+        for (int r = 0; r < rcount; ++r) {
+            if (!(cl[r] < best[r])) continue;
+            best[r] = cl[r];
+            if (t > 0)
+                FC_HIP(hipMemcpyAsync(lab + (size_t)r * N, tlab + (size_t)r * N, 4 * (size_t)N, hipMemcpyDeviceToDevice,
+                                      c.stream));
+        }
+    }
+    sync(c);
+    c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
+    c.labT_valid = false;
 }
 
 }  // namespace fc

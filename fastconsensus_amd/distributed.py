@@ -22,7 +22,7 @@ import torch.distributed as dist
 
 from .core import FINAL_PASS_ITER
 
-LOUVAIN, LPM, LOUVAIN_NC, LEIDEN = 0, 1, 2, 3
+LOUVAIN, LPM, LOUVAIN_NC, LEIDEN, INFOMAP = 0, 1, 2, 3, 4
 
 
 def on_device(t):

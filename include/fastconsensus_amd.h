@@ -48,6 +48,11 @@ extern "C" {
                              edge and check #1 (:229) converges on the empty graph: the result is
                              the final pass on G.  fc_run reports that one iteration (exit 1)
                              without running its discarded CD batch.   */
+#define FC_ALGO_INFOMAP 4 /* fast_consensus.py:260-310 with the infomap CD (:267-268, final pass
+                             :389-390): the lpm loop (co-membership count, threshold, weight-0
+                             closure, check after closure) around igraph community_infomap()
+                             (unweighted, trials=10): the two-level map-equation core, best of
+                             FC_OPT_INFOMAP_TRIALS runs.   */
 
 typedef struct fc_ctx fc_ctx;
 
@@ -124,6 +129,8 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 (fast local moving, Traag et al. 2019); unit-weight graphs keep
                                 0.  0: every neighbour of a mover, tracking from the first sweep
                                 that moves < n/4 vertices.                                       */
+#define FC_OPT_INFOMAP_TRIALS 13 /* independent Infomap runs per replica, the smallest codelength kept
+                                    (default 10, igraph community_infomap's trials)              */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */
@@ -154,7 +161,7 @@ int fc_run(fc_ctx* ctx, int algo, int n_p, double tau, double delta, int32_t* la
 /* ---- fine-grained steps (distributed driver; parity tests) ------------------------ */
 /* Community detection on the working graph for replicas [replica_begin,
  * replica_begin+replica_count) of n_p_total (:148 / :384 louvain level 0, :270 / :392 LPA,
- * :210-211 / :386-387 Leiden).
+ * :210-211 / :386-387 Leiden, :268 / :390 Infomap).
  * Randomness depends on (seed, global replica index, iteration), not on the sharding. */
 int fc_cd(fc_ctx* ctx, int algo, int replica_begin, int replica_count, int n_p_total,
           int iteration);

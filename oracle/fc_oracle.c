@@ -600,8 +600,160 @@ int orc_leiden(i64 N, const i64* rowptr, const i32* col, const i32* w, u64 seed,
     return levels;
 }
 
+/* ------------------------------------------------------------------ igraph Infomap (core)
+ * Restatement of the CORE of igraph_community_infomap (python-igraph 0.9.7
+ * Graph.community_infomap(), trials=10), as called unweighted at fast_consensus.py:268 and
+ * :390 (igraph absent: parity unpinned).  The two-level map equation for an undirected
+ * graph, with node flow p_a = k_a/2M and module exit flow q_i = o_i/2M (o_i: weight of the
+ * edges leaving module i),
+ *   L = plogp(sum_i q_i) - 2 sum_i plogp(q_i) - sum_a plogp(p_a) + sum_i plogp(q_i + p_i),
+ * is minimised by igraph's greedy core: passes over the nodes in random order, each node
+ * moving to the neighbour module of the most negative delta-L (< -1e-10), at most 10 passes
+ * or until a pass moves nothing; then the modules become the nodes of the next level
+ * (aggregation), until a level merges nothing.  The best of `trials` runs (smallest L) is
+ * kept.  igraph's alternating sub-module / single-node re-partitioning rounds around this
+ * core are NOT restated (documented deviation).  log base 2 as igraph.
+ * Output labels renumbered 0..k-1 by first node.  Returns the codelength (bits). */
+static inline double plogp2(double p) { return p > 0.0 ? p * log(p) * 1.4426950408889634 : 0.0; }
+
+static double im_delta(double inv, long long Q, long long oA, long long tA, long long oB, long long tB,
+                       long long kv, long long sv, long long wA, long long wB) {
+    const long long oA2 = oA - sv + 2 * wA, tA2 = tA - kv, oB2 = oB + sv - 2 * wB, tB2 = tB + kv;
+    const long long Q2 = Q + (oA2 - oA) + (oB2 - oB);
+    return (plogp2(Q2 * inv) - plogp2(Q * inv))
+           - 2.0 * (plogp2(oA2 * inv) - plogp2(oA * inv) + plogp2(oB2 * inv) - plogp2(oB * inv))
+           + (plogp2((oA2 + tA2) * inv) - plogp2((oA + tA) * inv) + plogp2((oB2 + tB2) * inv) - plogp2((oB + tB) * inv));
+}
+
+static double im_trial(i64 N, const i64* rowptr, const i32* col, u64* s, i32* lab) {
+    ld_graph g;
+    g.n = N;
+    const i64 E = rowptr[N];
+    g.rp = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    g.col = (i32*)malloc(sizeof(i32) * (size_t)(E ? E : 1));
+    g.w = (i64*)malloc(sizeof(i64) * (size_t)(E ? E : 1));
+    g.kv = (i64*)calloc((size_t)(N ? N : 1), sizeof(i64));
+    const size_t nn = (size_t)(N ? N : 1);
+    i64* sv = (i64*)malloc(sizeof(i64) * nn);
+    for (i64 v = 0; v <= N; ++v) g.rp[v] = rowptr[v];
+    for (i64 j = 0; j < E; ++j) { g.col[j] = col[j]; g.w[j] = 1; }
+    for (i64 v = 0; v < N; ++v) { g.kv[v] = rowptr[v + 1] - rowptr[v]; sv[v] = g.kv[v]; }
+    const long long M2 = E;
+    const double inv = M2 > 0 ? 1.0 / (double)M2 : 0.0;
+    i32* P = (i32*)malloc(sizeof(i32) * nn);
+    i64* tot = (i64*)malloc(sizeof(i64) * nn);
+    i64* out = (i64*)malloc(sizeof(i64) * nn);
+    i64* nw = (i64*)malloc(sizeof(i64) * nn);
+    u8* seen = (u8*)calloc(nn, 1);
+    i32* cands = (i32*)malloc(sizeof(i32) * nn);
+    i32* order = (i32*)malloc(sizeof(i32) * nn);
+    i32* memb = (i32*)malloc(sizeof(i32) * nn);
+    i32* nid = (i32*)malloc(sizeof(i32) * nn);
+    for (i64 v = 0; v < N; ++v) memb[v] = (i32)v;
+    long long Q = 0;
+    for (i64 v = 0; v < N; ++v) Q += sv[v];
+    while (M2 > 0) {
+        for (i64 v = 0; v < g.n; ++v) { P[v] = (i32)v; tot[v] = g.kv[v]; out[v] = sv[v]; order[v] = (i32)v; }
+        for (int pass = 0; pass < 10; ++pass) {
+            shuffle_i32(order, g.n, s);
+            i64 moved = 0;
+            for (i64 t = 0; t < g.n; ++t) {
+                const i32 v = order[t];
+                const i32 A = P[v];
+                i64 nc = 0;
+                for (i64 j = g.rp[v]; j < g.rp[v + 1]; ++j) {
+                    const i32 c = P[g.col[j]];
+                    if (!seen[c]) { seen[c] = 1; nw[c] = 0; cands[nc++] = c; }
+                    nw[c] += g.w[j];
+                }
+                const i64 wA = seen[A] ? nw[A] : 0;
+                i32 best = -1;
+                double bd = -1e-10;
+                shuffle_i32(cands, nc, s);
+                for (i64 k = 0; k < nc; ++k) {
+                    const i32 B = cands[k];
+                    if (B == A) continue;
+                    const double d = im_delta(inv, Q, out[A], tot[A], out[B], tot[B], g.kv[v], sv[v], wA, nw[B]);
+                    if (d < bd) { bd = d; best = B; }
+                }
+                if (best >= 0) {
+                    const i64 wB = nw[best];
+                    const long long dA = -sv[v] + 2 * wA, dB = sv[v] - 2 * wB;
+                    out[A] += dA; out[best] += dB; Q += dA + dB;
+                    tot[A] -= g.kv[v]; tot[best] += g.kv[v];
+                    P[v] = best;
+                    ++moved;
+                }
+                for (i64 k = 0; k < nc; ++k) seen[cands[k]] = 0;
+            }
+            if (!moved) break;
+        }
+        i64 k = 0;
+        for (i64 c = 0; c < g.n; ++c) nid[c] = -1;
+        for (i64 v = 0; v < g.n; ++v) nid[P[v]] = 0;
+        for (i64 c = 0; c < g.n; ++c) if (nid[c] == 0) nid[c] = (i32)k++;
+        if (k == g.n) break;
+        /* aggregate by modules: kv' = tot, sv' = out, rows = inter-module weights */
+        ld_graph h;
+        h.n = k;
+        h.rp = (i64*)calloc((size_t)k + 1, sizeof(i64));
+        h.kv = (i64*)calloc((size_t)(k ? k : 1), sizeof(i64));
+        i64* moff = (i64*)calloc((size_t)k + 1, sizeof(i64));
+        i32* ml = (i32*)malloc(sizeof(i32) * (size_t)(g.n ? g.n : 1));
+        for (i64 v = 0; v < g.n; ++v) moff[nid[P[v]] + 1]++;
+        for (i64 x = 0; x < k; ++x) moff[x + 1] += moff[x];
+        i64* cur = (i64*)malloc(sizeof(i64) * (size_t)(k ? k : 1));
+        for (i64 x = 0; x < k; ++x) cur[x] = moff[x];
+        for (i64 v = 0; v < g.n; ++v) ml[cur[nid[P[v]]]++] = (i32)v;
+        const i64 cap = g.rp[g.n] ? g.rp[g.n] : 1;
+        h.col = (i32*)malloc(sizeof(i32) * (size_t)cap);
+        h.w = (i64*)malloc(sizeof(i64) * (size_t)cap);
+        i64 e = 0;
+        for (i64 c = 0; c < g.n; ++c) if (nid[c] >= 0) { h.kv[nid[c]] = tot[c]; sv[nid[c]] = out[c]; }
+        for (i64 x = 0; x < k; ++x) {
+            i64 nc = 0;
+            for (i64 q = moff[x]; q < moff[x + 1]; ++q) {
+                const i32 v = ml[q];
+                for (i64 j = g.rp[v]; j < g.rp[v + 1]; ++j) {
+                    const i32 y = nid[P[g.col[j]]];
+                    if (y == x) continue;
+                    if (!seen[y]) { seen[y] = 1; nw[y] = 0; cands[nc++] = y; }
+                    nw[y] += g.w[j];
+                }
+            }
+            for (i64 q = 0; q < nc; ++q) { h.col[e] = cands[q]; h.w[e] = nw[cands[q]]; ++e; seen[cands[q]] = 0; }
+            h.rp[x + 1] = e;
+        }
+        for (i64 v = 0; v < N; ++v) memb[v] = nid[P[memb[v]]];
+        free(moff); free(ml); free(cur);
+        ld_free(&g);
+        g = h;
+    }
+    /* codelength of the final modules (P over the last level) */
+    double L = plogp2(Q * inv);
+    for (i64 c = 0; c < g.n; ++c) L += -2.0 * plogp2(out[c] * inv) + plogp2((out[c] + tot[c]) * inv);
+    for (i64 v = 0; v < N; ++v) L -= plogp2((double)(rowptr[v + 1] - rowptr[v]) * inv);
+    for (i64 v = 0; v < N; ++v) lab[v] = M2 > 0 ? P[memb[v]] : (i32)v;
+    renumber(N, lab, nid);
+    ld_free(&g);
+    free(sv); free(P); free(tot); free(out); free(nw); free(seen); free(cands); free(order); free(memb); free(nid);
+    return L;
+}
+
+double orc_infomap(i64 N, const i64* rowptr, const i32* col, u64 seed, int trials, i32* lab) {
+    u64 s = seed ^ 0x9FB21C651E98DF25ull;
+    i32* tmp = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    double best = 1e300;
+    for (int t = 0; t < (trials > 0 ? trials : 1); ++t) {
+        const double L = im_trial(N, rowptr, col, &s, tmp);
+        if (L < best) { best = L; memcpy(lab, tmp, sizeof(i32) * (size_t)N); }
+    }
+    free(tmp);
+    return best;
+}
+
 /* Batch helper: n_r independent runs (replicas) in parallel over host threads.
- * algo 0 = louvain level 0, 1 = lpa, 3 = leiden.  lab is [n_r][N]. */
+ * algo 0 = louvain level 0, 1 = lpa, 3 = leiden, 4 = infomap (10 trials).  lab is [n_r][N]. */
 void orc_cd_batch(int algo, int n_r, i64 N, const i64* rowptr, const i32* col, const i32* w,
                   u64 seed, i32* lab, int* sweeps, int nthreads) {
 #ifdef _OPENMP
@@ -614,6 +766,7 @@ void orc_cd_batch(int algo, int n_r, i64 N, const i64* rowptr, const i32* col, c
         u64 sd = seed * 0x9E3779B97F4A7C15ull + (u64)r * 0xC2B2AE3D27D4EB4Full + 1;
         int sw = algo == 0   ? orc_louvain_level0(N, rowptr, col, w, sd, lab + (i64)r * N)
                  : algo == 3 ? orc_leiden(N, rowptr, col, w, sd, lab + (i64)r * N)
+                 : algo == 4 ? (int)orc_infomap(N, rowptr, col, sd, 10, lab + (i64)r * N)
                              : orc_lpa(N, rowptr, col, sd, lab + (i64)r * N, 10000);
         if (sweeps) sweeps[r] = sw;
     }

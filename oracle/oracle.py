@@ -24,12 +24,12 @@ _i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
 _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
 _lib = None
 
-LOUVAIN, LPM, LOUVAIN_NC, LEIDEN = 0, 1, 2, 3   # LOUVAIN_NC: louvain with new_consensus.py's rule (:155-163)
+LOUVAIN, LPM, LOUVAIN_NC, LEIDEN, INFOMAP = 0, 1, 2, 3, 4   # LOUVAIN_NC: louvain with new_consensus.py's rule (:155-163)
 
 
 def _cd_algo(algo):
     """Community-detection algorithm of a loop variant (the new_consensus.py rule runs Louvain)."""
-    return algo if algo in (LPM, LEIDEN) else LOUVAIN
+    return algo if algo in (LPM, LEIDEN, INFOMAP) else LOUVAIN
 AGE_ITER_SHIFT = 40          # closure/repair edges created in iteration b get ages >= (b+1) << 40
 AGE_REPAIR_OFFSET = 1 << 39
 
@@ -66,6 +66,8 @@ def lib():
         L.orc_lpa.argtypes = [i64, _i64p, _i32p, u64, _i32p, ctypes.c_int]
         L.orc_leiden.argtypes = [i64, _i64p, _i32p, ctypes.c_void_p, u64, _i32p]
         L.orc_leiden.restype = ctypes.c_int
+        L.orc_infomap.argtypes = [i64, _i64p, _i32p, u64, ctypes.c_int, _i32p]
+        L.orc_infomap.restype = ctypes.c_double
         L.orc_lpa.restype = ctypes.c_int
         L.orc_cd_batch.argtypes = [ctypes.c_int, ctypes.c_int, i64, _i64p, _i32p, _i32p, u64, _i32p, _i32p,
                                    ctypes.c_int]
@@ -217,6 +219,15 @@ def cd_batch(algo, n_r, g, seed, nthreads=0):
     sw = np.empty(n_r, np.int32)
     lib().orc_cd_batch(_cd_algo(algo), n_r, g.N, rowptr, col, cw, int(seed) & (2**64 - 1), lab, sw, int(nthreads))
     return lab, sw
+
+
+def infomap(g, seed, trials=10):
+    """One restated igraph Infomap run (unweighted topology, fast_consensus.py:268); returns
+    (labels, codelength in bits)."""
+    rowptr, col, _ = g.csr()
+    lab = np.empty(g.N, np.int32)
+    L = lib().orc_infomap(g.N, rowptr, col, int(seed) & (2**64 - 1), int(trials), lab)
+    return lab, L
 
 
 def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8,

@@ -319,7 +319,7 @@ def test_fast_consensus_networkx_dropin(fcmod):
         assert set().union(*p) == set(G.nodes())
     assert fcmod.fast_consensus(G, algorithm="unknown", n_p=2) is None
     with pytest.raises(NotImplementedError):
-        fcmod.fast_consensus(G, algorithm="infomap", n_p=2)
+        fcmod.fast_consensus(G, algorithm="cnm", n_p=2)
 
 
 def test_determinism_same_seed(fcmod):

@@ -2,5 +2,8 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-FC_TRACE=1 timeout -k 10 300 python bench.py --config lfr1m_leiden --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> gpurun_out/b_l1m_trace.err || exit 1
-grep -E "leiden|step" gpurun_out/b_l1m_trace.err | tail -30
+FC_INFOMAP_DEBUG=1 timeout -k 10 120 python tools/im_dbg.py 2>&1 | grep -E "codelength|T " | grep -v "best 1000" | tail -12
+timeout -k 10 120 python tools/im_dist.py 2>&1 | grep -v amdgpu.ids || exit 1
+timeout -k 10 900 python -u -m pytest -p no:cacheprovider --timeout 600 --timeout-method thread -rf -s -v tests/test_infomap.py tests/test_leiden.py > gpurun_out/im.out 2>&1; rc=$?
+grep -E "infomap |leiden LFR|FAIL|passed|failed" gpurun_out/im.out | tail -20
+[ $rc -eq 0 ] || { tail -30 gpurun_out/im.out; exit $rc; }
