@@ -4,7 +4,7 @@
 //
 // leidenalg (not vendored, not installed; restated from its published algorithm, Traag,
 // Waltman & van Eck 2019, and the package's documented defaults -- parity unpinned, see
-// oracle/fc_oracle.c orc_leiden) optimises one level at a time:
+// the oracle's restatement in oracle/fc_oracle.c) optimises one level at a time:
 //   1. move nodes: a queue of every node in random order; a node moves to the neighbour (or
 //      empty) community of largest modularity gain if that gain is positive, and its
 //      neighbours outside the new community re-enter the queue;
