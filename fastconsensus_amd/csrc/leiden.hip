@@ -42,6 +42,7 @@ namespace {
 constexpr int LTB = 256;          // threads per block (4 waves)
 constexpr int LWS = 1024;         // LDS hash slots per wave (a table is sized to its row: 64..LWS)
 constexpr int LIGHT = LWS / 2;    // rows / member-row sums above this go to the block-per-vertex kernels
+constexpr int LWS_SMALL = 256;    // the short-row variant of k_lv_decide
 constexpr int HLS = 8192;         // LDS slots of a block-per-vertex table
 constexpr int HLIGHT = HLS / 2;   // longer rows use a global table
 constexpr int MODE_MOVE = 0, MODE_REFINE = 1, MODE_INFO = 2;   // Leiden move / refine; Infomap move
@@ -226,9 +227,11 @@ __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, 
 // table sized for it (64..LWS slots).  Rows longer than LIGHT go to k_lv_heavy.  Movers are
 // listed per block and stamped in mvt (the apply kernel decides the neighbours' queue
 // flags from the bucket's final state, so the result does not depend on thread timing).
-template <bool IMPL, int MODE>
+// TS: LDS slots per wave -- LWS, or LWS_SMALL when every row of the level is short (the input
+// graph: 8 KB of LDS per block instead of 32 KB, so 32 waves per CU instead of 20)
+template <bool IMPL, int MODE, int TS>
 __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_t stamp) {
-    __shared__ int32_t skey[LTB / 64][LWS], sval[LTB / 64][LWS];
+    __shared__ int32_t skey[LTB / 64][TS], sval[LTB / 64][TS];
     __shared__ int s_cnt;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_cnt = 0;
@@ -248,7 +251,20 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             }
         }
     }
-    unsigned long long mask = __ballot(elig);
+    // long rows go to k_lv_heavy: one list append per wave (ballot + one atomic)
+    bool hv = false;
+    if (elig) {
+        const int64_t xr0 = IMPL ? x0 % a.N0 : x0;
+        hv = a.rowptr[xr0 + 1] - a.rowptr[xr0] > TS / 2;
+    }
+    const unsigned long long hmask = __ballot(hv);
+    if (hmask) {
+        int hb = 0;
+        if (lane == 0) hb = atomicAdd(a.heavy_cnt, __popcll(hmask));
+        hb = __shfl(hb, 0);
+        if (hv) a.heavy[hb + __popcll(hmask & ((1ull << lane) - 1))] = (int32_t)x0;
+    }
+    unsigned long long mask = __ballot(elig && !hv);
     int32_t* keys = skey[wv];
     int32_t* vals = sval[wv];
     while (mask) {
@@ -258,10 +274,6 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
         const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
-        if (re - rb > LIGHT) {
-            if (lane == 0) a.heavy[atomicAdd(a.heavy_cnt, 1)] = (int32_t)x;
-            continue;
-        }
         const uint32_t ts = tsize(re - rb);
         for (uint32_t s = lane; s < ts; s += 64) { keys[s] = -1; vals[s] = 0; }
         wsync();
@@ -979,7 +991,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     };
     // heavy-kernel grid: one global table per block, bounded to ~2 GB of tables
     auto heavy_grid = [&](int64_t slots) {
-        int64_t gr = std::min<int64_t>(256, std::max<int64_t>(1, ((int64_t)2 << 30) / (12 * slots)));
+        int64_t gr = std::min<int64_t>(1024, std::max<int64_t>(1, ((int64_t)2 << 30) / (12 * slots)));
         const size_t need = (size_t)(gr * slots);
         const bool grow = c.lv[B_HKEY].bytes < need * 4 + 16;
         a.hkey = I32(B_HKEY, gr * slots);
@@ -1004,7 +1016,8 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
 #define LV_LAUNCH(IM, MD)                                                                        \
     do {                                                                                         \
-        k_lv_decide<IM, MD><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);                            \
+        if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
+        else k_lv_decide<IM, MD, LWS><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);                  \
         if (max_deg > LIGHT) k_lv_heavy<IM, MD><<<hg, LTB, 0, c.stream>>>(a, stamp);             \
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
