@@ -92,16 +92,29 @@ struct LvArgs {
     double inv;
 };
 
-__device__ __forceinline__ double plogp2(double p) { return p > 0.0 ? p * log(p) * 1.4426950408889634 : 0.0; }
-// Change of the two-level map equation (bits) when a vertex of flow kv and external weight
-// sv moves from module A (adjacency weight wA) to module B (wB); integer weights, /2M.
-__device__ __forceinline__ double info_delta(double inv, long long Q, long long oA, long long tA, long long oB,
-                                             long long tB, long long kv, long long sv, long long wA, long long wB) {
-    const long long oA2 = oA - sv + 2 * wA, tA2 = tA - kv, oB2 = oB + sv - 2 * wB, tB2 = tB + kv;
-    const long long Q2 = Q + (oA2 - oA) + (oB2 - oB);
-    return (plogp2(Q2 * inv) - plogp2(Q * inv)) -
-           2.0 * (plogp2(oA2 * inv) - plogp2(oA * inv) + plogp2(oB2 * inv) - plogp2(oB * inv)) +
-           (plogp2((oA2 + tA2) * inv) - plogp2((oA + tA) * inv) + plogp2((oB2 + tB2) * inv) - plogp2((oB + tB) * inv));
+__device__ __forceinline__ double plogp2(double p) { return p > 0.0 ? p * log2(p) : 0.0; }
+// The map-equation change split into the part of the source module A (computed once per
+// vertex) and the per-candidate part (module B and the total exit Q'), 5 logarithms each.
+struct InfoA {
+    long long dA;     // change of A's exit weight
+    double termA;     // A's terms of delta-L
+    double q0;        // plogp(Q)
+};
+__device__ __forceinline__ InfoA info_a(double inv, long long Q, long long oA, long long tA, long long kv, long long sv,
+                                        long long wA) {
+    InfoA r;
+    const long long oA2 = oA - sv + 2 * wA, tA2 = tA - kv;
+    r.dA = oA2 - oA;
+    r.termA = -2.0 * (plogp2(oA2 * inv) - plogp2(oA * inv)) + (plogp2((oA2 + tA2) * inv) - plogp2((oA + tA) * inv));
+    r.q0 = plogp2(Q * inv);
+    return r;
+}
+__device__ __forceinline__ double info_b(double inv, const InfoA& A, long long Q, long long oB, long long tB,
+                                         long long kv, long long sv, long long wB) {
+    const long long oB2 = oB + sv - 2 * wB, tB2 = tB + kv;
+    const long long Q2 = Q + A.dA + (oB2 - oB);
+    return (plogp2(Q2 * inv) - A.q0) + A.termA - 2.0 * (plogp2(oB2 * inv) - plogp2(oB * inv)) +
+           (plogp2((oB2 + tB2) * inv) - plogp2((oB + tB) * inv));
 }
 // smaller delta, then larger tie hash, then smaller id; c < 0 = none
 __device__ __forceinline__ bool info_better(double d1, uint32_t h1, int32_t c1, double d2, uint32_t h2, int32_t c2) {
@@ -137,21 +150,24 @@ __device__ __forceinline__ bool lv_better(long long s1, uint32_t h1, int32_t c1,
     if (h1 != h2) return h1 > h2;
     return c1 < c2;
 }
-// Infomap candidate scan over table slots [0, ts) (wave): the most negative delta-L
+// Infomap candidate scan over table slots [0, ts) by a group of GL lanes (a power of two
+// dividing 64, aligned): the most negative delta-L, reduced inside the group
+template <int GL = 64>
 __device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
                                                int32_t own, long long kvx, long long svx, long long wown, int32_t r,
                                                int64_t x, double& bd, uint32_t& bh, int32_t& bc, int32_t& bw) {
-    const int lane = threadIdx.x & 63;
+    const int gl = threadIdx.x & (GL - 1);
     bd = 0.0; bh = 0; bc = -1; bw = 0;
-    const long long Q = a.qrep[r], oA = a.out[own], tA = a.tot[own];
-    for (uint32_t s = lane; s < ts; s += 64) {
+    const long long Q = a.qrep[r];
+    const InfoA A = info_a(a.inv, Q, a.out[own], a.tot[own], kvx, svx, wown);
+    for (uint32_t s = gl; s < ts; s += GL) {
         const int32_t k = keys[s];
         if (k < 0 || k == own) continue;
-        const double d = info_delta(a.inv, Q, oA, tA, a.out[k], a.tot[k], kvx, svx, wown, vals[s]);
+        const double d = info_b(a.inv, A, Q, a.out[k], a.tot[k], kvx, svx, vals[s]);
         const uint32_t h = tie_of(a, r, x, k);
         if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = vals[s]; }
     }
-    for (int off = 32; off; off >>= 1) {
+    for (int off = GL / 2; off; off >>= 1) {
         const double d2 = __shfl_xor(bd, off);
         const uint32_t h2 = __shfl_xor(bh, off);
         const int32_t c2 = __shfl_xor(bc, off);
@@ -199,12 +215,13 @@ __device__ __forceinline__ uint32_t tsize(int64_t d) {
 
 // Wave-level candidate scan over table slots [0, ts): best (score, tie, community) and the
 // weight to the own community, reduced over the wave.
+template <int GL = 64>
 __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
                                           int32_t own, long long kvx, int32_t r, int64_t x, long long& bs,
                                           uint32_t& bh, int32_t& bc, long long& wown) {
-    const int lane = threadIdx.x & 63;
+    const int gl = threadIdx.x & (GL - 1);
     bs = LLONG_MIN; bh = 0; bc = -1; wown = 0;
-    for (uint32_t s = lane; s < ts; s += 64) {
+    for (uint32_t s = gl; s < ts; s += GL) {
         const int32_t k = keys[s];
         if (k < 0) continue;
         const long long val = vals[s];
@@ -213,7 +230,7 @@ __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, 
         const uint32_t h = tie_of(a, r, x, k);
         if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
     }
-    for (int off = 32; off; off >>= 1) {
+    for (int off = GL / 2; off; off >>= 1) {
         const long long s2 = __shfl_xor(bs, off);
         const uint32_t h2 = __shfl_xor(bh, off);
         const int32_t c2 = __shfl_xor(bc, off);
@@ -228,9 +245,12 @@ __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, 
 // listed per block and stamped in mvt (the apply kernel decides the neighbours' queue
 // flags from the bucket's final state, so the result does not depend on thread timing).
 // TS: LDS slots per wave -- LWS, or LWS_SMALL when every row of the level is short (the input
-// graph: 8 KB of LDS per block instead of 32 KB, so 32 waves per CU instead of 20)
-template <bool IMPL, int MODE, int TS>
+// graph: 8 KB of LDS per block instead of 32 KB, so 32 waves per CU instead of 20).
+// G: vertices a wave decides at once (64/G lanes and TS/G slots each): G = 4 on short-row
+// levels, where a 64-lane vertex left most lanes idle (LFR: 27 entries per row).
+template <bool IMPL, int MODE, int TS, int G>
 __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_t stamp) {
+    constexpr int GL = 64 / G, TSG = TS / G;
     __shared__ int32_t skey[LTB / 64][TS], sval[LTB / 64][TS];
     __shared__ int s_cnt;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -255,7 +275,7 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     bool hv = false;
     if (elig) {
         const int64_t xr0 = IMPL ? x0 % a.N0 : x0;
-        hv = a.rowptr[xr0 + 1] - a.rowptr[xr0] > TS / 2;
+        hv = a.rowptr[xr0 + 1] - a.rowptr[xr0] > TS / G / 2;
     }
     const unsigned long long hmask = __ballot(hv);
     if (hmask) {
@@ -265,22 +285,30 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         if (hv) a.heavy[hb + __popcll(hmask & ((1ull << lane) - 1))] = (int32_t)x0;
     }
     unsigned long long mask = __ballot(elig && !hv);
-    int32_t* keys = skey[wv];
-    int32_t* vals = sval[wv];
+    const int grp = lane / GL, gl = lane & (GL - 1);
+    int32_t* keys = skey[wv] + grp * TSG;
+    int32_t* vals = sval[wv] + grp * TSG;
     while (mask) {
-        const int l = __ffsll((long long)mask) - 1;
-        mask &= mask - 1;
-        const int64_t x = __shfl(x0, l);
+        // group g takes the g-th remaining eligible lane (every lane computes the same split)
+        int myl = -1;
+        for (int g = 0; g < G; ++g) {
+            if (!mask) break;
+            const int l = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            if (g == grp) myl = l;
+        }
+        const int64_t x = __shfl(x0, myl < 0 ? 0 : myl);
+        const bool valid = myl >= 0;
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
-        const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
+        const int64_t rb = valid ? a.rowptr[xr] : 0, re = valid ? a.rowptr[xr + 1] : 0;
         const uint32_t ts = tsize(re - rb);
-        for (uint32_t s = lane; s < ts; s += 64) { keys[s] = -1; vals[s] = 0; }
+        for (uint32_t s = gl; s < ts; s += GL) { keys[s] = -1; vals[s] = 0; }
         wsync();
-        const int32_t own = MODE == MODE_REFINE ? a.R[x] : a.P[x];
-        const int32_t pc = a.P[x];
+        const int32_t own = valid ? (MODE == MODE_REFINE ? a.R[x] : a.P[x]) : -1;
+        const int32_t pc = valid ? a.P[x] : -1;
         long long wl = 0;   // Infomap: weight to the own module
-        for (int64_t j = rb + lane; j < re; j += 64) {
+        for (int64_t j = rb + gl; j < re; j += GL) {
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
@@ -289,21 +317,26 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             tins(keys, vals, ts, true, cy, wy);
         }
         wsync();
-        const long long kvx = kv_of<IMPL>(a, x);
+        const long long kvx = valid ? kv_of<IMPL>(a, x) : 0;
+        const int32_t rx = valid ? rep_of<IMPL>(a, x) : 0;
         long long bs, wown;
         uint32_t bh;
         int32_t bc, bw = 0;
         if (MODE == MODE_INFO) {
-            for (int off = 32; off; off >>= 1) wl += __shfl_xor(wl, off);
+            for (int off = GL / 2; off; off >>= 1) wl += __shfl_xor(wl, off);
             wown = wl;
-            double bd;
-            wave_scan_info(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rep_of<IMPL>(a, x), x, bd, bh, bc, bw);
+            double bd = 0.0;
+            if (valid) {
+                wave_scan_info<GL>(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rx, x, bd, bh, bc, bw);
+            } else {
+                bc = -1;
+            }
             if (!(bd < -INFO_MIN_GAIN)) bc = -1;
             bs = 0;
         } else {
-            wave_scan(a, keys, vals, ts, own, kvx, rep_of<IMPL>(a, x), x, bs, bh, bc, wown);
+            wave_scan<GL>(a, keys, vals, ts, own, kvx, rx, x, bs, bh, bc, wown);
         }
-        if (lane == 0) {
+        if (valid && gl == 0) {
             const int32_t t = MODE == MODE_INFO ? bc : lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
             if (t >= 0) {
                 const int p = atomicAdd(&s_cnt, 1);
@@ -419,6 +452,8 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
         uint32_t bh = 0;
         int32_t bc = -1, bw = 0;
         const int cnt = lds ? (int)ts : s_n;
+        InfoA IA{};
+        if (MODE == MODE_INFO) IA = info_a(a.inv, a.qrep[r], a.out[own], a.tot[own], kvx, sv_of<IMPL>(a, x), wown);
         for (int q = threadIdx.x; q < cnt; q += LTB) {
             const int s = lds ? q : lst[q];
             const int32_t k = keys[s];
@@ -426,8 +461,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
             const long long val = vals[s];
             if (!lds) { gkey[s] = -1; gval[s] = 0; }   // clear for the next vertex (read before)
             if (MODE == MODE_INFO) {
-                const double d = info_delta(a.inv, a.qrep[r], a.out[own], a.tot[own], a.out[k], a.tot[k], kvx,
-                                            sv_of<IMPL>(a, x), wown, val);
+                const double d = info_b(a.inv, IA, a.qrep[r], a.out[k], a.tot[k], kvx, sv_of<IMPL>(a, x), val);
                 const uint32_t h = tie_of(a, r, x, k);
                 if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = (int32_t)val; }
                 continue;
@@ -500,16 +534,20 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
             } else {
                 yo = yn = a.P[y];
             }
-            if (xo != yo) {
-                atomicAdd((unsigned long long*)&a.out[xo], (unsigned long long)(-w));
-                atomicAdd((unsigned long long*)&a.out[yo], (unsigned long long)(-w));
-                dq -= 2 * w;
-            }
-            if (t != yn) {
-                atomicAdd((unsigned long long*)&a.out[t], (unsigned long long)w);
-                atomicAdd((unsigned long long*)&a.out[yn], (unsigned long long)w);
-                dq += 2 * w;
-            }
+            // (module, delta) pairs: -w at xo and yo if the edge was cut, +w at t and yn if it is;
+            // a module on both sides cancels (y staying in a third module: 2 atomics, not 4)
+            int32_t m[4];
+            long long d[4];
+            int nm = 0;
+            auto add = [&](int32_t mod, long long dv) {
+                for (int k = 0; k < nm; ++k)
+                    if (m[k] == mod) { d[k] += dv; return; }
+                m[nm] = mod; d[nm] = dv; ++nm;
+            };
+            if (xo != yo) { add(xo, -w); add(yo, -w); dq -= 2 * w; }
+            if (t != yn) { add(t, w); add(yn, w); dq += 2 * w; }
+            for (int k = 0; k < nm; ++k)
+                if (d[k]) atomicAdd((unsigned long long*)&a.out[m[k]], (unsigned long long)d[k]);
         }
         for (int off = 32; off; off >>= 1) dq += __shfl_xor(dq, off);
         if (lane == 0 && dq) atomicAdd((unsigned long long*)&a.qrep[rep_of<IMPL>(a, x)], (unsigned long long)dq);
@@ -1016,8 +1054,9 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
 #define LV_LAUNCH(IM, MD)                                                                        \
     do {                                                                                         \
-        if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
-        else k_lv_decide<IM, MD, LWS><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);                  \
+        if (max_deg <= 64) k_lv_decide<IM, MD, 512, 4><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);  \
+        else if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
+        else k_lv_decide<IM, MD, LWS, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);               \
         if (max_deg > LIGHT) k_lv_heavy<IM, MD><<<hg, LTB, 0, c.stream>>>(a, stamp);             \
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
