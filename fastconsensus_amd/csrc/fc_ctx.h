@@ -24,8 +24,10 @@ struct FcError {
 #define FC_HIP(call)                                                                       \
     do {                                                                                   \
         hipError_t _e = (call);                                                            \
-        if (_e != hipSuccess)                                                              \
+        if (_e != hipSuccess) {                                                            \
+            (void)hipGetLastError(); /* clear it: library calls (hipcub) re-check it later */ \
             throw ::fc::FcError{FC_EHIP, std::string(#call) + ": " + hipGetErrorString(_e)}; \
+        }                                                                                  \
     } while (0)
 #define FC_REQUIRE(cond, code, msg)                      \
     do {                                                 \

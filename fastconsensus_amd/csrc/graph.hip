@@ -276,7 +276,8 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
     const int64_t m = src.m > 0 ? src.m : 1, n = c.N;
     auto cp = [&](DevBuf& d, const DevBuf& s, size_t bytes) {
         d.ensure(bytes + 16);
-        FC_HIP(hipMemcpyAsync(d.p, s.p, bytes, hipMemcpyDeviceToDevice, c.stream));
+        if (!s.p) return;   // edgeless graph: a per-entry array was never allocated
+        FC_HIP(hipMemcpyAsync(d.p, s.p, std::min(bytes, s.bytes), hipMemcpyDeviceToDevice, c.stream));
     };
     cp(dst.eu, src.eu, 4 * m); cp(dst.ev, src.ev, 4 * m); cp(dst.ew, src.ew, 4 * m); cp(dst.eage, src.eage, 8 * m);
     cp(dst.rowptr, src.rowptr, 8 * (n + 1));

@@ -224,3 +224,39 @@ def test_cli_leiden_end_to_end_on_device(fcmod, tmp_path):
         assert [int(r[0]) for r in rows] == list(range(1, n + 1))
         assert min(int(r[1]) for r in rows) == 1
     assert os.listdir(tmp_path / "memberships_t0.2_d0.02_np5") == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", [3, 4])
+def test_multilevel_edge_cases(fcmod, algo):
+    """Isolated nodes, an edgeless graph and disjoint components (Leiden: 3, Infomap: 4): labels
+    stay in [0, n), isolated nodes alone, components never merged."""
+    # two triangles + a path, plus isolated nodes 9..11
+    e = np.array([[0, 1], [1, 2], [0, 2], [3, 4], [4, 5], [3, 5], [6, 7], [7, 8]], np.int32)
+    n = 12
+    with fcmod.Engine(seed=3) as eng:
+        eng.load_graph(n, e[:, 0], e[:, 1])
+        eng.cd(algo, 0, 4, 4, 0)
+        lab = eng.get_labels(4, renumber=True)
+    for x in lab:
+        assert x.min() >= 0 and x.max() < n
+        for a_, b_ in [(0, 3), (3, 6), (0, 6)]:
+            assert x[a_] != x[b_]                      # components never share a community
+        assert len({x[9], x[10], x[11]}) == 3 and not set(x[9:]) & set(x[:9])
+        assert x[0] == x[1] == x[2] and x[3] == x[4] == x[5]
+    with fcmod.Engine(seed=3) as eng:                 # no edges at all: singletons
+        eng.load_graph(5, np.zeros(0, np.int32), np.zeros(0, np.int32))
+        eng.cd(algo, 0, 2, 2, 0)
+        lab = eng.get_labels(2, renumber=True)
+    assert (lab == np.arange(5)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", [0, 1, 3, 4])
+def test_run_on_edgeless_graph(fcmod, algo):
+    """An edgeless G: every algorithm returns singletons (python-louvain returns one community
+    per node for a graph without edges; the loop converges on the empty graph)."""
+    with fcmod.Engine(seed=1) as eng:
+        eng.load_graph(6, np.zeros(0, np.int32), np.zeros(0, np.int32))
+        labels, st = eng.run(algo, 3, 0.2, 0.02)
+    assert (labels == np.arange(6)).all() and st["m_final"] == 0
