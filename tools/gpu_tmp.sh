@@ -1,4 +1,5 @@
 #!/bin/bash
 set -u
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -p no:cacheprovider --timeout 300 --timeout-method thread -rf -q tests/test_leiden.py -k "edge" 2>&1 | tail -15
+NPS="8 16" bash tools/exp_np.sh
+cp gpurun_out/np/np8.json gpurun_out/np8.json
