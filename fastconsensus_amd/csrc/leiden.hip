@@ -904,10 +904,12 @@ struct LvGraph {
 // One multi-level run per local replica on the working graph c.g; labels -> lab_out (slot
 // order, values in [0, N) per replica), exactly like cd_run leaves c.lab.
 //   info = false: Leiden (level-0 move on the Louvain engine, refine, aggregate by R);
-//   info = true:  one Infomap trial (map-equation passes at every level, aggregate by the
-//                 modules); cl_out[r] = the replica's codelength (without the constant
-//                 node-entropy term) for the best-of-trials choice.
-static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total, int iteration, int trial,
+//   info = true:  `tu` Infomap trials per replica side by side in the union (union replica
+//                 u = r*tu + j runs trial trial0 + j of replica r: the same random streams as
+//                 running the trials one after the other); map-equation passes at every
+//                 level, aggregation by the modules; cl_out[u] = its codelength (without the
+//                 constant node-entropy term) for the best-of-trials choice.
+static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total, int iteration, int tu, int trial0,
                        int32_t* lab_out, double* cl_out) {
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
     FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
@@ -916,7 +918,9 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     // Infomap runs on the topology (community_infomap() without weights, :268 / :390)
     const int64_t M2 = info ? 2 * g.m : g.M2;
     FC_REQUIRE(M2 < 0x7fffffffll, FC_ELIMIT, "leiden/infomap: total edge weight must stay below 2^30");
-    FC_REQUIRE((int64_t)rcount * N < 0x7fffffffll, FC_ELIMIT, "leiden/infomap: replicas x nodes must stay below 2^31");
+    FC_REQUIRE(tu >= 1 && (info || tu == 1), FC_EINVAL, "trials side by side are for Infomap");
+    FC_REQUIRE((int64_t)rcount * tu * N < 0x7fffffffll, FC_ELIMIT,
+               "leiden/infomap: replicas x trials x nodes must stay below 2^31");
 
     if (!info) {
         // ---- level 0, move phase: the replica-batched local-moving engine run to exhaustion
@@ -935,7 +939,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     const int sl0 = timer_begin(c);   // (cd_run timed itself) refinement, Infomap passes and the levels
     const char* name = info ? "infomap" : "leiden";
 
-    const int n_r = rcount;
+    const int n_r = rcount * tu;   // union replicas
     const int64_t nU0 = (int64_t)n_r * N;
     const int B = std::max(1, c.buckets);
     auto I32 = [&](int k, int64_t n) { return ensure<int32_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };
@@ -1001,8 +1005,8 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
 
     auto set_keys = [&](int level, int sweep, uint32_t salt) {
         for (int r = 0; r < n_r; ++r)
-            h_rkey[r] = stream_key(c.seed, (uint32_t)(rbegin + r), (uint32_t)iteration,
-                                   (uint32_t)(level * 4096 + sweep), 16 + salt + 8 * (uint32_t)trial);
+            h_rkey[r] = stream_key(c.seed, (uint32_t)(rbegin + r / tu), (uint32_t)iteration,
+                                   (uint32_t)(level * 4096 + sweep), 16 + salt + 8 * (uint32_t)(trial0 + r % tu));
         FC_HIP(hipMemcpyAsync(rkey, h_rkey.data(), 4 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
     };
     auto set_graph = [&]() {
@@ -1109,7 +1113,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
                     Lh += pl(hq[r] * a.inv);
                     fprintf(stderr, "[fc] infomap dbg host L %.6f\n", Lh);
                     fprintf(stderr, "[fc] infomap dbg trial %d level %d replica %d range [%d,%d) sum tot %lld (2M %lld) sum out %lld Q %lld\n",
-                            trial, level, r, hr0[r], hr1[r], st, (long long)M2, so, (long long)hq[r]);
+                            trial0, level, r, hr0[r], hr1[r], st, (long long)M2, so, (long long)hq[r]);
                 }
             }
             a.R = R; a.rsize = rsize;
@@ -1293,31 +1297,38 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
 }
 
 void leiden_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
-    multilevel(c, false, rbegin, rcount, n_p_total, iteration, 0, nullptr, nullptr);   // -> c.lab
+    multilevel(c, false, rbegin, rcount, n_p_total, iteration, 1, 0, nullptr, nullptr);   // -> c.lab
 }
 
 // igraph community_infomap(trials=10) (fast_consensus.py:268, :390): the best of `trials`
-// independent runs per replica, by codelength.
+// independent runs per replica, by codelength.  The trials run side by side in one union
+// (as many as fit: int32 union ids, ~2^29 union vertices), so the small upper levels are
+// one launch sequence for all of them instead of one per trial.
 void infomap_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
-    const int64_t N = c.N;
+    const int64_t N = std::max<int64_t>(c.N, 1);
     const int T = std::max(1, c.infomap_trials);
-    int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * (size_t)std::max<int64_t>(N, 1));
-    int32_t* tlab = T > 1 ? ensure<int32_t>(c.lv[B_TLAB], (size_t)rcount * (size_t)std::max<int64_t>(N, 1)) : lab;
-    std::vector<double> best(rcount, 1e300), cl(rcount);
-    for (int t = 0; t < T; ++t) {
-        multilevel(c, true, rbegin, rcount, n_p_total, iteration, t, t == 0 ? lab : tlab, cl.data());
-        if (getenv("FC_INFOMAP_DEBUG"))
-            for (int r = 0; r < std::min(rcount, 4); ++r)
-                fprintf(stderr, "[fc] infomap trial %d replica %d codelength %.6f (best %.6f)\n", t, r, cl[r], best[r]);
-        for (int r = 0; r < rcount; ++r) {
-            if (!(cl[r] < best[r])) continue;
-            best[r] = cl[r];
-            if (t > 0)
-                FC_HIP(hipMemcpyAsync(lab + (size_t)r * N, tlab + (size_t)r * N, 4 * (size_t)N, hipMemcpyDeviceToDevice,
+    const int64_t per = (int64_t)rcount * N;
+    int tu = T;
+    while (tu > 1 && per * tu > ((int64_t)1 << 29)) --tu;
+    int32_t* lab = ensure<int32_t>(c.lab, (size_t)per);
+    int32_t* tlab = ensure<int32_t>(c.lv[B_TLAB], (size_t)(per * tu));
+    std::vector<double> best(rcount, 1e300), cl((size_t)rcount * tu);
+    for (int t0 = 0; t0 < T; t0 += tu) {
+        const int k = std::min(tu, T - t0);
+        multilevel(c, true, rbegin, rcount, n_p_total, iteration, k, t0, tlab, cl.data());
+        for (int r = 0; r < rcount; ++r)
+            for (int j = 0; j < k; ++j) {   // trial order: the earliest of equal codelengths wins
+                const size_t u = (size_t)r * k + j;
+                if (getenv("FC_INFOMAP_DEBUG") && r < 4)
+                    fprintf(stderr, "[fc] infomap trial %d replica %d codelength %.6f (best %.6f)\n", t0 + j, r, cl[u],
+                            best[r]);
+                if (!(cl[u] < best[r])) continue;
+                best[r] = cl[u];
+                FC_HIP(hipMemcpyAsync(lab + (size_t)r * N, tlab + u * N, 4 * (size_t)N, hipMemcpyDeviceToDevice,
                                       c.stream));
-        }
+            }
+        sync(c);
     }
-    sync(c);
     c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
     c.labT_valid = false;
 }
