@@ -50,9 +50,18 @@ class OracleEngine:
 
     # steps -----------------------------------------------------------------------------
     def cd(self, algo, r0, count, n_p, iteration):
-        self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
-                                    chunk=self.chunk, prune=self.prune, coarsen=self.coarsen,
-                                    prune_mark=self.prune_mark)
+        if algo in (orc.LEIDEN, orc.INFOMAP):
+            # the sequential restatements, one per replica, seeded by the GLOBAL replica index
+            # (the device keys its randomness the same way, so results do not depend on sharding)
+            rows = []
+            for r in range(r0, r0 + count):
+                sd = (self.seed * 0x9E3779B1 + r * 0x85EBCA77 + iteration * 0xC2B2AE3D) & (2**63 - 1)
+                rows.append(orc.cd_batch(algo, 1, self.g, sd)[0][0])
+            self.lab = np.stack(rows) if rows else np.zeros((0, self.g.N), np.int32)
+        else:
+            self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
+                                        chunk=self.chunk, prune=self.prune, coarsen=self.coarsen,
+                                        prune_mark=self.prune_mark)
         self.r0 = r0
 
     def consensus_partial(self, algo, out):
@@ -78,7 +87,7 @@ class OracleEngine:
         keep = orc.threshold(nw, tau, n_p)
         self.kept = orc.EdgeGraph(g.N, g.u[keep], g.v[keep], nw[keep], g.age[keep])
         conv, cnt = orc.check(self.kept.w, n_p, delta)
-        return (conv if algo != 1 else False), self.kept.m, cnt
+        return (conv if algo in (0, 2) else False), self.kept.m, cnt   # louvain loops have check #1
 
     def closure_sample(self, attempts, iteration):
         pairs = orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration)
@@ -95,11 +104,12 @@ class OracleEngine:
     def closure_apply(self, algo, n_p, delta, counts, iteration):
         cu, cv, cf = self.cand
         base = np.int64(iteration + 1) << orc.AGE_ITER_SHIFT
-        w = counts.numpy()[:len(cu)].astype(np.int32) if (algo != 1 and counts is not None) else \
+        louv = algo in (0, 2)                          # lpm and infomap: weight-0 closure, no repair
+        w = counts.numpy()[:len(cu)].astype(np.int32) if (louv and counts is not None) else \
             np.zeros(len(cu), np.int32)
         closure = orc.EdgeGraph(self.g.N, cu, cv, w, base + cf)
         parts = [self.kept, closure]
-        if algo != 1:
+        if louv:
             deg = self.kept.degrees() + closure.degrees()
             ru, rv, rw, rx = orc.repair(self.g, deg, self.sigma)
             parts.append(orc.EdgeGraph(self.g.N, ru, rv, rw, base + orc.AGE_REPAIR_OFFSET + rx))

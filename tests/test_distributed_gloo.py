@@ -65,7 +65,8 @@ def _single(algo, n_p, tau, delta):
 
 
 # n_p=10 louvain runs 9 consensus iterations on this graph (closure + repair every time)
-@pytest.mark.parametrize("world,algo,n_p,tau", [(2, 0, 10, 0.2), (2, 1, 4, 0.8), (3, 0, 12, 0.2), (2, 2, 10, 0.2)])
+@pytest.mark.parametrize("world,algo,n_p,tau", [(2, 0, 10, 0.2), (2, 1, 4, 0.8), (3, 0, 12, 0.2), (2, 2, 10, 0.2),
+                                                (2, 3, 6, 0.2), (3, 4, 5, 0.6)])
 def test_sharded_equals_single_rank(world, algo, n_p, tau):
     ref_labels, ref_graph, ref_st = _single(algo, n_p, tau, 0.02)
     with tempfile.TemporaryDirectory() as d:
