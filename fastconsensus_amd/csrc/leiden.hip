@@ -407,9 +407,11 @@ __device__ __forceinline__ void block_best_info(BRedI& red, double& bd, uint32_t
 
 // Long rows: one block per vertex; an LDS table of up to HLS slots, or (rows > HLIGHT) a
 // global table per block, cleared through the list of slots it created.
-template <bool IMPL, int MODE>
+template <bool IMPL, int MODE, int HS>
 __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
-    __shared__ int32_t lkey[HLS], lval[HLS];
+    // HS: LDS slots (HLS, or HLS/2 when no row of the level is longer than HLS/4: 32 KB instead
+    // of 64 KB per block, so 4-5 blocks per CU instead of 2)
+    __shared__ int32_t lkey[HS], lval[HS];
     __shared__ int s_n;
     __shared__ long long s_wown;
     __shared__ BRed red;
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
         const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
-        const bool lds = re - rb <= HLIGHT;
+        const bool lds = re - rb <= HS / 2;
         const uint32_t ts = lds ? tsize(re - rb) : (uint32_t)a.hslots;
         int32_t* keys = lds ? lkey : gkey;
         int32_t* vals = lds ? lval : gval;
@@ -1061,7 +1063,8 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         if (max_deg <= 64) k_lv_decide<IM, MD, 512, 4><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);  \
         else if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
         else k_lv_decide<IM, MD, LWS, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);               \
-        if (max_deg > LIGHT) k_lv_heavy<IM, MD><<<hg, LTB, 0, c.stream>>>(a, stamp);             \
+        if (max_deg > LIGHT && max_deg <= HLS / 4) k_lv_heavy<IM, MD, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, stamp); \
+        else if (max_deg > LIGHT) k_lv_heavy<IM, MD, HLS><<<hg, LTB, 0, c.stream>>>(a, stamp);   \
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
             if (impl && MODE == MODE_MOVE) LV_LAUNCH(true, MODE_MOVE);
