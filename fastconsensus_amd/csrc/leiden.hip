@@ -711,12 +711,12 @@ __global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const in
     }
     if (lane == 0) olen[xn] = cnt;
 }
-template <bool IMPL>
+template <bool IMPL, int HS>
 __global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* nid, const int32_t* moff,
                                                        const int32_t* mlist, const int64_t* ubo, int32_t* ocol,
                                                        int32_t* ow, int32_t* olen, const int32_t* hlist,
                                                        const int32_t* hcnt) {
-    __shared__ int32_t lkey[HLS], lval[HLS];
+    __shared__ int32_t lkey[HS], lval[HS];   // HLS, or HLS/2 when every member-row sum fits
     __shared__ int s_n;
     const int n = *hcnt;
     int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
@@ -725,7 +725,7 @@ __global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* 
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int64_t xn = hlist[i];
         const int64_t ubn = ubo[xn + 1] - ubo[xn];
-        const bool lds = ubn <= HLIGHT;
+        const bool lds = ubn <= HS / 2;
         const uint32_t ts = lds ? tsize(ubn) : (uint32_t)a.hslots;
         int32_t* keys = lds ? lkey : gkey;
         int32_t* vals = lds ? lval : gval;
@@ -1221,8 +1221,11 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
                 while (hs < 2 * ubmax) hs <<= 1;
             a.hslots = hs;
             const int hg = heavy_grid(hs);
-            if (impl) k_ag_rows_heavy<true><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
-            else k_ag_rows_heavy<false><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+            const bool small = ubmax <= HLS / 4;
+            if (impl && small) k_ag_rows_heavy<true, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+            else if (impl) k_ag_rows_heavy<true, HLS><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+            else if (small) k_ag_rows_heavy<false, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+            else k_ag_rows_heavy<false, HLS><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
         }
         int64_t* len64 = I64(B_LEN64, nUn + 1);
         k_ag_len64<<<nb(nUn + 1), LTB, 0, c.stream>>>(nUn, olen, len64);
