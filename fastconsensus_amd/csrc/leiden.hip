@@ -86,6 +86,7 @@ struct LvArgs {
     // vertex's external weight (row sum; its weighted degree kv also counts internal edges),
     // the two adjacency weights a move changes, 1/2M
     int64_t* out;
+    int64_t* mod;                // Infomap: per module {flow, exit weight} as one 16-byte record
     int64_t* qrep;
     const int64_t* sv;
     int32_t* mvo;                // [nU] Infomap: the old module of this bucket's movers (with mvt)
@@ -159,11 +160,13 @@ __device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* k
     const int gl = threadIdx.x & (GL - 1);
     bd = 0.0; bh = 0; bc = -1; bw = 0;
     const long long Q = a.qrep[r];
-    const InfoA A = info_a(a.inv, Q, a.out[own], a.tot[own], kvx, svx, wown);
+    const longlong2 mo = *(const longlong2*)(a.mod + 2 * (int64_t)own);
+    const InfoA A = info_a(a.inv, Q, mo.y, mo.x, kvx, svx, wown);
     for (uint32_t s = gl; s < ts; s += GL) {
         const int32_t k = keys[s];
         if (k < 0 || k == own) continue;
-        const double d = info_b(a.inv, A, Q, a.out[k], a.tot[k], kvx, svx, vals[s]);
+        const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);   // one gather: flow and exit
+        const double d = info_b(a.inv, A, Q, mk.y, mk.x, kvx, svx, vals[s]);
         const uint32_t h = tie_of(a, r, x, k);
         if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = vals[s]; }
     }
@@ -455,7 +458,10 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
         int32_t bc = -1, bw = 0;
         const int cnt = lds ? (int)ts : s_n;
         InfoA IA{};
-        if (MODE == MODE_INFO) IA = info_a(a.inv, a.qrep[r], a.out[own], a.tot[own], kvx, sv_of<IMPL>(a, x), wown);
+        if (MODE == MODE_INFO) {
+            const longlong2 mo = *(const longlong2*)(a.mod + 2 * (int64_t)own);
+            IA = info_a(a.inv, a.qrep[r], mo.y, mo.x, kvx, sv_of<IMPL>(a, x), wown);
+        }
         for (int q = threadIdx.x; q < cnt; q += LTB) {
             const int s = lds ? q : lst[q];
             const int32_t k = keys[s];
@@ -463,7 +469,8 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
             const long long val = vals[s];
             if (!lds) { gkey[s] = -1; gval[s] = 0; }   // clear for the next vertex (read before)
             if (MODE == MODE_INFO) {
-                const double d = info_b(a.inv, IA, a.qrep[r], a.out[k], a.tot[k], kvx, sv_of<IMPL>(a, x), val);
+                const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);
+                const double d = info_b(a.inv, IA, a.qrep[r], mk.y, mk.x, kvx, sv_of<IMPL>(a, x), val);
                 const uint32_t h = tie_of(a, r, x, k);
                 if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = (int32_t)val; }
                 continue;
@@ -506,8 +513,10 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
         int32_t* lab = MODE == MODE_REFINE ? a.R : a.P;
         const int32_t old = lab[x];
         lab[x] = t;
-        atomicAdd((unsigned long long*)&a.tot[t], (unsigned long long)kvx);
-        atomicAdd((unsigned long long*)&a.tot[old], (unsigned long long)(-kvx));
+        int64_t* tt = MODE == MODE_INFO ? a.mod + 2 * (int64_t)t : a.tot + t;
+        int64_t* to = MODE == MODE_INFO ? a.mod + 2 * (int64_t)old : a.tot + old;
+        atomicAdd((unsigned long long*)tt, (unsigned long long)kvx);
+        atomicAdd((unsigned long long*)to, (unsigned long long)(-kvx));
         if (MODE == MODE_REFINE) {
             atomicAdd(&a.rsize[t], 1);
             atomicAdd(&a.rsize[old], -1);
@@ -549,7 +558,7 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
             if (xo != yo) { add(xo, -w); add(yo, -w); dq -= 2 * w; }
             if (t != yn) { add(t, w); add(yn, w); dq += 2 * w; }
             for (int k = 0; k < nm; ++k)
-                if (d[k]) atomicAdd((unsigned long long*)&a.out[m[k]], (unsigned long long)d[k]);
+                if (d[k]) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)m[k] + 1], (unsigned long long)d[k]);
         }
         for (int off = 32; off; off >>= 1) dq += __shfl_xor(dq, off);
         if (lane == 0 && dq) atomicAdd((unsigned long long*)&a.qrep[rep_of<IMPL>(a, x)], (unsigned long long)dq);
@@ -626,7 +635,7 @@ __global__ void k_ag_nodes(LvArgs a, const int32_t* nid, int32_t* nrep, int64_t*
     nrep[xn] = rep_of<IMPL>(a, c);
     nkv[xn] = a.tot[c];   // rtot: the refined community's weighted degree
     mcnt[xn] = a.rsize[c];
-    if (nsv) nsv[xn] = a.out[c];   // Infomap: the module's exit weight = the new node's external weight
+    if (nsv) nsv[xn] = a.mod[2 * c + 1];   // Infomap: the module's exit weight = the new node's external weight
 }
 // pofR[R[x]] = P[x] (every member agrees: R refines P); prep[P] = min new id over members;
 // ub[new id] += deg(x)
@@ -813,27 +822,26 @@ __global__ void k_degree(int64_t N, const int64_t* rowptr, int64_t* deg) {
     if (v < N) deg[v] = rowptr[v + 1] - rowptr[v];
 }
 // level 0: every vertex its own module (flow = degree, exit = degree)
-__global__ void k_info_init0(int64_t N, int n_r, const int64_t* deg, int32_t* P, int64_t* ptot, int64_t* pout,
-                             int32_t* memb) {
+__global__ void k_info_init0(int64_t N, int n_r, const int64_t* deg, int32_t* P, int64_t* mod, int32_t* memb) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)n_r * N) return;
     P[i] = (int32_t)i;
-    ptot[i] = pout[i] = deg[i % N];
+    mod[2 * i] = mod[2 * i + 1] = deg[i % N];
     memb[i] = (int32_t)i;
 }
 // explicit level: singleton modules of the aggregate nodes
-__global__ void k_info_level(int64_t nU, const int64_t* kv, const int64_t* sv, int64_t* ptot, int64_t* pout) {
+__global__ void k_info_level(int64_t nU, const int64_t* kv, const int64_t* sv, int64_t* mod) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nU) return;
-    ptot[i] = kv[i];
-    pout[i] = sv[i];
+    mod[2 * i] = kv[i];
+    mod[2 * i + 1] = sv[i];
 }
 // the modules play the refined communities' part in the aggregation: R = P, sizes, totals
-__global__ void k_info_rclear(int64_t nU, const int64_t* ptot, int32_t* rsize, int64_t* rtot) {
+__global__ void k_info_rclear(int64_t nU, const int64_t* mod, int32_t* rsize, int64_t* rtot) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nU) return;
     rsize[c] = 0;
-    rtot[c] = ptot[c];
+    rtot[c] = mod[2 * c];
 }
 template <bool IMPL>
 __global__ void k_info_modules(LvArgs a) {
@@ -846,14 +854,14 @@ __global__ void k_info_modules(LvArgs a) {
 // codelength (bits, without the constant node-entropy term) of replica r's modules: one
 // block per finishing replica, fixed-order reduction (deterministic)
 __global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const int32_t* roff, const int32_t* rend,
-                                                      const int64_t* ptot, const int64_t* pout, const int64_t* qrep,
+                                                      const int64_t* mod, const int64_t* qrep,
                                                       double inv, double* cl) {
     __shared__ double sm[LTB];
     const int r = blockIdx.x;
     if (!fin[r]) return;
     double acc = 0.0;
     for (int64_t c = roff[r] + threadIdx.x; c < rend[r]; c += LTB)
-        acc += -2.0 * plogp2(pout[c] * inv) + plogp2((pout[c] + ptot[c]) * inv);
+        acc += -2.0 * plogp2(mod[2 * c + 1] * inv) + plogp2((mod[2 * c + 1] + mod[2 * c]) * inv);
     sm[threadIdx.x] = acc;
     __syncthreads();
     for (int k = LTB / 2; k > 0; k >>= 1) {
@@ -963,18 +971,17 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     int32_t* misc = I32(B_MISC, 2 * (int64_t)n_r + 16);
     FC_HIP(hipMemsetAsync(done, 0, n_r, c.stream));
     int64_t* deg = nullptr;
-    int64_t* ptot = nullptr;
-    int64_t* pout = nullptr;
+    int64_t* ptot = nullptr;   // Leiden: move-phase community totals
+    int64_t* mod = nullptr;    // Infomap: {flow, exit weight} per module
     int64_t* qrep = nullptr;
     double* dcl = nullptr;
     if (info) {
         deg = I64(B_DEG, N);
-        ptot = I64(B_PTOT, nU0);
-        pout = I64(B_POUT, nU0);
+        mod = I64(B_POUT, 2 * nU0);
         qrep = I64(B_QREP, n_r);
         dcl = (double*)I64(B_CL, n_r);
         k_degree<<<nb(N), LTB, 0, c.stream>>>(N, g.rowptr.as<int64_t>(), deg);
-        k_info_init0<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, deg, P, ptot, pout, memb);
+        k_info_init0<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, deg, P, mod, memb);
         std::vector<int64_t> q0(n_r, M2);   // singletons: total exit weight = every edge end
         FC_HIP(hipMemcpyAsync(qrep, q0.data(), 8 * (size_t)n_r, hipMemcpyHostToDevice, c.stream));
         sync(c);
@@ -993,7 +1000,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     LvArgs a{};
     a.N0 = N; a.M2 = M2; a.B = B;
     a.inv = M2 > 0 ? 1.0 / (double)M2 : 0.0;
-    a.out = pout; a.qrep = qrep;
+    a.mod = mod; a.qrep = qrep;
     a.roff = roff; a.rkey = rkey; a.done = done; a.moves = moves;
     a.heavy_cnt = hcnt;
     a.mvt = (unsigned long long*)I64(B_MVT, nU0);
@@ -1090,37 +1097,13 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         if (info) {
             // ---- Infomap: greedy passes (at most 10, until one moves nothing), then the
             // modules are the units the level aggregates
-            a.P = P; a.tot = ptot; a.out = pout; a.qrep = qrep;
+            a.P = P; a.mod = mod; a.qrep = qrep;
             for (int sw = 0; sw < 10; ++sw) {
                 ++lv_sweeps;
                 if (sweep(MODE_INFO, level, sw) == 0) break;
             }
-            if (getenv("FC_INFOMAP_DEBUG") && nU < 100000) {   // invariants: sum tot = 2M, sum out = Q per replica
-                sync(c);
-                std::vector<int64_t> ht(nU), ho(nU), hq(n_r);
-                std::vector<int32_t> hr0(n_r), hr1(n_r);
-                FC_HIP(hipMemcpy(ht.data(), ptot, 8 * nU, hipMemcpyDeviceToHost));
-                FC_HIP(hipMemcpy(ho.data(), pout, 8 * nU, hipMemcpyDeviceToHost));
-                FC_HIP(hipMemcpy(hq.data(), qrep, 8 * n_r, hipMemcpyDeviceToHost));
-                FC_HIP(hipMemcpy(hr0.data(), roff, 4 * n_r, hipMemcpyDeviceToHost));
-                FC_HIP(hipMemcpy(hr1.data(), rend, 4 * n_r, hipMemcpyDeviceToHost));
-                for (int r = 0; r < std::min(n_r, 4); ++r) {
-                    if (h_done[r]) continue;
-                    long long st = 0, so = 0;
-                    double Lh = 0;
-                    auto pl = [](double p) { return p > 0 ? p * log(p) * 1.4426950408889634 : 0.0; };
-                    for (int64_t x = hr0[r]; x < hr1[r]; ++x) {
-                        st += ht[x]; so += ho[x];
-                        Lh += -2 * pl(ho[x] * a.inv) + pl((ho[x] + ht[x]) * a.inv);
-                    }
-                    Lh += pl(hq[r] * a.inv);
-                    fprintf(stderr, "[fc] infomap dbg host L %.6f\n", Lh);
-                    fprintf(stderr, "[fc] infomap dbg trial %d level %d replica %d range [%d,%d) sum tot %lld (2M %lld) sum out %lld Q %lld\n",
-                            trial0, level, r, hr0[r], hr1[r], st, (long long)M2, so, (long long)hq[r]);
-                }
-            }
             a.R = R; a.rsize = rsize;
-            k_info_rclear<<<nb(nU), LTB, 0, c.stream>>>(nU, ptot, rsize, rtot);
+            k_info_rclear<<<nb(nU), LTB, 0, c.stream>>>(nU, mod, rsize, rtot);
             if (impl) k_info_modules<true><<<nb(nU), LTB, 0, c.stream>>>(a);
             else k_info_modules<false><<<nb(nU), LTB, 0, c.stream>>>(a);
             a.tot = rtot;
@@ -1151,7 +1134,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         if (any_fin) {
             uint8_t* dfin = (uint8_t*)(misc + n_r);
             FC_HIP(hipMemcpyAsync(dfin, fin.data(), n_r, hipMemcpyHostToDevice, c.stream));
-            if (info) k_info_codelen<<<n_r, LTB, 0, c.stream>>>(dfin, roff, rend, ptot, pout, qrep, a.inv, dcl);
+            if (info) k_info_codelen<<<n_r, LTB, 0, c.stream>>>(dfin, roff, rend, mod, qrep, a.inv, dcl);
             k_lv_final<<<nb(nU0), LTB, 0, c.stream>>>(N, n_r, dfin, memb, P, roff, c.spos.as<int32_t>(), lab_out);
             for (int r = 0; r < n_r; ++r) h_done[r] |= fin[r];
             FC_HIP(hipMemcpyAsync(done, h_done.data(), n_r, hipMemcpyHostToDevice, c.stream));
@@ -1256,10 +1239,9 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         nU = nUn;
         max_deg = nx.max_deg;
         if (info) {   // singleton modules of the aggregate nodes; the next loop trip optimises them
-            ptot = I64(B_PTOT, nU);
-            pout = I64(B_POUT, nU);
+            mod = I64(B_POUT, 2 * nU);
             R = I32(B_R, nU); rtot = I64(B_RTOT, nU); rsize = I32(B_RSIZE, nU);
-            k_info_level<<<nb(nU), LTB, 0, c.stream>>>(nU, cur.kv, cur.sv, ptot, pout);
+            k_info_level<<<nb(nU), LTB, 0, c.stream>>>(nU, cur.kv, cur.sv, mod);
             if (c.trace) {
                 sync(c);
                 fprintf(stderr, "[fc] infomap level %d: %lld union vertices, %lld entries, max degree %d\n", level + 1,
