@@ -1095,10 +1095,11 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     for (;; ++level) {
         set_graph();
         if (info) {
-            // ---- Infomap: greedy passes (at most 10, until one moves nothing), then the
+            // ---- Infomap: greedy passes until one moves nothing (igraph: until the codelength
+            // stops improving; its tune() every 10 passes only refreshes float flows), then the
             // modules are the units the level aggregates
             a.P = P; a.mod = mod; a.qrep = qrep;
-            for (int sw = 0; sw < 10; ++sw) {
+            for (int sw = 0; sw < c.max_sweeps; ++sw) {
                 ++lv_sweeps;
                 if (sweep(MODE_INFO, level, sw) == 0) break;
             }

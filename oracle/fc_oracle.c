@@ -608,8 +608,8 @@ int orc_leiden(i64 N, const i64* rowptr, const i32* col, const i32* w, u64 seed,
  * edges leaving module i),
  *   L = plogp(sum_i q_i) - 2 sum_i plogp(q_i) - sum_a plogp(p_a) + sum_i plogp(q_i + p_i),
  * is minimised by igraph's greedy core: passes over the nodes in random order, each node
- * moving to the neighbour module of the most negative delta-L (< -1e-10), at most 10 passes
- * or until a pass moves nothing; then the modules become the nodes of the next level
+ * moving to the neighbour module of the most negative delta-L (< -1e-10), passes until one
+ * moves nothing (igraph: until the codelength stops improving); then the modules become the nodes of the next level
  * (aggregation), until a level merges nothing.  The best of `trials` runs (smallest L) is
  * kept.  igraph's alternating sub-module / single-node re-partitioning rounds around this
  * core are NOT restated (documented deviation).  log base 2 as igraph.
@@ -654,7 +654,7 @@ static double im_trial(i64 N, const i64* rowptr, const i32* col, u64* s, i32* la
     for (i64 v = 0; v < N; ++v) Q += sv[v];
     while (M2 > 0) {
         for (i64 v = 0; v < g.n; ++v) { P[v] = (i32)v; tot[v] = g.kv[v]; out[v] = sv[v]; order[v] = (i32)v; }
-        for (int pass = 0; pass < 10; ++pass) {
+        for (int pass = 0; pass < 200; ++pass) {   /* igraph: until the codelength stops improving */
             shuffle_i32(order, g.n, s);
             i64 moved = 0;
             for (i64 t = 0; t < g.n; ++t) {
