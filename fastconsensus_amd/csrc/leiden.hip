@@ -81,6 +81,8 @@ struct LvArgs {
     int32_t* hlst;            // [LHB][hslots] created slots
     int64_t hslots;
     unsigned long long* moves;   // [MSH]
+    unsigned long long* rmoves;  // Infomap: [n_r] moves of each replica in this pass
+    const uint8_t* lvdone;       // Infomap: [n_r] replica's passes at this level are over (a pass moved nothing)
     unsigned long long* mvt;     // [nU] move phase: (bucket stamp << 32) | target of this bucket's movers
     // Infomap (map equation): module exit weights, the replica's total exit weight, every
     // vertex's external weight (row sum; its weighted degree kv also counts internal edges),
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             } else if (MODE == MODE_REFINE) {
                 elig = a.rsize[a.R[x0]] == 1;   // only nodes still alone in their refined community
             } else {
-                elig = true;                    // Infomap: full passes
+                elig = !a.lvdone[r];            // Infomap: full passes until the replica's pass moves nothing
             }
         }
     }
@@ -577,22 +579,45 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
 }
 template <bool IMPL, int MODE>
 __global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk, uint32_t stamp) {
+    // Infomap: moves per replica (a decide block's 256 union ids span at most two replicas of the
+    // input graph: LDS counters for those, global atomics otherwise)
+    __shared__ unsigned long long s_rm[2];
     unsigned long long mv = 0;
-    const int wv = threadIdx.x >> 6;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int32_t r0 = 0;
+    if (MODE == MODE_INFO) {
+        if (threadIdx.x < 2) s_rm[threadIdx.x] = 0;
+        if ((int)blockIdx.x < nblk) r0 = rep_of<IMPL>(a, (int64_t)blockIdx.x * LTB);
+        __syncthreads();
+    }
+    auto count_rep = [&](int64_t x) {
+        if (MODE != MODE_INFO || lane != 0) return;
+        const int32_t r = rep_of<IMPL>(a, x);
+        if ((int)blockIdx.x < nblk && r - r0 < 2) atomicAdd(&s_rm[r - r0], 1ull);
+        else atomicAdd(&a.rmoves[r], 1ull);
+    };
     if ((int)blockIdx.x < nblk) {
         const int n = a.bcnt[blockIdx.x];
         for (int i = wv; i < n; i += LTB / 64) {
             const int64_t q = (int64_t)blockIdx.x * LTB + i;
             lv_move<IMPL, MODE>(a, a.blist[q], a.btgt[q], stamp, mv);
+            count_rep(a.blist[q]);
         }
     } else {
         const int n = *a.heavy_cnt;
         for (int i = (blockIdx.x - nblk) * (LTB / 64) + wv; i < n; i += hblk * (LTB / 64)) {
             const int32_t t = a.htgt[i];
-            if (t >= 0) lv_move<IMPL, MODE>(a, a.heavy[i], t, stamp, mv);
+            if (t >= 0) {
+                lv_move<IMPL, MODE>(a, a.heavy[i], t, stamp, mv);
+                count_rep(a.heavy[i]);
+            }
         }
     }
-    if ((threadIdx.x & 63) == 0 && mv) atomicAdd(&a.moves[blockIdx.x & (MSH - 1)], mv);
+    if (lane == 0 && mv) atomicAdd(&a.moves[blockIdx.x & (MSH - 1)], mv);
+    if (MODE == MODE_INFO) {
+        __syncthreads();
+        if (threadIdx.x < 2 && s_rm[threadIdx.x]) atomicAdd(&a.rmoves[r0 + threadIdx.x], s_rm[threadIdx.x]);
+    }
 }
 
 // ---------------------------------------------------------------- level bookkeeping kernels
@@ -875,7 +900,7 @@ __global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const 
 enum {
     B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
     B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC, B_MVT,
-    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB,
+    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB, B_LVDONE, B_RMOVES,
     // aggregation scratch
     B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
     // explicit level graphs, ping-pong: rowptr, col, w, kv, rep, sv (x2)
@@ -1099,9 +1124,23 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             // stops improving; its tune() every 10 passes only refreshes float flows), then the
             // modules are the units the level aggregates
             a.P = P; a.mod = mod; a.qrep = qrep;
+            // a replica whose pass moved nothing is done at this level (re-sweeping it would
+            // move nothing again), so the trials and replicas still moving run alone
+            uint8_t* lvd = U8(B_LVDONE, n_r);
+            unsigned long long* rmv = (unsigned long long*)I64(B_RMOVES, n_r);
+            std::vector<uint8_t> h_lvd(h_done);
+            std::vector<unsigned long long> h_rmv(n_r);
+            FC_HIP(hipMemcpyAsync(lvd, h_lvd.data(), n_r, hipMemcpyHostToDevice, c.stream));
+            a.lvdone = lvd; a.rmoves = rmv;
             for (int sw = 0; sw < c.max_sweeps; ++sw) {
                 ++lv_sweeps;
-                if (sweep(MODE_INFO, level, sw) == 0) break;
+                FC_HIP(hipMemsetAsync(rmv, 0, 8 * (size_t)n_r, c.stream));
+                const unsigned long long mvs = sweep(MODE_INFO, level, sw);   // syncs
+                if (mvs == 0) break;
+                FC_HIP(hipMemcpy(h_rmv.data(), rmv, 8 * (size_t)n_r, hipMemcpyDeviceToHost));
+                for (int r = 0; r < n_r; ++r) h_lvd[r] |= h_rmv[r] == 0;
+                FC_HIP(hipMemcpyAsync(lvd, h_lvd.data(), n_r, hipMemcpyHostToDevice, c.stream));
+                sync(c);
             }
             a.R = R; a.rsize = rsize;
             k_info_rclear<<<nb(nU), LTB, 0, c.stream>>>(nU, mod, rsize, rtot);
