@@ -83,6 +83,9 @@ struct LvArgs {
     unsigned long long* moves;   // [MSH]
     unsigned long long* rmoves;  // Infomap: [n_r] moves of each replica in this pass
     const uint8_t* lvdone;       // Infomap: [n_r] replica's passes at this level are over (a pass moved nothing)
+    const int32_t* bmap;         // Infomap, input-graph level: launch only the replicas still moving --
+    int bpr;                     //   block b covers replica bmap[b / bpr], ids (b % bpr)*LTB.. of it
+    int nact;                    //   replicas in bmap
     unsigned long long* mvt;     // [nU] move phase: (bucket stamp << 32) | target of this bucket's movers
     // Infomap (map equation): module exit weights, the replica's total exit weight, every
     // vertex's external weight (row sum; its weighted degree kv also counts internal edges),
@@ -261,7 +264,11 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    const int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    if (IMPL && a.bmap) {
+        const int64_t loc = (int64_t)(blockIdx.x % a.bpr) * LTB + threadIdx.x;
+        x0 = loc < a.N0 ? (int64_t)a.bmap[blockIdx.x / a.bpr] * a.N0 + loc : a.nU;
+    }
     bool elig = false;
     if (x0 < a.nU) {
         const int32_t r = rep_of<IMPL>(a, x0);
@@ -587,7 +594,8 @@ __global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk, 
     int32_t r0 = 0;
     if (MODE == MODE_INFO) {
         if (threadIdx.x < 2) s_rm[threadIdx.x] = 0;
-        if ((int)blockIdx.x < nblk) r0 = rep_of<IMPL>(a, (int64_t)blockIdx.x * LTB);
+        if ((int)blockIdx.x < nblk)
+            r0 = (IMPL && a.bmap) ? a.bmap[blockIdx.x / a.bpr] : rep_of<IMPL>(a, (int64_t)blockIdx.x * LTB);
         __syncthreads();
     }
     auto count_rep = [&](int64_t x) {
@@ -900,7 +908,7 @@ __global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const 
 enum {
     B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
     B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC, B_MVT,
-    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB, B_LVDONE, B_RMOVES,
+    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB, B_LVDONE, B_RMOVES, B_BMAP,
     // aggregation scratch
     B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
     // explicit level graphs, ping-pong: rowptr, col, w, kv, rep, sv (x2)
@@ -1054,7 +1062,8 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             a.rowptr = cur.rowptr; a.col = cur.col; a.w = cur.w; a.kv = cur.kv; a.rep = cur.rep; a.sv = cur.sv;
         }
         if (info) a.mvo = I32(B_BWA, nU);
-        const int64_t nblk = nb(nU);
+        // block lists for scan grids, or (Infomap, input-graph level) per-replica grids of nb(N) blocks
+        const int64_t nblk = std::max<int64_t>(nb(nU), impl ? (int64_t)nb(N) * n_r : 0);
         a.blist = I32(B_BLIST, nblk * LTB);
         a.btgt = I32(B_BTGT, nblk * LTB);
         a.bcnt = I32(B_BCNT, nblk);
@@ -1084,7 +1093,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     auto sweep = [&](int MODE, int level, int sw) -> unsigned long long {
         set_keys(level, sw, (uint32_t)MODE);
         FC_HIP(hipMemsetAsync(moves, 0, 8 * MSH, c.stream));
-        const int nblk = (int)nb(nU);
+        const int nblk = a.bmap ? a.bpr * a.nact : (int)nb(nU);
         const int hg = heavy_grid(a.hslots);
         const int hblk = 64;
         for (int b = 0; b < B; ++b) {
@@ -1132,6 +1141,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             std::vector<unsigned long long> h_rmv(n_r);
             FC_HIP(hipMemcpyAsync(lvd, h_lvd.data(), n_r, hipMemcpyHostToDevice, c.stream));
             a.lvdone = lvd; a.rmoves = rmv;
+            a.bmap = nullptr;
             for (int sw = 0; sw < c.max_sweeps; ++sw) {
                 ++lv_sweeps;
                 FC_HIP(hipMemsetAsync(rmv, 0, 8 * (size_t)n_r, c.stream));
@@ -1140,8 +1150,19 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
                 FC_HIP(hipMemcpy(h_rmv.data(), rmv, 8 * (size_t)n_r, hipMemcpyDeviceToHost));
                 for (int r = 0; r < n_r; ++r) h_lvd[r] |= h_rmv[r] == 0;
                 FC_HIP(hipMemcpyAsync(lvd, h_lvd.data(), n_r, hipMemcpyHostToDevice, c.stream));
+                if (impl) {   // the next passes launch blocks for the replicas still moving only
+                    std::vector<int32_t> act;
+                    for (int r = 0; r < n_r; ++r)
+                        if (!h_lvd[r]) act.push_back(r);
+                    if (act.empty()) { sync(c); break; }
+                    int32_t* bm = I32(B_BMAP, n_r);
+                    FC_HIP(hipMemcpyAsync(bm, act.data(), 4 * act.size(), hipMemcpyHostToDevice, c.stream));
+                    a.bmap = bm; a.nact = (int)act.size(); a.bpr = (int)nb(N);
+                    sync(c);   // `act` is pageable and local
+                }
                 sync(c);
             }
+            a.bmap = nullptr;
             a.R = R; a.rsize = rsize;
             k_info_rclear<<<nb(nU), LTB, 0, c.stream>>>(nU, mod, rsize, rtot);
             if (impl) k_info_modules<true><<<nb(nU), LTB, 0, c.stream>>>(a);
