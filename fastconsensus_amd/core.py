@@ -301,7 +301,9 @@ class Cover:
     ascending), ``membership[j]`` is ``[cluster of vertex j]`` (:465-466) and ``len`` is the
     number of clusters.  igraph vertex j is the j-th smallest node label (``nx_to_igraph``
     adds ``sorted(G.nodes())``, :47).  Clusters are numbered by decreasing size, as leidenalg
-    renumbers its communities (ties: the cluster holding the smaller vertex first)."""
+    renumbers its communities (ties: the cluster holding the smaller vertex first).  Parity
+    unpinned: leidenalg is absent here, so this numbering (and the Leiden/Infomap partitions
+    themselves) are checked only against the restatement in oracle/fc_oracle.c."""
 
     def __init__(self, vertex_labels):
         lab = np.asarray(vertex_labels)
@@ -390,6 +392,12 @@ def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, se
             raise ValueError("the new_consensus.py rule exists for louvain only")
         algo = FC_ALGO_LOUVAIN_NC
     g = G if isinstance(G, IdGraph) else IdGraph.from_networkx(G)
+    if algo == FC_ALGO_LEIDEN and not np.issubdtype(np.asarray(g.labels).dtype, np.integer):
+        # The engine's leiden loop is the one-iteration exit the reference takes when its
+        # str(vertex id)-keyed lookup (:97) never matches an int node (:214-217).  With other
+        # node types that lookup can match and the reference runs a real loop: not modelled.
+        raise NotImplementedError("algorithm='leiden' is modelled for integer node labels only "
+                                  "(fast_consensus.py:97, :214-217)")
     with Engine(device=device, seed=seed) as eng:
         eng.set_option("store", store_order_pays(n_p))
         eng.load_graph(g.n, g.u, g.v)

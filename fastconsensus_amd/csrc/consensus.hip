@@ -282,21 +282,24 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
 }
 // This block's candidates (the attempts that created a slot, in attempt order) appended to
 // the accumulated list at the device-side count *nacc (no host round trip per block).
-__global__ void k_slot_flags(int64_t n, const int64_t* slot, int64_t* flag) {
+// The running count is snapshotted here (nacc[1] = nacc[0]), one launch before k_append_cand
+// reads it: reading and bumping nacc[0] inside one launch raced across workgroups.
+__global__ void k_slot_flags(int64_t n, const int64_t* slot, int64_t* flag, int64_t* nacc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     flag[i] = (i < n && slot[i] >= 0) ? 1 : 0;
+    if (i == n) nacc[1] = nacc[0];
 }
 __global__ void k_append_cand(int64_t n, const int64_t* slot, const int64_t* pos, const uint64_t* hkey,
                               const uint32_t* hval, int64_t t0, int64_t* nacc, uint64_t* akey, int64_t* aval) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t base = nacc[0];
+    const int64_t base = nacc[1];                  // the block's first entry (k_slot_flags); not written here
     if (i < n && slot[i] >= 0) {
         const int64_t h = slot[i];
         akey[base + pos[i]] = hkey[h];
         aval[base + pos[i]] = t0 + (int64_t)hval[h];
     }
-    if (i == n) { nacc[1] = base; nacc[0] = base + pos[n]; }   // [1]: the block's first entry
+    if (i == n) nacc[0] = base + pos[n];           // nobody in this launch reads [0]
 }
 // C graph, grown block by block: the new block's entries (both directions) are counted and
 // scattered per node (int32 atomics), then every node merges its old row with its sorted new
@@ -430,7 +433,7 @@ void closure_sample(Ctx& c, int64_t attempts, int iteration) {
                                                       r > 0 ? c.clo_rowptr.as<int64_t>() : nullptr,
                                                       r > 0 ? c.clo_col.as<int32_t>() : nullptr, bits, hkey, hval,
                                                       hsize - 1, slot);
-        k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, fl);
+        k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, fl, nacc);
         exclusive_scan(c, fl, ps, n + 1);
         k_append_cand<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, ps, hkey, hval, t0, nacc, akey, aval);
         if (r + 1 == R) continue;

@@ -1368,7 +1368,7 @@ void infomap_run(Ctx& c, int rbegin, int rcount, int n_p_total, int iteration) {
         for (int r = 0; r < rcount; ++r)
             for (int j = 0; j < k; ++j) {   // trial order: the earliest of equal codelengths wins
                 const size_t u = (size_t)r * k + j;
-                if (getenv("FC_INFOMAP_DEBUG") && r < 4)
+                if (c.trace && r < 4)
                     fprintf(stderr, "[fc] infomap trial %d replica %d codelength %.6f (best %.6f)\n", t0 + j, r, cl[u],
                             best[r]);
                 if (!(cl[u] < best[r])) continue;

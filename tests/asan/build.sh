@@ -13,7 +13,7 @@ for s in capi.cpp gen.cpp; do
     $HIPCC $FLAGS $SAN -c "$ROOT/fastconsensus_amd/csrc/$s" -o "$OUT/$s.o"
 done
 OBJ=$ROOT/fastconsensus_amd/lib/obj
-$HIPCC --offload-arch=gfx950 -fsanitize=address -fsanitize=undefined -g -o "$OUT/asan_driver" \
+$HIPCC --offload-arch=gfx950 $SAN -g -o "$OUT/asan_driver" \
     -x c "$ROOT/tests/asan/asan_driver.c" -x none "$OUT/capi.cpp.o" "$OUT/gen.cpp.o" \
     "$OBJ/graph.hip.o" "$OBJ/consensus.hip.o" "$OBJ/cd.hip.o" "$OBJ/leiden.hip.o"
 echo "built $OUT/asan_driver"

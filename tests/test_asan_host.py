@@ -18,6 +18,8 @@ def _asan_clean(p):
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc absent")
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "tests", "asan", "build.sh")),
+                    reason="tests/asan/ not shipped (it is CPU-only and listed in .gpurunignore)")
 def test_capi_host_code_under_asan(tmp_path):
     from fastconsensus_amd.build import build
     build(verbose=False)                                   # the regular device objects
@@ -50,7 +52,9 @@ def test_oracle_under_asan(tmp_path):
             "    lab, sw = orc.engine_cd(c.algo, g[0], 3, 0, 0, 5)\n"
             "    lab2, _ = orc.cd_batch(c.algo, 2, g[0], seed=5, nthreads=2)\n"
             "print('oracle under asan ok')\n" % (ROOT, lib))
-    env = dict(os.environ, LD_PRELOAD=libasan, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+    # libasan must come first; whatever the environment already preloads stays after it
+    pre = ":".join(x for x in (libasan, os.environ.get("LD_PRELOAD", "")) if x)
+    env = dict(os.environ, LD_PRELOAD=pre, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1", OMP_NUM_THREADS="2")
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
     _asan_clean(p)
