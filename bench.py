@@ -177,12 +177,20 @@ def cpu_baseline(n, u, v, cfg, seed):
 
 
 def load_traffic(config):
+    """HBM bytes per decide launch from profiles/pmc_<config>.json, only when that profile was
+    taken on a library built from the same sources as the one being timed (csrc_hash);
+    returns (bytes or None, note)."""
+    from fastconsensus_amd.build import built_hash
     p = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
-    if os.path.exists(p):
-        with open(p) as f:
-            d = json.load(f)
-        return d.get("decide_hbm_bytes_per_launch")
-    return None
+    if not os.path.exists(p):
+        return None, "no PMC profile for %s" % config
+    with open(p) as f:
+        d = json.load(f)
+    lib, prof = built_hash(), d.get("csrc_hash")
+    if not lib or prof != lib:
+        return None, "PMC profile %s is from csrc %s, the timed library from %s: traffic not attached" % (
+            os.path.basename(p), prof, lib)
+    return d.get("decide_hbm_bytes_per_launch"), "traffic from %s (csrc %s)" % (os.path.basename(p), prof)
 
 
 # ------------------------------------------------------------------------------- launcher
@@ -374,9 +382,12 @@ def main():
         avg_s = tim["decide_ms"] / launches / 1e3
         bytes_per_launch = tim["decide_bytes"] / launches
         achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-        traffic = load_traffic(args.config) if args.n_p <= 0 else None   # the PMC summary is for the config's n_p
+        if args.n_p <= 0:
+            traffic, traffic_note = load_traffic(args.config)
+        else:
+            traffic, traffic_note = None, "the PMC summary is for the config's n_p"
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                 "kernel": "k_decide_light<%s>" % ("true" if algo != 1 else "false"),
                 "note": (None if cfg["algo"] in ("louvain", "lpm") else
                          "the %s CD runs its own kernels (leiden.hip); this roofline covers the Louvain-engine "

@@ -3,6 +3,7 @@
     python -m fastconsensus_amd.build      # or __graft_entry__.build()
 """
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -11,6 +12,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 OUT_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(OUT_DIR, "libfastconsensus_amd.so")
+SRC_HASH = LIB + ".srchash"     # the source hash the library was built from (profiles are matched to it)
 SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "leiden.hip", "capi.cpp", "gen.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -25,6 +27,27 @@ def _obj(src):
 def _deps():
     return [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + \
         [os.path.join(os.path.dirname(PKG), "include", "fastconsensus_amd.h")]
+
+
+def source_hash():
+    """sha256 (16 hex) over the library's sources and header, by name: what a PMC profile under
+    profiles/ records, so bench.py attaches traffic only from a profile of the same code."""
+    h = hashlib.sha256()
+    for d in sorted(_deps(), key=os.path.basename):
+        if os.path.isfile(d):
+            h.update(os.path.basename(d).encode())
+            with open(d, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash():
+    """Source hash recorded when the library was linked (None if unknown)."""
+    try:
+        with open(SRC_HASH) as f:
+            return f.read().strip() or None
+    except OSError:
+        return None
 
 
 def _compile(src):
@@ -44,10 +67,13 @@ def build(verbose=True, jobs=None):
     jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2), 8)
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, SOURCES))
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs) \
+            and built_hash() == source_hash():
         return LIB
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
     subprocess.check_call(cmd)
+    with open(SRC_HASH, "w") as f:
+        f.write(source_hash() + "\n")
     if verbose:
         print("built", LIB, file=sys.stderr)
     return LIB

@@ -1142,3 +1142,63 @@ void orc_closure_sample(i64 N, const i64* krowptr, const i32* kcol, i64 attempts
     }
     free(crow); free(ccol); free(cand); free(rk);
 }
+
+/* ------------------------------------------------------------------ sequential closure
+ * The reference's closure loop itself (fast_consensus.py:175-184, :292-300), one attempt after
+ * the other on a GROWING nextgraph: node x uniform over all N (np.random.choice, :177); if
+ * it has >= 2 neighbours, two distinct ones uniformly (random.sample(set(...), 2), :181); if
+ * a-b is absent (:183) it is added and is a neighbour / an edge for every later attempt.  The
+ * RNG is the oracle's own (the reference's numpy/random streams cannot be reproduced), so
+ * this is the reference's sampling DISTRIBUTION.  Used only as the reference-semantics
+ * baseline of the engine's blocked sampler (tests/golden/make_refsem.py c3).
+ * pairs_out: the added pairs in attempt order; returns their count (<= attempts). */
+typedef struct { i32* a; i32 n, cap; } seq_row;
+static void seq_push(seq_row* r, i32 x) {
+    if (r->n == r->cap) { r->cap = r->cap ? 2 * r->cap : 4; r->a = (i32*)realloc(r->a, sizeof(i32) * (size_t)r->cap); }
+    r->a[r->n++] = x;
+}
+static inline u64 seq_key(i32 a, i32 b) {
+    const u64 u = (u64)(uint32_t)(a < b ? a : b), v = (u64)(uint32_t)(a < b ? b : a);
+    return (u << 32) | v;
+}
+static int seq_insert(u64* tab, u64 mask, u64 k) {   /* 1 when newly inserted */
+    u64 h = tw_mix64(k) & mask;
+    while (tab[h] != ~0ull) {
+        if (tab[h] == k) return 0;
+        h = (h + 1) & mask;
+    }
+    tab[h] = k;
+    return 1;
+}
+i64 orc_closure_sequential(i64 N, i64 m, const i32* eu, const i32* ev, i64 attempts, u64 seed, i32* pairs_out) {
+    seq_row* rows = (seq_row*)calloc((size_t)(N > 0 ? N : 1), sizeof(seq_row));
+    u64 tsize = 1024;
+    while (tsize < 2 * (u64)(m + attempts + 1)) tsize <<= 1;
+    u64* tab = (u64*)malloc(sizeof(u64) * tsize);
+    memset(tab, 0xff, sizeof(u64) * tsize);
+    for (i64 i = 0; i < m; ++i) {
+        seq_push(&rows[eu[i]], ev[i]);
+        seq_push(&rows[ev[i]], eu[i]);
+        seq_insert(tab, tsize - 1, seq_key(eu[i], ev[i]));
+    }
+    u64 s = seed ^ 0x5E9C105Eull;
+    i64 k = 0;
+    for (i64 t = 0; t < attempts && N > 0; ++t) {
+        const i32 x = (i32)rng_below(&s, (u64)N);
+        const i32 d = rows[x].n;
+        if (d < 2) continue;
+        const i32 i1 = (i32)rng_below(&s, (u64)d);
+        i32 i2 = (i32)rng_below(&s, (u64)(d - 1));
+        if (i2 >= i1) ++i2;
+        const i32 a = rows[x].a[i1], b = rows[x].a[i2];
+        if (!seq_insert(tab, tsize - 1, seq_key(a, b))) continue;
+        seq_push(&rows[a], b);
+        seq_push(&rows[b], a);
+        pairs_out[2 * k] = a;
+        pairs_out[2 * k + 1] = b;
+        ++k;
+    }
+    for (i64 x = 0; x < N; ++x) free(rows[x].a);
+    free(rows); free(tab);
+    return k;
+}

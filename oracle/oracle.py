@@ -78,6 +78,8 @@ def lib():
                                     ctypes.c_int, ctypes.c_int, _i32p, _i32p]
         L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
+        L.orc_closure_sequential.argtypes = [i64, i64, _i32p, _i32p, i64, u64, _i32p]
+        L.orc_closure_sequential.restype = i64
         _lib = L
     return _lib
 
@@ -198,6 +200,42 @@ def closure_sample_pairs(kept, attempts, seed, iteration, rounds=CLOSURE_ROUNDS)
     lib().orc_closure_sample(kept.N, rowptr, col, int(attempts), int(seed) & (2**64 - 1), int(iteration),
                              int(rounds), pairs)
     return pairs[:attempts]
+
+
+def closure_sequential_pairs(kept, attempts, seed):
+    """The reference's own closure loop (fast_consensus.py:175-184, :292-300): attempts one
+    after the other on the growing graph; returns the pairs it added, in attempt order
+    (orc_closure_sequential; the oracle's RNG, the reference's distribution)."""
+    out = np.empty((max(int(attempts), 1), 2), np.int32)
+    k = lib().orc_closure_sequential(kept.N, kept.m, kept.u, kept.v, int(attempts), int(seed) & (2**64 - 1), out)
+    return out[:k].copy()
+
+
+def refsem_run(algo, g0, n_p, tau, delta, seed, nthreads=0, max_iters=100):
+    """The reference while-loop and final pass (fast_consensus.py:129-202 louvain, :260-310
+    lpm, :383-392) with the oracle's sequential CD restatements (python-louvain level 0 /
+    igraph LPA, one fresh stream per batch) and the SEQUENTIAL closure over the growing graph:
+    the reference's semantics at sizes where running the reference script itself is infeasible
+    (its np.random.choice(nodes) closure is O(L*N) per iteration).  Every step but the CD and the
+    closure's RNG is the golden-pinned replay (`iterate`).  Returns (final labels [n_p][N],
+    iterations)."""
+    graph = g0
+    L = g0.m                                        # L = G.number_of_edges(), :132/:144
+    for it in range(max_iters):
+        lab, _ = cd_batch(algo, n_p, graph, seed=seed * 1000003 + it, nthreads=nthreads)
+        w_new = consensus(algo, graph, lab, n_p)
+        keep = threshold(w_new, tau, n_p)
+        kept = EdgeGraph(graph.N, graph.u[keep], graph.v[keep], w_new[keep], graph.age[keep])
+        pairs = None
+        if algo != LPM and check(kept.w, n_p, delta)[0]:
+            break                                   # check #1: final pass on the old graph
+        pairs = closure_sequential_pairs(kept, L, seed * 7919 + it)
+        new, tr = iterate(algo, graph, lab, pairs, n_p, tau, delta, it)
+        graph = new
+        if tr["check2"][0]:
+            break
+    lab, _ = cd_batch(algo, n_p, graph, seed=seed * 1000003 + 999, nthreads=nthreads)
+    return lab, it + 1
 
 
 def repair(old, deg, sigma=None):

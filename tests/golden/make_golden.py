@@ -13,7 +13,9 @@ unmodified; only its three un-vendored third-party imports are replaced by stubs
   ``community_label_propagation().as_cover()`` runs networkx ``asyn_lpa_communities``
   (unweighted, seeded) on the vertex-id graph that ``nx_to_igraph``
   (fast_consensus.py:41-52) builds.
-* ``leidenalg``: empty module (out of scope).
+* ``leidenalg``: ``find_partition(...).as_cover()`` returns a seeded networkx louvain level 0
+  (stand-in), and the module's ``mp.Pool`` is a serial map, so the reference's leiden
+  branch runs in this process and its exit point is recorded.
 
 Every community-detection result is RECORDED, as are the closure samples
 (``random.sample`` at fast_consensus.py:181/297), the adjacency order of ``graph``
@@ -25,8 +27,8 @@ bit-exactly (weights, keep masks, convergence decisions, closure/repair edges).
 The same harness runs the ``new_consensus.py`` fork (its weight rule, :155-163, is the
 ``louvain_nc`` variant).
 
-Usage:  python tests/golden/make_golden.py [nc]   (writes tests/golden/*.npz, *.json;
-        ``nc``: only the new_consensus.py cases)
+Usage:  python tests/golden/make_golden.py [nc|r03]   (writes tests/golden/*.npz, *.json;
+        ``nc``: only the new_consensus.py cases; ``r03``: only the round-3 cases)
 """
 import contextlib
 import importlib.util
@@ -170,8 +172,80 @@ class Graph:
         return _Cover(comms)
 
 
+def _community_infomap(self, *a, **k):
+    # stand-in for igraph's Infomap (absent): networkx louvain level 0 on the vertex-id graph,
+    # unweighted as called (fast_consensus.py:268, :390); only the loop around it is pinned
+    H = nx.Graph()
+    H.add_nodes_from(range(len(self.names)))
+    H.add_edges_from(self.edges)
+    _on_cd_call(None)
+    rs = REC.seed * 100003 + REC.calls
+    comms = [sorted(c) for c in next(iter(nx.community.louvain_partitions(H, seed=rs)))]
+    lab = np.full(len(self.names), -1, np.int32)
+    for ci, c in enumerate(comms):
+        for v in c:
+            lab[REC.node_index[v]] = ci
+    REC.cd_labels.append(lab)
+    return _Cover(comms)
+
+
+Graph.community_infomap = _community_infomap
+
 igraph_stub = types.ModuleType("igraph")
 igraph_stub.Graph = Graph
+
+
+# ---------------------------------------------------------------- stub: leidenalg
+class _LeidenResult:
+    def __init__(self, comms):
+        self._c = comms
+
+    def as_cover(self):
+        return self._c
+
+
+def _find_partition(graph, partition_type, weights=None, seed=None, n_iterations=2, **k):
+    """Stand-in for leidenalg.find_partition (absent): a seeded networkx louvain level 0 on the
+    vertex-id graph nx_to_igraph built (fast_consensus.py:123).  Clusters are lists of igraph
+    vertex ids, as as_cover() yields them."""
+    H = nx.Graph()
+    H.add_nodes_from(range(len(graph.names)))
+    H.add_edges_from(graph.edges)
+    _on_cd_call(None)
+    rs = REC.seed * 100003 + REC.calls * 7 + int(seed or 0)
+    comms = [sorted(c) for c in next(iter(nx.community.louvain_partitions(H, seed=rs)))]
+    lab = np.full(len(graph.names), -1, np.int32)
+    for ci, c in enumerate(comms):
+        for v in c:
+            lab[REC.node_index[v]] = ci      # vertex id == node label for 0..N-1 graphs (README:62)
+    REC.cd_labels.append(lab)
+    return _LeidenResult(comms)
+
+
+leiden_stub = types.ModuleType("leidenalg")
+leiden_stub.find_partition = _find_partition
+leiden_stub.ModularityVertexPartition = object
+
+
+class _SerialPool:
+    """multiprocessing.Pool replaced by a serial map (fast_consensus.py:210-211, :386-387):
+    the recorder and the seeded RNGs live in this process."""
+
+    def __init__(self, processes=None):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+    def map(self, f, it):
+        return [f(x) for x in it]
+
+
+mp_stub = types.ModuleType("multiprocessing")
+mp_stub.Pool = _SerialPool
 
 
 # ---------------------------------------------------------------- recording RNG proxy
@@ -192,10 +266,11 @@ class _RecordingRandom:
 def load_reference(path=REF):
     sys.modules["community"] = community_stub
     sys.modules["igraph"] = igraph_stub
-    sys.modules["leidenalg"] = types.ModuleType("leidenalg")
+    sys.modules["leidenalg"] = leiden_stub
     spec = importlib.util.spec_from_file_location("fc_reference_%d" % len(path), path)
     fc = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fc)
+    fc.mp = mp_stub
     orig_check = fc.check_consensus_graph
 
     def check_wrapper(G, n_p, delta):
@@ -249,7 +324,12 @@ def run_case(fc, name, edgefile, algorithm, n_p, tau, delta, seed, max_iters=30,
     # final output as labels (id space)
     finals = []
     for part in out:
-        if isinstance(part, dict):
+        if algorithm == "leiden":            # as_cover(): clusters of igraph vertex ids (== node ids here)
+            lab = np.full(len(nodes), -1, np.int32)
+            for ci, c in enumerate(part):
+                for v in c:
+                    lab[REC.node_index[v]] = ci
+        elif isinstance(part, dict):
             lab = np.array([part[v] for v in nodes], np.int32)
         else:
             lab = np.full(len(nodes), -1, np.int32)
@@ -362,9 +442,46 @@ def main_nc():
     run_case(nc, "lfr1k_louvain_nc_np20", lfr, "louvain", 20, 0.2, 0.02, seed=13, rule="new_consensus")
 
 
+def main_r03():
+    """Round-3 cases (existing fixtures untouched):
+    * lpm on the native LFR n=1000 mu=0.55 graph, where LPA finds structure (the networkx
+      mu=0.4 graph floods to one community), so the recorded LPA labelings are non-degenerate;
+    * the leiden branch (fast_consensus.py:204-258, final pass :385-388) with leidenalg and
+      the process pool stubbed: records where the reference exits;
+    * the infomap branch (the lpm loop, :260-310, with community_infomap, :268, :390)."""
+    karate = os.path.join(HERE, "karate_club.txt")
+    lfr = os.path.join(HERE, "lfr1k_mu04.txt")
+    mu055 = os.path.join(HERE, "lfr1k_mu055_synth.txt")
+    fc = load_reference()
+    run_case(fc, "karate_leiden_np20", karate, "leiden", 20, 0.2, 0.02, seed=31)
+    run_case(fc, "lfr1k_leiden_np20", lfr, "leiden", 20, 0.2, 0.02, seed=32)
+    if os.environ.get("FC_GOLDEN_ONLY") == "leiden":
+        return
+    best = (-1, None)                        # the seed whose first reference LPA batch has most k > 1 replicas
+    for seed in range(21, 41):
+        run_case(fc, "lfr1k_mu055_lpm_np20", mu055, "lpm", 20, 0.8, 0.02, seed=seed)
+        nd = sum(len(np.unique(x)) > 1 for x in REC.cd_labels[:20])
+        best = max(best, (nd, seed))
+    run_case(fc, "lfr1k_mu055_lpm_np20", mu055, "lpm", 20, 0.8, 0.02, seed=best[1])
+    # a graph well inside LPA's detectable range (native LFR n=1000 mu=0.3): every replica finds structure
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from fastconsensus_amd import synth
+    mu03 = os.path.join(HERE, "lfr1k_mu03_synth.txt")
+    u, v, planted = synth.lfr(1000, 0.3, seed=8)
+    with open(mu03, "w") as f:
+        for a, b in zip(u.tolist(), v.tolist()):
+            f.write("%d %d\n" % (a, b))
+    np.save(os.path.join(HERE, "lfr1k_mu03_synth_planted.npy"), planted)
+    run_case(fc, "lfr1k_mu03_lpm_np20", mu03, "lpm", 20, 0.8, 0.02, seed=41)
+    run_case(fc, "karate_infomap_np20", karate, "infomap", 20, 0.6, 0.02, seed=33)
+    run_case(fc, "lfr1k_infomap_np20", lfr, "infomap", 20, 0.6, 0.02, seed=34)
+
+
 def main():
     if sys.argv[1:] == ["nc"]:
         return main_nc()
+    if sys.argv[1:] == ["r03"]:
+        return main_r03()
     shutil.copy(KARATE, os.path.join(HERE, "karate_club.txt"))
     karate = os.path.join(HERE, "karate_club.txt")
     lfr = make_lfr1k()

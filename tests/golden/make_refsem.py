@@ -18,7 +18,7 @@ partitions to the planted communities is recorded, so a device run is compared w
 reference's distribution, not with a single sample (the consensus NMI varies from run to run:
 0.80-0.95 on LFR-1k).  Output: tests/golden/refsem_*.json (data only).
 
-Usage:  python tests/golden/make_refsem.py
+Usage:  python tests/golden/make_refsem.py [c3]   (c3: the LFR-100k records, see run_c3)
 """
 import importlib.util
 import json
@@ -160,7 +160,43 @@ def make_lfr1k_mu055_synth():
     return path
 
 
+def run_c3(algorithm, tau, seeds, n_p=64):
+    """C3 (LFR n=100k mu=0.5, n_p=64; BASELINE configs[2]): the reference script's closure is
+    O(L*N) per iteration there (np.random.choice over the node view, :177), so the reference
+    loop is run as its restatement orc.refsem_run -- the golden-pinned replay steps with the
+    sequential CD restatements and the SEQUENTIAL closure over the growing graph.  At 1k,
+    refsem_run's NMI distribution matches the reference script's own
+    (tests/test_oracle_golden.py::test_refsem_loop_matches_reference_loop_distribution)."""
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    from fastconsensus_amd import synth
+    u, v, planted = synth.lfr(100_000, 0.5, seed=42)
+    g = orc.EdgeGraph.from_lines(100_000, np.stack([u, v], 1))
+    algo = 0 if algorithm == "louvain" else 1
+    name = "lfr100k_%s_np%d" % (algorithm, n_p)
+    rec = {"name": name, "algorithm": algorithm, "n_p": n_p, "tau": tau, "delta": 0.02,
+           "graph": "fastconsensus_amd.synth.lfr(100000, 0.5, seed=42)", "N": 100_000, "m": int(g.m), "seeds": [],
+           "nmi": [], "k": [], "iterations": [],
+           "cd": "oracle restatement (orc_louvain_level0 / orc_lpa)",
+           "loop": "orc.refsem_run: reference loop restated (golden-pinned steps), sequential closure"}
+    for seed in seeds:
+        lab, it = orc.refsem_run(algo, g, n_p, tau, 0.02, seed=seed, nthreads=8)
+        rec["seeds"].append(seed)
+        rec["nmi"].append(float(np.mean([nmi(planted, x) for x in lab])))
+        rec["k"].append(float(np.mean([len(np.unique(x)) for x in lab])))
+        rec["iterations"].append(int(it))
+        print(name, seed, "NMI %.4f k %.1f iterations %d" % (rec["nmi"][-1], rec["k"][-1], it), flush=True)
+    rec["nmi_mean"] = float(np.mean(rec["nmi"]))
+    rec["nmi_sd"] = float(np.std(rec["nmi"]))
+    with open(os.path.join(HERE, "refsem_%s.json" % name), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(name, "mean %.4f sd %.4f" % (rec["nmi_mean"], rec["nmi_sd"]))
+
+
 def main():
+    if sys.argv[1:] == ["c3"]:
+        run_c3("louvain", 0.2, list(range(16)))
+        run_c3("lpm", 0.8, list(range(8)))
+        return
     fc = load_reference()
     seeds = list(range(30))
     run(fc, "lfr1k_louvain_np20", os.path.join(HERE, "lfr1k_mu04.txt"), os.path.join(HERE, "lfr1k_mu04_planted.npy"),

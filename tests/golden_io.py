@@ -6,7 +6,10 @@ import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["karate_louvain_np50", "karate_lpm_np20", "lfr1k_louvain_np20", "lfr1k_lpm_np20",
-         "karate_louvain_nc_np50", "lfr1k_louvain_nc_np20"]   # nc: new_consensus.py's weight rule
+         "karate_louvain_nc_np50", "lfr1k_louvain_nc_np20",    # nc: new_consensus.py's weight rule
+         "lfr1k_mu055_lpm_np20", "lfr1k_mu03_lpm_np20",        # lpm where LPA finds structure
+         "karate_infomap_np20", "lfr1k_infomap_np20"]          # infomap: the lpm loop (:260-310)
+LEIDEN_CASES = ["karate_leiden_np20", "lfr1k_leiden_np20"]     # the leiden branch's exit (:204-258)
 
 
 class Case:
@@ -16,8 +19,10 @@ class Case:
         z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
         self.z = {k: z[k] for k in z.files}
         self.name = name
-        # 0 louvain, 1 lpm, 2 louvain with the new_consensus.py rule (FC_ALGO_LOUVAIN_NC)
-        self.algo = 1 if self.meta["algorithm"] == "lpm" else (2 if self.meta.get("rule") == "new_consensus" else 0)
+        # loop rule: 0 louvain, 1 lpm (and infomap: the same loop, :260-310), 2 louvain with the
+        # new_consensus.py rule (FC_ALGO_LOUVAIN_NC), 3 leiden (:204-258)
+        a = self.meta["algorithm"]
+        self.algo = {"lpm": 1, "infomap": 1, "leiden": 3}.get(a, 2 if self.meta.get("rule") == "new_consensus" else 0)
         self.n_p = self.meta["n_p"]
         self.tau = self.meta["tau"]
         self.delta = self.meta["delta"]

@@ -78,21 +78,51 @@ def test_c2_louvain_vs_restatement_and_reference_run(fcmod):
 
 
 def test_c2_lpa_vs_restatement_and_reference_run(fcmod):
-    """LPA is called without weights (fast_consensus.py:270): unweighted modularity."""
-    case = golden_io.load("lfr1k_lpm_np20")
-    _, g, planted = lfr1k()
+    """LPA is called without weights (fast_consensus.py:270): unweighted modularity.  On the
+    networkx LFR-1k (mu=0.4) LPA floods to one community in every replica -- the restatement,
+    the reference run and the device alike -- so parity is checked on a native LFR n=1000
+    mu=0.3 graph where every replica finds structure, against the labelings the reference run
+    recorded there (lfr1k_mu03_lpm_np20, make_golden.py r03), with the C2 tolerances."""
+    case = golden_io.load("lfr1k_mu03_lpm_np20")
+    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu03_synth_planted.npy")[case.z["nodes"]]
+    g = orc.EdgeGraph.from_lines(case.N, case.edges_file)
     e = case.edges_file
     gpu = summary(g, device_cd(fcmod, 1, case.N, e, 32, seed=12), planted, weighted=False)
     ref_lab, _ = orc.cd_batch(1, 32, g, seed=6)
     ref = summary(g, ref_lab, planted, weighted=False)
     run = summary(g, case.cd_batches[0], planted, weighted=False)   # reference run's LPA batch (:270)
-    print("C2 lpa gpu", gpu, "restatement", ref, "reference-run", run)
+    print("C2 lpa (mu=0.3) gpu", gpu, "restatement", ref, "reference-run", run)
+    assert min(gpu["k"], ref["k"], run["k"]) > 1.5          # structure found: the comparison is not vacuous
     assert abs(gpu["q"] - ref["q"]) <= 0.02
     assert gpu["nmi"] >= ref["nmi"] - 0.03
-    # on this graph LPA floods: the restatement and the reference run collapse to ONE
-    # community in every replica; the count tolerance is 25 % or one community
-    assert abs(gpu["k"] - ref["k"]) <= max(0.25 * ref["k"], 1.0)
+    assert abs(gpu["k"] - ref["k"]) <= 0.25 * ref["k"]
     assert gpu["q"] >= run["q"] - 0.02 and gpu["nmi"] >= run["nmi"] - 0.03
+
+
+def test_c2_lpa_detectability_edge_vs_reference_run(fcmod):
+    """LFR n=1000 mu=0.55 (LPA's detectability edge): a replica either finds the communities
+    or floods to one.  The reference run's first LPA batch (lfr1k_mu055_lpm_np20) has 8 of 20
+    structured replicas.  Device (64 replicas) vs restatement (64): structured fraction within
+    0.25 of each other (about 3 binomial standard errors) and NMI of the structured replicas
+    >= restatement - 0.03 and >= reference run - 0.05."""
+    case = golden_io.load("lfr1k_mu055_lpm_np20")
+    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu055_synth_planted.npy")[case.z["nodes"]]
+    g = orc.EdgeGraph.from_lines(case.N, case.edges_file)
+    dev = device_cd(fcmod, 1, case.N, case.edges_file, 64, seed=13)
+    ref, _ = orc.cd_batch(1, 64, g, seed=8)
+    runl = case.cd_batches[0]
+
+    def split(L):
+        ok = [x for x in L if len(np.unique(x)) > 1]
+        return len(ok) / len(L), (float(np.mean([nmi(planted, x) for x in ok])) if ok else 0.0)
+    fd, nd = split(dev)
+    fr, nr = split(ref)
+    fu, nu = split(runl)
+    print("C2 lpa (mu=0.55) structured fraction / NMI: gpu %.3f / %.4f | restatement %.3f / %.4f | "
+          "reference run %.3f / %.4f" % (fd, nd, fr, nr, fu, nu))
+    assert fu > 0 and fd > 0
+    assert abs(fd - fr) <= 0.25
+    assert nd >= nr - 0.03 and nd >= nu - 0.05
 
 
 def refsem(name):
@@ -210,6 +240,22 @@ def test_c3_consensus_update_bit_exact_and_run(fcmod, lfr100k, algo, tau):
     print("C3 run", ["louvain", "lpm"][algo], st, "NMI %.4f" % s)
     if algo == 0:
         assert s > 0.8
+
+
+def test_c3_consensus_nmi_vs_reference_semantics(fcmod, lfr100k):
+    """BASELINE configs[2] louvain and lpm, n_p=64: the device's whole-consensus NMI to the
+    planted communities (mean of the n_p final partitions, fast_consensus.py:383-392), averaged
+    over 8 seeds, against the reference loop's distribution at the same size
+    (refsem_lfr100k_*_np64.json: orc.refsem_run, the golden-pinned loop with the sequential CD
+    restatements and the reference's sequential closure; 16 / 8 seeds, make_refsem.py c3).
+    Tolerance: device mean >= reference mean - 0.01 (louvain) / - 0.02 (lpm)."""
+    n, e, planted = lfr100k
+    for algo, name, tau, tol in ((0, "lfr100k_louvain_np64", 0.2, 0.01), (1, "lfr100k_lpm_np64", 0.8, 0.02)):
+        ref = refsem(name)
+        got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 308))
+        print("C3 %s consensus NMI: device mean %.4f sd %.4f min %.4f | reference semantics mean %.4f sd %.4f min %.4f"
+              % (name, got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"], min(ref["nmi"])))
+        assert got.mean() >= ref["nmi_mean"] - tol
 
 
 # ------------------------------------------------------------------------------ C5 (SBM-4M lpm)

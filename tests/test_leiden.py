@@ -6,7 +6,9 @@ orc_leiden: queue-based move, constrained refinement, aggregation by the refined
 partition) and the device is held to it statistically, with the tolerances written in each
 test.  What the reference's loop does around the CD is deterministic and pinned here:
 on integer-labelled graphs the str-keyed lookups (:97, :217) never match, so the loop
-converges at check #1 after one iteration and the result is n_p Leiden runs on G.
+converges at check #1 after one iteration and the result is n_p Leiden runs on G -- recorded
+by running the reference's leiden branch itself (karate/lfr1k_leiden_np20 fixtures,
+tests/golden/make_golden.py r03, leidenalg and the process pool stubbed).
 """
 import os
 import shutil
@@ -103,6 +105,23 @@ def test_cli_leiden_writer(tmp_path):
     assert os.listdir(tmp_path / "memberships_t0.2_d0.02_np2") == []
 
 
+@pytest.mark.parametrize("name", golden_io.LEIDEN_CASES)
+def test_reference_leiden_branch_exit(name):
+    """The reference's own leiden branch, run with leidenalg and the process pool stubbed
+    (make_golden.py r03): on int-labelled graphs the first check (:229) sees an EMPTY graph --
+    every weight stayed 0 (:213-221: int nodes never match the str(vertex id) keys of :97)
+    and :223-227 removed every edge -- and converges; the result is the final pass (:385-388):
+    n_p more Leiden runs on the unchanged input graph.  The engine's leiden loop is exactly
+    this (fc_run(FC_ALGO_LEIDEN): one iteration, exit at check #1, final graph = G)."""
+    case = golden_io.load(name)
+    assert case.algo == 3 and case.meta["n_checks"] == 1 and case.checks[0][1] is True
+    assert len(case.checks[0][0]) == 0                        # the checked graph is empty
+    assert case.meta["n_cd_batches"] == 2                     # the loop's batch + the final pass
+    fin, last = case.z["final_labels"], case.cd_batches[1]
+    for a, b in zip(fin, last):                               # the output IS the final-pass CD
+        assert len(np.unique(np.stack([a, b], 1), axis=0)) == len(np.unique(a)) == len(np.unique(b))
+
+
 # ------------------------------------------------------------------------------ device
 torch = pytest.importorskip("torch")
 
@@ -193,6 +212,27 @@ def test_leiden_run_semantics(fcmod):
     assert st["partition_edges"] == 10 * m
     assert np.array_equal(labels, direct) and np.array_equal(sh, labels)
     assert st2["iterations"] == 1 and st2["exit_check"] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", golden_io.LEIDEN_CASES)
+def test_leiden_run_matches_reference_fixture(fcmod, name):
+    """fc_run(FC_ALGO_LEIDEN) against the reference-run fixture: the same number of loop
+    iterations (CD batches before the final pass), the same exit check, and a final graph equal
+    to the input graph with unit weights (the graph the reference's final pass ran on)."""
+    case = golden_io.load(name)
+    e = case.edges_file
+    with fcmod.Engine(seed=7) as eng:
+        eng.load_graph(case.N, e[:, 0], e[:, 1])
+        m0 = eng.m
+        u0, v0, _, _ = eng.get_graph()
+        labels, st = eng.run(3, case.n_p, case.tau, case.delta)
+        u, v, w, _ = eng.get_graph()
+    assert st["iterations"] == case.meta["n_cd_batches"] - 1
+    assert st["exit_check"] == 1 and case.checks[-1][1]
+    assert m0 == case.meta["m"] and st["m_final"] == case.meta["m"]
+    assert np.array_equal(u, u0) and np.array_equal(v, v0) and (w == 1).all()
+    assert labels.shape == (case.n_p, case.N)
 
 
 @pytest.mark.gpu

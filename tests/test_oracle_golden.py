@@ -126,3 +126,25 @@ def test_lpa_restatement_quality():
             l[list(c)] = i
         ref.append(nmi(planted, l))
     assert np.mean(scores) > np.mean(ref) - 0.1, (scores, ref)
+
+
+def test_refsem_loop_matches_reference_loop_distribution():
+    """orc.refsem_run (the golden-pinned replay steps + sequential CD restatements + the
+    reference's sequential closure, used where the reference script is too slow: C3) against
+    the reference script's own loop driving the same restated CD (refsem_lfr1k_louvain_np20,
+    30 seeds, make_refsem.py): mean consensus NMI over 24 seeds within 0.02 (about 2.5
+    standard errors of the difference)."""
+    import json
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    case = golden_io.load("lfr1k_louvain_np20")
+    planted = np.load(golden_io.GOLDEN + "/lfr1k_mu04_planted.npy")[case.z["nodes"]]
+    g = orc.EdgeGraph.from_lines(case.N, case.edges_file)
+    got = []
+    for s in range(500, 524):
+        lab, _ = orc.refsem_run(0, g, 20, 0.2, 0.02, seed=s, nthreads=4)
+        got.append(np.mean([nmi(planted, x) for x in lab]))
+    with open(golden_io.GOLDEN + "/refsem_lfr1k_louvain_np20.json") as f:
+        ref = json.load(f)
+    print("refsem_run %.4f +- %.4f vs reference loop %.4f +- %.4f" % (np.mean(got), np.std(got), ref["nmi_mean"],
+                                                                      ref["nmi_sd"]))
+    assert abs(np.mean(got) - ref["nmi_mean"]) <= 0.02

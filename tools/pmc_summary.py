@@ -20,7 +20,10 @@ def rows(pattern):
 def main(prof_dir, config, out_dir="profiles", tag="r01"):
     os.makedirs(out_dir, exist_ok=True)
     stats = rows(os.path.join(prof_dir, "trace", "**", "*kernel_stats.csv"))
-    summary = {"config": config, "kernels": []}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from fastconsensus_amd.build import built_hash
+    # the library these counters came from (bench.py attaches traffic only to a same-hash run)
+    summary = {"config": config, "csrc_hash": built_hash(), "kernels": []}
     for r in stats:
         summary["kernels"].append({k: r[k] for k in r})
     counters = defaultdict(lambda: defaultdict(list))
