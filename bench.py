@@ -399,7 +399,31 @@ def main():
                 # ~56 G requests/s x 128 B, whether or not the Infinity Cache holds the line)
                 "traffic_rate_gbs": (traffic / avg_s / 1e9) if (traffic and avg_s > 0) else None,
                 "gather_line_ceiling_gbs": GATHER_LINE_CEILING_GBS}
-        phases = {k: tim[k] / args.steps for k in ("cd_ms", "consensus_ms", "closure_ms", "rebuild_ms", "decide_ms")}
+        if cfg["algo"] in ("leiden", "infomap"):
+            # the CD's own dominant kernel (leiden.hip): k_lv_decide or k_lv_heavy, whichever took
+            # longer in the timed region; both are reported
+            lv = {}
+            for k in ("decide", "heavy"):
+                n_l = tim["lv_%s_launches" % k]
+                if n_l:
+                    a_s = tim["lv_%s_ms" % k] / n_l / 1e3
+                    b_l = tim["lv_%s_bytes" % k] / n_l
+                    ach = b_l / a_s / 1e9 if a_s > 0 else 0.0
+                    lv["k_lv_" + k] = {"launches": n_l, "avg_us": a_s * 1e6, "algorithmic_bytes_per_launch": b_l,
+                                       "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+                                       "ms_per_step": tim["lv_%s_ms" % k] / args.steps}
+            if lv:
+                dom = max(lv, key=lambda k: lv[k]["ms_per_step"])
+                traffic, traffic_note = None, "no PMC profile of %s attached" % dom
+                roof = {"bound": "hbm", "achieved": lv[dom]["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": lv[dom]["frac"], "traffic": traffic, "traffic_note": traffic_note, "kernel": dom,
+                        "note": "the %s CD's dominant kernel by time in the timed region; level 0 of Leiden runs the "
+                                "Louvain engine (k_decide_light: %d launches, %.1f ms per step)"
+                                % (cfg["algo"], tim["decide_launches"], tim["decide_ms"] / args.steps),
+                        "launches": lv[dom]["launches"], "avg_us": lv[dom]["avg_us"],
+                        "algorithmic_bytes_per_launch": lv[dom]["algorithmic_bytes_per_launch"], "kernels": lv}
+        phases = {k: tim[k] / args.steps for k in ("cd_ms", "consensus_ms", "closure_ms", "rebuild_ms", "decide_ms",
+                                                    "lv_decide_ms", "lv_heavy_ms")}
 
     if rank == 0:
         cpu = None

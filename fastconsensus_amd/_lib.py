@@ -45,6 +45,8 @@ class Stats(ctypes.Structure):
         ("cd_ms", ctypes.c_double), ("consensus_ms", ctypes.c_double), ("closure_ms", ctypes.c_double),
         ("rebuild_ms", ctypes.c_double), ("decide_ms", ctypes.c_double), ("decide_launches", ctypes.c_int64),
         ("decide_bytes", ctypes.c_int64),
+        ("lv_decide_ms", ctypes.c_double), ("lv_decide_launches", ctypes.c_int64), ("lv_decide_bytes", ctypes.c_int64),
+        ("lv_heavy_ms", ctypes.c_double), ("lv_heavy_launches", ctypes.c_int64), ("lv_heavy_bytes", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -36,23 +36,25 @@ void timer_end(Ctx& c, int slot, int b) {
 }
 void timer_collect(Ctx& c, fc_stats* st) {
     Timer& t = c.timer;
-    double ms[5] = {0, 0, 0, 0, 0};
-    int64_t launches = 0;
+    double ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    int64_t launches[7] = {0, 0, 0, 0, 0, 0, 0};
     if (!t.pool.empty()) FC_HIP(hipStreamSynchronize(c.stream));
-    for (int s = 0; s < 5; ++s) {
+    for (int s = 0; s < 7; ++s) {
         for (auto& pr : t.spans[s]) {
             float x = 0.f;
             FC_HIP(hipEventElapsedTime(&x, t.pool[pr.first], t.pool[pr.second]));
             ms[s] += x;
         }
-        if (s == 4) launches = (int64_t)t.spans[s].size();
+        launches[s] = (int64_t)t.spans[s].size();
         t.spans[s].clear();
     }
     t.next = 0;
     if (st) {
         *st = c.prof;
         st->cd_ms = ms[0]; st->consensus_ms = ms[1]; st->closure_ms = ms[2]; st->rebuild_ms = ms[3];
-        st->decide_ms = ms[4]; st->decide_launches = launches;
+        st->decide_ms = ms[4]; st->decide_launches = launches[4];
+        st->lv_decide_ms = ms[5]; st->lv_decide_launches = launches[5];
+        st->lv_heavy_ms = ms[6]; st->lv_heavy_launches = launches[6];
     }
     c.prof = fc_stats{};
 }

@@ -82,7 +82,8 @@ struct Graph {
 struct Timer {
     bool on = false;
     std::vector<hipEvent_t> pool;
-    std::vector<std::pair<int, int>> spans[5];  // cd, consensus, closure, rebuild, decide
+    // cd, consensus, closure, rebuild, decide, lv decide, lv heavy
+    std::vector<std::pair<int, int>> spans[7];
     size_t next = 0;
 };
 

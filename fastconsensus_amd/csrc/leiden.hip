@@ -96,7 +96,29 @@ struct LvArgs {
     const int64_t* sv;
     int32_t* mvo;                // [nU] Infomap: the old module of this bucket's movers (with mvt)
     double inv;
+    unsigned long long* lvb;     // [2][MSH] algorithmic bytes of k_lv_decide / k_lv_heavy launches,
+                                 // sharded by block: one hot address serialised every wave's atomic
 };
+
+// Algorithmic bytes (DESIGN.md "Leiden and Infomap"): the per-vertex records a decision
+// reads and writes, per adjacency entry its column, weight and neighbour label(s), per
+// candidate community its Sigma (int64) or Infomap module record (flow, exit: 16 B).
+template <int MODE> __device__ __forceinline__ constexpr int lv_vertex_bytes() {
+    return 16 /* rowptr */ + 4 /* own */ + 8 /* kv */ + (MODE == MODE_REFINE ? 4 : 0) /* P[x] */ +
+           (MODE == MODE_INFO ? 8 + 16 + 8 : 0) /* sv, own module, qrep */;
+}
+template <int MODE> __device__ __forceinline__ constexpr int lv_mover_bytes() {
+    return 4 + 4 + (MODE == MODE_REFINE ? 0 : 8) + (MODE == MODE_INFO ? 4 : 0);   // list, target, mvt, mvo
+}
+template <int MODE> __device__ __forceinline__ int lv_entry_bytes(bool weighted) {
+    return 4 + (weighted ? 4 : 0) + (MODE == MODE_REFINE ? 8 : 4);
+}
+template <int MODE> __device__ __forceinline__ constexpr int lv_cand_bytes() { return MODE == MODE_INFO ? 16 : 8; }
+// wave sum of a per-lane byte count, one atomic per wave into the block's shard
+__device__ __forceinline__ void lv_count(unsigned long long* dst, unsigned long long v) {
+    for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst + (blockIdx.x & (MSH - 1)), v);
+}
 
 __device__ __forceinline__ double plogp2(double p) { return p > 0.0 ? p * log2(p) : 0.0; }
 // The map-equation change split into the part of the source module A (computed once per
@@ -161,7 +183,8 @@ __device__ __forceinline__ bool lv_better(long long s1, uint32_t h1, int32_t c1,
 template <int GL = 64>
 __device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
                                                int32_t own, long long kvx, long long svx, long long wown, int32_t r,
-                                               int64_t x, double& bd, uint32_t& bh, int32_t& bc, int32_t& bw) {
+                                               int64_t x, double& bd, uint32_t& bh, int32_t& bc, int32_t& bw,
+                                               int& ncand) {
     const int gl = threadIdx.x & (GL - 1);
     bd = 0.0; bh = 0; bc = -1; bw = 0;
     const long long Q = a.qrep[r];
@@ -170,6 +193,7 @@ __device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* k
     for (uint32_t s = gl; s < ts; s += GL) {
         const int32_t k = keys[s];
         if (k < 0 || k == own) continue;
+        ++ncand;
         const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);   // one gather: flow and exit
         const double d = info_b(a.inv, A, Q, mk.y, mk.x, kvx, svx, vals[s]);
         const uint32_t h = tie_of(a, r, x, k);
@@ -226,7 +250,7 @@ __device__ __forceinline__ uint32_t tsize(int64_t d) {
 template <int GL = 64>
 __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
                                           int32_t own, long long kvx, int32_t r, int64_t x, long long& bs,
-                                          uint32_t& bh, int32_t& bc, long long& wown) {
+                                          uint32_t& bh, int32_t& bc, long long& wown, int& ncand) {
     const int gl = threadIdx.x & (GL - 1);
     bs = LLONG_MIN; bh = 0; bc = -1; wown = 0;
     for (uint32_t s = gl; s < ts; s += GL) {
@@ -234,6 +258,7 @@ __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, 
         if (k < 0) continue;
         const long long val = vals[s];
         if (k == own) { wown = val; continue; }
+        ++ncand;
         const long long sc = val * a.M2 - kvx * a.tot[k];
         const uint32_t h = tie_of(a, r, x, k);
         if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
@@ -264,6 +289,8 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
+    // this lane's share of the algorithmic bytes: scanned / decided vertices, movers, entries, candidates
+    uint32_t c_scan = 0, c_vtx = 0, c_mov = 0, c_ent = 0, c_cand = 0;
     int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
     if (IMPL && a.bmap) {
         const int64_t loc = (int64_t)(blockIdx.x % a.bpr) * LTB + threadIdx.x;
@@ -271,6 +298,7 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     }
     bool elig = false;
     if (x0 < a.nU) {
+        c_scan = 1;   // the eligibility scan: replica id (explicit levels), queue flag / refined size
         const int32_t r = rep_of<IMPL>(a, x0);
         if (!a.done[r] && in_bucket(a, r, x0, bucket)) {
             if (MODE == MODE_MOVE) {
@@ -320,7 +348,9 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         const int32_t own = valid ? (MODE == MODE_REFINE ? a.R[x] : a.P[x]) : -1;
         const int32_t pc = valid ? a.P[x] : -1;
         long long wl = 0;   // Infomap: weight to the own module
+        c_vtx += (valid && gl == 0) ? 1u : 0u;
         for (int64_t j = rb + gl; j < re; j += GL) {
+            ++c_ent;
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
@@ -334,23 +364,26 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         long long bs, wown;
         uint32_t bh;
         int32_t bc, bw = 0;
+        int ncand = 0;
         if (MODE == MODE_INFO) {
             for (int off = GL / 2; off; off >>= 1) wl += __shfl_xor(wl, off);
             wown = wl;
             double bd = 0.0;
             if (valid) {
-                wave_scan_info<GL>(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rx, x, bd, bh, bc, bw);
+                wave_scan_info<GL>(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rx, x, bd, bh, bc, bw, ncand);
             } else {
                 bc = -1;
             }
             if (!(bd < -INFO_MIN_GAIN)) bc = -1;
             bs = 0;
         } else {
-            wave_scan<GL>(a, keys, vals, ts, own, kvx, rx, x, bs, bh, bc, wown);
+            wave_scan<GL>(a, keys, vals, ts, own, kvx, rx, x, bs, bh, bc, wown, ncand);
         }
+        c_cand += valid ? (uint32_t)ncand : 0u;
         if (valid && gl == 0) {
             const int32_t t = MODE == MODE_INFO ? bc : lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
             if (t >= 0) {
+                ++c_mov;
                 const int p = atomicAdd(&s_cnt, 1);
                 const int64_t q = (int64_t)blockIdx.x * LTB + p;
                 a.blist[q] = (int32_t)x;
@@ -361,6 +394,10 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         }
         wsync();
     }
+    lv_count(a.lvb, (unsigned long long)c_scan * ((IMPL ? 0 : 4) + (MODE == MODE_MOVE ? 1 : MODE == MODE_REFINE ? 8 : 0)) +
+                        (unsigned long long)c_vtx * lv_vertex_bytes<MODE>() + (unsigned long long)c_mov * lv_mover_bytes<MODE>() +
+                        (unsigned long long)c_ent * lv_entry_bytes<MODE>(a.w != nullptr) +
+                        (unsigned long long)c_cand * lv_cand_bytes<MODE>());
     __syncthreads();
     if (threadIdx.x == 0) a.bcnt[blockIdx.x] = s_cnt;
 }
@@ -429,6 +466,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
     __shared__ BRed red;
     __shared__ BRedI redi;
     const int n = *a.heavy_cnt;
+    uint32_t c_vtx = 0, c_ent = 0, c_cand = 0;   // this thread's share of the algorithmic bytes
     int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
     int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
     int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
@@ -448,7 +486,9 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
         const int32_t own = MODE == MODE_REFINE ? a.R[x] : a.P[x];
         const int32_t pc = a.P[x];
         long long wl = 0;
+        c_vtx += threadIdx.x == 0 ? 1u : 0u;
         for (int64_t j = rb + threadIdx.x; j < re; j += LTB) {
+            ++c_ent;
             const int64_t y = base + a.col[j];
             const int32_t wy = a.w ? a.w[j] : 1;
             if (MODE == MODE_REFINE && a.P[y] != pc) continue;
@@ -477,6 +517,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
             if (k < 0) continue;
             const long long val = vals[s];
             if (!lds) { gkey[s] = -1; gval[s] = 0; }   // clear for the next vertex (read before)
+            c_cand += (MODE == MODE_INFO || k != own) ? 1u : 0u;
             if (MODE == MODE_INFO) {
                 const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);
                 const double d = info_b(a.inv, IA, a.qrep[r], mk.y, mk.x, kvx, sv_of<IMPL>(a, x), val);
@@ -506,6 +547,9 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
         }
         __syncthreads();
     }
+    lv_count(a.lvb + MSH, (unsigned long long)c_vtx * (lv_vertex_bytes<MODE>() + 4 /* heavy list */ + 4 /* htgt */) +
+                            (unsigned long long)c_ent * lv_entry_bytes<MODE>(a.w != nullptr) +
+                            (unsigned long long)c_cand * lv_cand_bytes<MODE>());
 }
 
 // Apply one bucket's moves, one wave per mover: blocks [0, nblk) take the decide blocks'
@@ -908,7 +952,7 @@ __global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const 
 enum {
     B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
     B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC, B_MVT,
-    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB, B_LVDONE, B_RMOVES, B_BMAP,
+    B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB, B_LVDONE, B_RMOVES, B_BMAP, B_LVB,
     // aggregation scratch
     B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
     // explicit level graphs, ping-pong: rowptr, col, w, kv, rep, sv (x2)
@@ -1036,6 +1080,8 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     a.mod = mod; a.qrep = qrep;
     a.roff = roff; a.rkey = rkey; a.done = done; a.moves = moves;
     a.heavy_cnt = hcnt;
+    a.lvb = (unsigned long long*)I64(B_LVB, 2 * MSH);
+    FC_HIP(hipMemsetAsync(a.lvb, 0, 16 * MSH, c.stream));
     a.mvt = (unsigned long long*)I64(B_MVT, nU0);
     FC_HIP(hipMemsetAsync(a.mvt, 0, 8 * (size_t)nU0, c.stream));
 
@@ -1099,13 +1145,20 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         for (int b = 0; b < B; ++b) {
             const uint32_t stamp = ++stamp_ctr;   // unique per bucket launch of this run (mvt)
             FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
+            // (timed per launch into spans 5 / 6 when timing is on: lv decide / lv heavy)
 #define LV_LAUNCH(IM, MD)                                                                        \
     do {                                                                                         \
+        const int t5 = timer_begin(c);                                                           \
         if (max_deg <= 64) k_lv_decide<IM, MD, 512, 4><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);  \
         else if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
         else k_lv_decide<IM, MD, LWS, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);               \
-        if (max_deg > LIGHT && max_deg <= HLS / 4) k_lv_heavy<IM, MD, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, stamp); \
-        else if (max_deg > LIGHT) k_lv_heavy<IM, MD, HLS><<<hg, LTB, 0, c.stream>>>(a, stamp);   \
+        timer_end(c, 5, t5);                                                                     \
+        if (max_deg > LIGHT) {                                                                   \
+            const int t6 = timer_begin(c);                                                       \
+            if (max_deg <= HLS / 4) k_lv_heavy<IM, MD, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, stamp); \
+            else k_lv_heavy<IM, MD, HLS><<<hg, LTB, 0, c.stream>>>(a, stamp);                    \
+            timer_end(c, 6, t6);                                                                 \
+        }                                                                                        \
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
             if (impl && MODE == MODE_MOVE) LV_LAUNCH(true, MODE_MOVE);
@@ -1322,7 +1375,13 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         int sw = 0;
         for (; sw < c.max_sweeps; ++sw) {
             ++lv_sweeps;
-            if (sweep(MODE_MOVE, level + 1, sw + 1) == 0) break;
+            const auto t_sw = std::chrono::steady_clock::now();
+            const unsigned long long mvs = sweep(MODE_MOVE, level + 1, sw + 1);
+            if (c.trace)
+                fprintf(stderr, "[fc] leiden level %d sweep %d: %llu moves, %.2f ms\n", level + 1, sw, mvs,
+                        1e-3 * (double)std::chrono::duration_cast<std::chrono::microseconds>(
+                                   std::chrono::steady_clock::now() - t_sw).count());
+            if (mvs == 0) break;
         }
         if (c.trace) {
             sync(c);
@@ -1337,8 +1396,16 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     if (c.trace) fprintf(stderr, "[fc] %s it=%d: %d levels, %lld level sweeps\n", name, iteration, level + 1,
                          (long long)lv_sweeps);
     if (info) FC_HIP(hipMemcpyAsync(cl_out, dcl, 8 * (size_t)n_r, hipMemcpyDeviceToHost, c.stream));
-    c.acc.cd_sweeps += lv_sweeps * n_r;
-    c.prof.cd_sweeps += lv_sweeps * n_r;
+    std::vector<unsigned long long> lvb(2 * MSH);
+    FC_HIP(hipMemcpyAsync(lvb.data(), a.lvb, 16 * MSH, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    unsigned long long lvd = 0, lvh = 0;
+    for (int k = 0; k < MSH; ++k) { lvd += lvb[k]; lvh += lvb[MSH + k]; }
+    for (fc_stats* st : {&c.acc, &c.prof}) {
+        st->cd_sweeps += lv_sweeps * n_r;
+        st->lv_decide_bytes += (int64_t)lvd;
+        st->lv_heavy_bytes += (int64_t)lvh;
+    }
     c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
     c.labT_valid = false;
     timer_end(c, 0, sl0);

@@ -73,6 +73,15 @@ typedef struct fc_stats {
     double decide_ms;         /* light local-moving kernel (the dominant kernel)            */
     int64_t decide_launches;
     int64_t decide_bytes;     /* algorithmic bytes of those launches */
+    /* Leiden / Infomap (leiden.hip): the move/refine decide kernel (k_lv_decide) and the
+     * block-per-vertex kernel for long rows (k_lv_heavy), timed per launch like decide_ms;
+     * bytes per the model in DESIGN.md (counted on the device) */
+    double lv_decide_ms;
+    int64_t lv_decide_launches;
+    int64_t lv_decide_bytes;
+    double lv_heavy_ms;
+    int64_t lv_heavy_launches;
+    int64_t lv_heavy_bytes;
 } fc_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------- */
