@@ -612,7 +612,8 @@ int orc_leiden(i64 N, const i64* rowptr, const i32* col, const i32* w, u64 seed,
  * moves nothing (igraph: until the codelength stops improving); then the modules become the nodes of the next level
  * (aggregation), until a level merges nothing.  The best of `trials` runs (smallest L) is
  * kept.  igraph's alternating sub-module / single-node re-partitioning rounds around this
- * core are NOT restated (documented deviation).  log base 2 as igraph.
+ * core are not part of this function or of the engine; orc_infomap_full (below) restates them
+ * to measure the gap (0 to 0.01 % of the codelength).  log base 2 as igraph.
  * Output labels renumbered 0..k-1 by first node.  Returns the codelength (bits). */
 static inline double plogp2(double p) { return p > 0.0 ? p * log(p) * 1.4426950408889634 : 0.0; }
 
@@ -1201,4 +1202,305 @@ i64 orc_closure_sequential(i64 N, i64 m, const i32* eu, const i32* ev, i64 attem
     for (i64 x = 0; x < N; ++x) free(rows[x].a);
     free(rows); free(tab);
     return k;
+}
+
+/* ------------------------------------------------------------------ Infomap outer loop
+ * igraph's infomap_partition() around the greedy core (restated from the published igraph
+ * 0.9 infomap.cc, itself a port of Rosvall & Bergstrom's code; igraph absent: parity
+ * unpinned).  The engine (leiden.hip MODE_INFO) and orc_infomap run the CORE only; this
+ * fuller restatement exists to MEASURE what the re-partition rounds change
+ * (tests/test_infomap.py::test_core_vs_repartition_rounds_gap):
+ *   iteration 0: the core from singletons (passes + aggregation while the codelength improves);
+ *   odd iterations: single-node movements -- the core again on the original nodes, starting
+ *     from the current modules;
+ *   even iterations >= 2: sub-module movements -- every module of > 1 node is partitioned by
+ *     a recursive infomap_partition on its induced subgraph (a standalone graph: flows from
+ *     the subgraph's degrees), the original nodes are grouped into those sub-modules, and the
+ *     core runs on the sub-modules starting from their modules;
+ *   repeat while an iteration lowers the codelength by > 1e-10.
+ * The two-level map equation, flows and the greedy core are orc_infomap's. */
+typedef struct {
+    i64 n;
+    i64* rp; i32* col; i64* w;      /* symmetric weighted CSR (no self entries) */
+    i64* kv;                        /* node flow weight (weighted degree at the base level) */
+    i64* sv;                        /* node exit weight (== kv at the base level) */
+} im_graph;
+
+static void im_free(im_graph* g) { free(g->rp); free(g->col); free(g->w); free(g->kv); free(g->sv); }
+
+/* codelength (bits) of partition lab over g, with base-node flows kv0 (the original nodes
+ * the codelength's node term counts) */
+static double im_codelength(const im_graph* g, const i32* lab, double inv, double node_term) {
+    const i64 n = g->n;
+    i64* tot = (i64*)calloc((size_t)(n ? n : 1), sizeof(i64));
+    i64* out = (i64*)calloc((size_t)(n ? n : 1), sizeof(i64));
+    for (i64 v = 0; v < n; ++v) {
+        tot[lab[v]] += g->kv[v];
+        out[lab[v]] += g->sv[v];
+        for (i64 j = g->rp[v]; j < g->rp[v + 1]; ++j)
+            if (lab[g->col[j]] == lab[v]) out[lab[v]] -= g->w[j];
+    }
+    long long Q = 0;
+    for (i64 c = 0; c < n; ++c) Q += out[c];
+    double L = plogp2(Q * inv) - node_term;
+    for (i64 c = 0; c < n; ++c)
+        if (tot[c] || out[c]) L += -2.0 * plogp2(out[c] * inv) + plogp2((out[c] + tot[c]) * inv);
+    free(tot); free(out);
+    return L;
+}
+
+/* aggregate g by lab (ids 0..k-1): kv, sv summed / exit weights, inter-module rows */
+static im_graph im_aggregate(const im_graph* g, const i32* lab, i64 k) {
+    im_graph h;
+    h.n = k;
+    h.rp = (i64*)calloc((size_t)k + 1, sizeof(i64));
+    h.kv = (i64*)calloc((size_t)(k ? k : 1), sizeof(i64));
+    h.sv = (i64*)calloc((size_t)(k ? k : 1), sizeof(i64));
+    i64* moff = (i64*)calloc((size_t)k + 1, sizeof(i64));
+    i32* ml = (i32*)malloc(sizeof(i32) * (size_t)(g->n ? g->n : 1));
+    for (i64 v = 0; v < g->n; ++v) moff[lab[v] + 1]++;
+    for (i64 x = 0; x < k; ++x) moff[x + 1] += moff[x];
+    i64* cur = (i64*)malloc(sizeof(i64) * (size_t)(k ? k : 1));
+    for (i64 x = 0; x < k; ++x) cur[x] = moff[x];
+    for (i64 v = 0; v < g->n; ++v) ml[cur[lab[v]]++] = (i32)v;
+    const i64 cap = g->rp[g->n] ? g->rp[g->n] : 1;
+    h.col = (i32*)malloc(sizeof(i32) * (size_t)cap);
+    h.w = (i64*)malloc(sizeof(i64) * (size_t)cap);
+    i64* nw = (i64*)calloc((size_t)(k ? k : 1), sizeof(i64));
+    u8* seen = (u8*)calloc((size_t)(k ? k : 1), 1);
+    i32* cands = (i32*)malloc(sizeof(i32) * (size_t)(k ? k : 1));
+    i64 e = 0;
+    for (i64 x = 0; x < k; ++x) {
+        i64 nc = 0;
+        for (i64 q = moff[x]; q < moff[x + 1]; ++q) {
+            const i32 v = ml[q];
+            h.kv[x] += g->kv[v];
+            h.sv[x] += g->sv[v];
+            for (i64 j = g->rp[v]; j < g->rp[v + 1]; ++j) {
+                const i32 y = lab[g->col[j]];
+                if (y == x) { h.sv[x] -= g->w[j]; continue; }
+                if (!seen[y]) { seen[y] = 1; nw[y] = 0; cands[nc++] = y; }
+                nw[y] += g->w[j];
+            }
+        }
+        for (i64 q = 0; q < nc; ++q) { h.col[e] = cands[q]; h.w[e] = nw[cands[q]]; ++e; seen[cands[q]] = 0; }
+        h.rp[x + 1] = e;
+    }
+    free(moff); free(ml); free(cur); free(nw); free(seen); free(cands);
+    return h;
+}
+
+/* the greedy core (orc_infomap's im_trial) on g from partition init (NULL: singletons):
+ * passes until one moves nothing, aggregation, repeat while a level merges; lab_out = module
+ * of every node of g, renumbered 0..k-1 */
+static void im_core(const im_graph* g0, const i32* init, double inv, u64* s, i32* lab_out) {
+    const i64 N = g0->n;
+    const size_t nn = (size_t)(N ? N : 1);
+    im_graph g;
+    g.n = N;
+    g.rp = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    const i64 E = g0->rp[N];
+    g.col = (i32*)malloc(sizeof(i32) * (size_t)(E ? E : 1));
+    g.w = (i64*)malloc(sizeof(i64) * (size_t)(E ? E : 1));
+    g.kv = (i64*)malloc(sizeof(i64) * nn);
+    g.sv = (i64*)malloc(sizeof(i64) * nn);
+    memcpy(g.rp, g0->rp, sizeof(i64) * (size_t)(N + 1));
+    if (E) { memcpy(g.col, g0->col, sizeof(i32) * (size_t)E); memcpy(g.w, g0->w, sizeof(i64) * (size_t)E); }
+    memcpy(g.kv, g0->kv, sizeof(i64) * nn);
+    memcpy(g.sv, g0->sv, sizeof(i64) * nn);
+    i32* memb = (i32*)malloc(sizeof(i32) * nn);
+    i32* P = (i32*)malloc(sizeof(i32) * nn);
+    i64* tot = (i64*)malloc(sizeof(i64) * nn);
+    i64* out = (i64*)malloc(sizeof(i64) * nn);
+    i64* nw = (i64*)malloc(sizeof(i64) * nn);
+    u8* seen = (u8*)calloc(nn, 1);
+    i32* cands = (i32*)malloc(sizeof(i32) * nn);
+    i32* order = (i32*)malloc(sizeof(i32) * nn);
+    i32* nid = (i32*)malloc(sizeof(i32) * nn);
+    for (i64 v = 0; v < N; ++v) memb[v] = (i32)v;
+    int first = 1;
+    while (1) {
+        for (i64 v = 0; v < g.n; ++v) { P[v] = (first && init) ? init[v] : (i32)v; order[v] = (i32)v; tot[v] = 0; out[v] = 0; }
+        for (i64 v = 0; v < g.n; ++v) {
+            tot[P[v]] += g.kv[v];
+            out[P[v]] += g.sv[v];
+            for (i64 j = g.rp[v]; j < g.rp[v + 1]; ++j)
+                if (P[g.col[j]] == P[v]) out[P[v]] -= g.w[j];
+        }
+        long long Q = 0;
+        for (i64 c = 0; c < g.n; ++c) Q += out[c];
+        for (int pass = 0; pass < 200; ++pass) {
+            shuffle_i32(order, g.n, s);
+            i64 moved = 0;
+            for (i64 t = 0; t < g.n; ++t) {
+                const i32 v = order[t];
+                const i32 A = P[v];
+                i64 nc = 0;
+                for (i64 j = g.rp[v]; j < g.rp[v + 1]; ++j) {
+                    const i32 c = P[g.col[j]];
+                    if (!seen[c]) { seen[c] = 1; nw[c] = 0; cands[nc++] = c; }
+                    nw[c] += g.w[j];
+                }
+                const i64 wA = seen[A] ? nw[A] : 0;
+                i32 best = -1;
+                double bd = -1e-10;
+                shuffle_i32(cands, nc, s);
+                for (i64 k = 0; k < nc; ++k) {
+                    const i32 B = cands[k];
+                    if (B == A) continue;
+                    const double d = im_delta(inv, Q, out[A], tot[A], out[B], tot[B], g.kv[v], g.sv[v], wA, nw[B]);
+                    if (d < bd) { bd = d; best = B; }
+                }
+                if (best >= 0) {
+                    const i64 wB = nw[best];
+                    const long long dA = -g.sv[v] + 2 * wA, dB = g.sv[v] - 2 * wB;
+                    out[A] += dA; out[best] += dB; Q += dA + dB;
+                    tot[A] -= g.kv[v]; tot[best] += g.kv[v];
+                    P[v] = best;
+                    ++moved;
+                }
+                for (i64 k = 0; k < nc; ++k) seen[cands[k]] = 0;
+            }
+            if (!moved) break;
+        }
+        i64 k = 0;
+        for (i64 c = 0; c < g.n; ++c) nid[c] = -1;
+        for (i64 v = 0; v < g.n; ++v) nid[P[v]] = 0;
+        for (i64 c = 0; c < g.n; ++c) if (nid[c] == 0) nid[c] = (i32)k++;
+        for (i64 v = 0; v < g.n; ++v) P[v] = nid[P[v]];
+        for (i64 v = 0; v < N; ++v) memb[v] = P[memb[v]];
+        if (k == g.n && !(first && init)) break;
+        first = 0;
+        if (k == g.n) break;
+        im_graph h = im_aggregate(&g, P, k);
+        im_free(&g);
+        g = h;
+    }
+    for (i64 v = 0; v < N; ++v) lab_out[v] = memb[v];
+    renumber(N, lab_out, nid);
+    im_free(&g);
+    free(memb); free(P); free(tot); free(out); free(nw); free(seen); free(cands); free(order); free(nid);
+}
+
+static double im_node_term(const im_graph* g, double inv) {
+    double t = 0.0;
+    for (i64 v = 0; v < g->n; ++v) t += plogp2(g->kv[v] * inv);
+    return t;
+}
+
+/* infomap_partition(g, rcall): lab = the outer loop's final partition; returns its codelength */
+static double im_partition(const im_graph* g, u64* s, i32* lab, int depth) {
+    const i64 N = g->n;
+    long long M2 = 0;
+    for (i64 v = 0; v < N; ++v) M2 += g->kv[v];
+    for (i64 v = 0; v < N; ++v) lab[v] = (i32)v;
+    if (M2 <= 0 || N <= 1) return 0.0;
+    const double inv = 1.0 / (double)M2, nt = im_node_term(g, inv);
+    double L = im_codelength(g, lab, inv, nt);       /* singletons (calibrate() after initiate()) */
+    i32* nl = (i32*)malloc(sizeof(i32) * (size_t)N);
+    for (int iteration = 0;; ++iteration) {
+        const double outer_old = L;
+        if (iteration == 0) {
+            im_core(g, NULL, inv, s, nl);
+        } else if (iteration % 2 == 1 || depth > 30) {
+            im_core(g, lab, inv, s, nl);              /* single-node movements from the modules */
+        } else {
+            /* sub-module movements: partition every module's induced subgraph recursively */
+            i64 k = 0;
+            for (i64 v = 0; v < N; ++v) if (lab[v] + 1 > k) k = lab[v] + 1;
+            i64* moff = (i64*)calloc((size_t)k + 1, sizeof(i64));
+            i32* ml = (i32*)malloc(sizeof(i32) * (size_t)N);
+            i32* loc = (i32*)malloc(sizeof(i32) * (size_t)N);
+            for (i64 v = 0; v < N; ++v) moff[lab[v] + 1]++;
+            for (i64 x = 0; x < k; ++x) moff[x + 1] += moff[x];
+            i64* cur = (i64*)malloc(sizeof(i64) * (size_t)(k ? k : 1));
+            for (i64 x = 0; x < k; ++x) cur[x] = moff[x];
+            for (i64 v = 0; v < N; ++v) { loc[v] = (i32)(cur[lab[v]] - moff[lab[v]]); ml[cur[lab[v]]++] = (i32)v; }
+            i32* sub = (i32*)malloc(sizeof(i32) * (size_t)N);   /* node -> sub-module (global id) */
+            i32* smod = (i32*)malloc(sizeof(i32) * (size_t)N);  /* sub-module -> its module */
+            i32 next = 0;
+            for (i64 x = 0; x < k; ++x) {
+                const i64 sn = moff[x + 1] - moff[x];
+                if (sn <= 1) {
+                    for (i64 q = moff[x]; q < moff[x + 1]; ++q) { sub[ml[q]] = next; smod[next] = (i32)x; ++next; }
+                    continue;
+                }
+                im_graph sg;                           /* induced subgraph, standalone flows */
+                sg.n = sn;
+                sg.rp = (i64*)calloc((size_t)sn + 1, sizeof(i64));
+                i64 e = 0;
+                for (i64 q = moff[x]; q < moff[x + 1]; ++q)
+                    for (i64 j = g->rp[ml[q]]; j < g->rp[ml[q] + 1]; ++j) e += lab[g->col[j]] == x;
+                sg.col = (i32*)malloc(sizeof(i32) * (size_t)(e ? e : 1));
+                sg.w = (i64*)malloc(sizeof(i64) * (size_t)(e ? e : 1));
+                sg.kv = (i64*)calloc((size_t)sn, sizeof(i64));
+                sg.sv = (i64*)calloc((size_t)sn, sizeof(i64));
+                e = 0;
+                for (i64 q = moff[x]; q < moff[x + 1]; ++q) {
+                    const i32 v = ml[q];
+                    for (i64 j = g->rp[v]; j < g->rp[v + 1]; ++j)
+                        if (lab[g->col[j]] == x) { sg.col[e] = loc[g->col[j]]; sg.w[e] = g->w[j]; sg.kv[q - moff[x]] += g->w[j]; ++e; }
+                    sg.rp[q - moff[x] + 1] = e;
+                    sg.sv[q - moff[x]] = sg.kv[q - moff[x]];
+                }
+                i32* sl = (i32*)malloc(sizeof(i32) * (size_t)sn);
+                im_partition(&sg, s, sl, depth + 1);
+                i32 sk = 0;
+                for (i64 q = 0; q < sn; ++q) if (sl[q] + 1 > sk) sk = sl[q] + 1;
+                for (i64 q = moff[x]; q < moff[x + 1]; ++q) sub[ml[q]] = next + sl[q - moff[x]];
+                for (i32 t = 0; t < sk; ++t) smod[next + t] = (i32)x;
+                next += sk;
+                free(sl);
+                im_free(&sg);
+            }
+            im_graph h = im_aggregate(g, sub, next);     /* the sub-modules become the nodes */
+            i32* hl = (i32*)malloc(sizeof(i32) * (size_t)(next ? next : 1));
+            im_core(&h, smod, inv, s, hl);               /* from the modules they came from */
+            for (i64 v = 0; v < N; ++v) nl[v] = hl[sub[v]];
+            renumber(N, nl, loc);
+            im_free(&h);
+            free(hl); free(moff); free(ml); free(loc); free(cur); free(sub); free(smod);
+        }
+        const double Ln = im_codelength(g, nl, inv, nt);
+        memcpy(lab, nl, sizeof(i32) * (size_t)N);       /* igraph keeps the iteration's result */
+        L = Ln;
+        if (!(outer_old - Ln > 1e-10)) break;
+    }
+    free(nl);
+    return L;
+}
+
+/* The fuller restatement: best of `trials` infomap_partition runs (unweighted topology).
+ * Also returns, through core_L, the best core-only codelength of the same trials' first
+ * iteration (what orc_infomap and the engine compute) for the gap measurement. */
+double orc_infomap_full(i64 N, const i64* rowptr, const i32* col, u64 seed, int trials, i32* lab, double* core_L) {
+    u64 s = seed ^ 0x9FB21C651E98DF25ull;
+    im_graph g;
+    g.n = N;
+    const i64 E = rowptr[N];
+    g.rp = (i64*)malloc(sizeof(i64) * (size_t)(N + 1));
+    g.col = (i32*)malloc(sizeof(i32) * (size_t)(E ? E : 1));
+    g.w = (i64*)malloc(sizeof(i64) * (size_t)(E ? E : 1));
+    g.kv = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
+    g.sv = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
+    memcpy(g.rp, rowptr, sizeof(i64) * (size_t)(N + 1));
+    if (E) memcpy(g.col, col, sizeof(i32) * (size_t)E);
+    for (i64 j = 0; j < E; ++j) g.w[j] = 1;
+    for (i64 v = 0; v < N; ++v) g.kv[v] = g.sv[v] = rowptr[v + 1] - rowptr[v];
+    long long M2 = E;
+    const double inv = M2 > 0 ? 1.0 / (double)M2 : 0.0, nt = im_node_term(&g, inv);
+    i32* tmp = (i32*)malloc(sizeof(i32) * (size_t)(N ? N : 1));
+    double best = 1e300, bcore = 1e300;
+    for (int t = 0; t < (trials > 0 ? trials : 1); ++t) {
+        u64 s2 = s;
+        im_core(&g, NULL, inv, &s2, tmp);
+        const double Lc = im_codelength(&g, tmp, inv, nt);
+        if (Lc < bcore) bcore = Lc;
+        const double L = im_partition(&g, &s, tmp, 0);
+        if (L < best) { best = L; memcpy(lab, tmp, sizeof(i32) * (size_t)N); }
+    }
+    if (core_L) *core_L = bcore;
+    im_free(&g);
+    free(tmp);
+    return best;
 }

@@ -78,6 +78,8 @@ def lib():
                                     ctypes.c_int, ctypes.c_int, _i32p, _i32p]
         L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
+        L.orc_infomap_full.argtypes = [i64, _i64p, _i32p, u64, ctypes.c_int, _i32p, ctypes.POINTER(dbl)]
+        L.orc_infomap_full.restype = dbl
         L.orc_closure_sequential.argtypes = [i64, i64, _i32p, _i32p, i64, u64, _i32p]
         L.orc_closure_sequential.restype = i64
         _lib = L
@@ -266,6 +268,17 @@ def infomap(g, seed, trials=10):
     lab = np.empty(g.N, np.int32)
     L = lib().orc_infomap(g.N, rowptr, col, int(seed) & (2**64 - 1), int(trials), lab)
     return lab, L
+
+
+def infomap_full(g, seed, trials=10):
+    """igraph's infomap_partition outer loop (single-node and sub-module re-partition rounds)
+    around the same greedy core (orc_infomap_full).  Returns (labels, codelength, the core-only
+    codelength of the same trials)."""
+    rowptr, col, _ = g.csr()
+    lab = np.empty(g.N, np.int32)
+    core = ctypes.c_double()
+    L = lib().orc_infomap_full(g.N, rowptr, col, int(seed) & (2**64 - 1), int(trials), lab, ctypes.byref(core))
+    return lab, L, core.value
 
 
 def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8,

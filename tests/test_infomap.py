@@ -79,6 +79,33 @@ def test_oracle_infomap_karate():
     assert L <= 4.312 and len(np.unique(lab)) == 3
 
 
+@pytest.mark.parametrize("graph", ["karate", "lfr1k_mu04", "lfr1k_mu06", "lesmis"])
+def test_core_vs_repartition_rounds_gap(graph):
+    """igraph's infomap_partition wraps the greedy core in alternating single-node and
+    sub-module re-partition rounds (restated in orc_infomap_full; the engine and orc_infomap run
+    the core only).  Measured gap, core-only minus full codelength over the same 10 trials:
+    0 on karate, LFR-1k mu=0.4/0.6, les Miserables, LFR-10k mu=0.5/0.6 and LFR-100k mu=0.5;
+    0.0102 % on LFR-10k mu=0.7.  Held here to <= 0.05 %, full <= core."""
+    import networkx as nx
+    from fastconsensus_amd import synth
+    if graph == "karate":
+        n, e = karate()
+    elif graph == "lesmis":
+        G = nx.convert_node_labels_to_integers(nx.les_miserables_graph())
+        n, e = G.number_of_nodes(), np.array(G.edges(), np.int32)
+    else:
+        u, v, _ = synth.lfr(1000, 0.4 if graph.endswith("04") else 0.6, seed=42)
+        n, e = 1000, np.stack([u, v], 1)
+    g = orc.EdgeGraph.from_lines(n, e)
+    lab, L, Lc = orc.infomap_full(g, seed=1)
+    print("%s: full %.6f bits, core %.6f bits, gap %.4f %%, %d modules" % (graph, L, Lc, 100 * (Lc - L) / Lc,
+                                                                        len(np.unique(lab))))
+    assert L <= Lc + 1e-9
+    assert (Lc - L) / Lc <= 5e-4
+    if graph == "karate":
+        assert abs(L - 4.3118) < 1e-4 and len(np.unique(lab)) == 3
+
+
 # ------------------------------------------------------------------------------ device
 torch = pytest.importorskip("torch")
 
