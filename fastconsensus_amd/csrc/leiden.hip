@@ -45,6 +45,13 @@ constexpr int LIGHT = LWS / 2;    // rows / member-row sums above this go to the
 constexpr int LWS_SMALL = 256;    // the short-row variant of k_lv_decide
 constexpr int HLS = 8192;         // LDS slots of a block-per-vertex table
 constexpr int HLIGHT = HLS / 2;   // longer rows use a global table
+// Long rows are listed by length tier, each tier decided by a block-per-vertex kernel whose LDS
+// table just fits it: <= 1024 entries in 2048 slots (16 KB: 8 blocks per CU), <= 2048 in 4096
+// (32 KB: 5), <= 4096 in 8192 (64 KB: 2), longer rows in global tables.  One table size for a
+// whole level (the longest row's) left a level of ~1000-entry rows with one 9576-entry row at 2
+// blocks per CU.
+constexpr int NTIER = 4;
+__host__ __device__ constexpr int heavy_tier(int64_t d) { return d <= 1024 ? 0 : d <= 2048 ? 1 : d <= 4096 ? 2 : 3; }
 constexpr int MODE_MOVE = 0, MODE_REFINE = 1, MODE_INFO = 2;   // Leiden move / refine; Infomap move
 constexpr int MSH = 256;          // move-counter shards
 constexpr int MAX_LEVELS = 64;
@@ -73,9 +80,10 @@ struct LvArgs {
     int32_t* blist;           // [nblk][LTB] movers of each decide block (vertex)
     int32_t* btgt;            // [nblk][LTB] their targets
     int32_t* bcnt;            // [nblk]
-    int32_t* heavy;           // heavy vertices of this bucket
-    int32_t* heavy_cnt;
-    int32_t* htgt;            // their decisions (-1: stay)
+    int32_t* heavy;           // [NTIER][hcap] heavy vertices of this bucket, by length tier
+    int32_t* heavy_cnt;       // [NTIER]
+    int32_t* htgt;            // [NTIER][hcap] their decisions (-1: stay)
+    int64_t hcap;
     int32_t* hkey;            // [LHB][hslots] global tables (kept cleared)
     int32_t* hval;
     int32_t* hlst;            // [LHB][hslots] created slots
@@ -311,18 +319,25 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             }
         }
     }
-    // long rows go to k_lv_heavy: one list append per wave (ballot + one atomic)
+    // long rows go to k_lv_heavy, listed by length tier: one append per wave and tier (ballot +
+    // one atomic)
     bool hv = false;
+    int tier = -1;
     if (elig) {
         const int64_t xr0 = IMPL ? x0 % a.N0 : x0;
-        hv = a.rowptr[xr0 + 1] - a.rowptr[xr0] > TS / G / 2;
+        const int64_t d0 = a.rowptr[xr0 + 1] - a.rowptr[xr0];
+        hv = d0 > TS / G / 2;
+        if (hv) tier = heavy_tier(d0);
     }
-    const unsigned long long hmask = __ballot(hv);
-    if (hmask) {
-        int hb = 0;
-        if (lane == 0) hb = atomicAdd(a.heavy_cnt, __popcll(hmask));
-        hb = __shfl(hb, 0);
-        if (hv) a.heavy[hb + __popcll(hmask & ((1ull << lane) - 1))] = (int32_t)x0;
+    if (__ballot(hv)) {
+        for (int t = 0; t < NTIER; ++t) {
+            const unsigned long long hmask = __ballot(tier == t);
+            if (!hmask) continue;
+            int hb = 0;
+            if (lane == 0) hb = atomicAdd(a.heavy_cnt + t, __popcll(hmask));
+            hb = __shfl(hb, 0);
+            if (tier == t) a.heavy[t * a.hcap + hb + __popcll(hmask & ((1ull << lane) - 1))] = (int32_t)x0;
+        }
     }
     unsigned long long mask = __ballot(elig && !hv);
     const int grp = lane / GL, gl = lane & (GL - 1);
@@ -457,7 +472,7 @@ __device__ __forceinline__ void block_best_info(BRedI& red, double& bd, uint32_t
 // Long rows: one block per vertex; an LDS table of up to HLS slots, or (rows > HLIGHT) a
 // global table per block, cleared through the list of slots it created.
 template <bool IMPL, int MODE, int HS>
-__global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
+__global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int tier) {
     // HS: LDS slots (HLS, or HLS/2 when no row of the level is longer than HLS/4: 32 KB instead
     // of 64 KB per block, so 4-5 blocks per CU instead of 2)
     __shared__ int32_t lkey[HS], lval[HS];
@@ -465,13 +480,15 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
     __shared__ long long s_wown;
     __shared__ BRed red;
     __shared__ BRedI redi;
-    const int n = *a.heavy_cnt;
+    const int n = a.heavy_cnt[tier];
+    const int32_t* hlist = a.heavy + tier * a.hcap;
+    int32_t* htgt = a.htgt + tier * a.hcap;
     uint32_t c_vtx = 0, c_ent = 0, c_cand = 0;   // this thread's share of the algorithmic bytes
     int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
     int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
     int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int64_t x = a.heavy[i];
+        const int64_t x = hlist[i];
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
         const int64_t rb = a.rowptr[xr], re = a.rowptr[xr + 1];
@@ -534,14 +551,14 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp) {
             block_best_info(redi, bd, bh, bc, bw);
             if (threadIdx.x == 0) {
                 const int32_t t = (bc >= 0 && bd < -INFO_MIN_GAIN) ? bc : -1;
-                a.htgt[i] = t;
+                htgt[i] = t;
                 if (t >= 0) { a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t; a.mvo[x] = own; }
             }
         } else {
             block_best(red, bs, bh, bc, wown);
             if (threadIdx.x == 0) {
                 const int32_t t = lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
-                a.htgt[i] = t;
+                htgt[i] = t;
                 if (MODE == MODE_MOVE && t >= 0) a.mvt[x] = ((unsigned long long)stamp << 32) | (uint32_t)t;
             }
         }
@@ -656,12 +673,16 @@ __global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk, 
             count_rep(a.blist[q]);
         }
     } else {
-        const int n = *a.heavy_cnt;
-        for (int i = (blockIdx.x - nblk) * (LTB / 64) + wv; i < n; i += hblk * (LTB / 64)) {
-            const int32_t t = a.htgt[i];
-            if (t >= 0) {
-                lv_move<IMPL, MODE>(a, a.heavy[i], t, stamp, mv);
-                count_rep(a.heavy[i]);
+        for (int tier = 0; tier < NTIER; ++tier) {
+            const int n = a.heavy_cnt[tier];
+            const int32_t* hl = a.heavy + tier * a.hcap;
+            const int32_t* ht = a.htgt + tier * a.hcap;
+            for (int i = (blockIdx.x - nblk) * (LTB / 64) + wv; i < n; i += hblk * (LTB / 64)) {
+                const int32_t t = ht[i];
+                if (t >= 0) {
+                    lv_move<IMPL, MODE>(a, hl[i], t, stamp, mv);
+                    count_rep(hl[i]);
+                }
             }
         }
     }
@@ -759,13 +780,14 @@ __global__ void k_ag_memb(int64_t total, int64_t N, const uint8_t* done, const i
 template <bool IMPL>
 __global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const int32_t* nid, const int32_t* moff,
                                                  const int32_t* mlist, const int64_t* ubo, int32_t* ocol, int32_t* ow,
-                                                 int32_t* olen, int32_t* hlist, int32_t* hcnt) {
+                                                 int32_t* olen, int32_t* hlist, int32_t* hcnt, int64_t hcap) {
     __shared__ int32_t skey[LTB / 64][LWS], sval[LTB / 64][LWS];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t xn = (int64_t)blockIdx.x * (LTB / 64) + wv;
     if (xn >= nUn) return;
-    if (ubo[xn + 1] - ubo[xn] > LIGHT) {
-        if (lane == 0) hlist[atomicAdd(hcnt, 1)] = (int32_t)xn;
+    if (ubo[xn + 1] - ubo[xn] > LIGHT) {   // listed by length tier for k_ag_rows_heavy
+        const int t = heavy_tier(ubo[xn + 1] - ubo[xn]);
+        if (lane == 0) hlist[t * hcap + atomicAdd(hcnt + t, 1)] = (int32_t)xn;
         return;
     }
     int32_t* keys = skey[wv];
@@ -800,11 +822,12 @@ __global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const in
 template <bool IMPL, int HS>
 __global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* nid, const int32_t* moff,
                                                        const int32_t* mlist, const int64_t* ubo, int32_t* ocol,
-                                                       int32_t* ow, int32_t* olen, const int32_t* hlist,
-                                                       const int32_t* hcnt) {
-    __shared__ int32_t lkey[HS], lval[HS];   // HLS, or HLS/2 when every member-row sum fits
+                                                       int32_t* ow, int32_t* olen, const int32_t* hlist_all,
+                                                       const int32_t* hcnt, int64_t hcap, int tier) {
+    __shared__ int32_t lkey[HS], lval[HS];   // sized for the tier's rows (tier 3: global tables)
     __shared__ int s_n;
-    const int n = *hcnt;
+    const int n = hcnt[tier];
+    const int32_t* hlist = hlist_all + tier * hcap;
     int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
     int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
     int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
@@ -1113,8 +1136,9 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         a.blist = I32(B_BLIST, nblk * LTB);
         a.btgt = I32(B_BTGT, nblk * LTB);
         a.bcnt = I32(B_BCNT, nblk);
-        a.heavy = I32(B_HEAVY, nU);
-        a.htgt = I32(B_HTGT, nU);
+        a.hcap = nU;
+        a.heavy = I32(B_HEAVY, NTIER * nU);
+        a.htgt = I32(B_HTGT, NTIER * nU);
         int64_t hs = 64;   // global tables only for rows beyond the block's LDS table
         if (max_deg > HLIGHT)
             while (hs < 2 * (int64_t)max_deg) hs <<= 1;
@@ -1144,7 +1168,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         const int hblk = 64;
         for (int b = 0; b < B; ++b) {
             const uint32_t stamp = ++stamp_ctr;   // unique per bucket launch of this run (mvt)
-            FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
+            FC_HIP(hipMemsetAsync(hcnt, 0, 4 * NTIER, c.stream));
             // (timed per launch into spans 5 / 6 when timing is on: lv decide / lv heavy)
 #define LV_LAUNCH(IM, MD)                                                                        \
     do {                                                                                         \
@@ -1153,10 +1177,12 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         else if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
         else k_lv_decide<IM, MD, LWS, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);               \
         timer_end(c, 5, t5);                                                                     \
-        if (max_deg > LIGHT) {                                                                   \
+        if (max_deg > LIGHT) {   /* tiers by row length (heavy_tier); tier 3: global tables */  \
             const int t6 = timer_begin(c);                                                       \
-            if (max_deg <= HLS / 4) k_lv_heavy<IM, MD, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, stamp); \
-            else k_lv_heavy<IM, MD, HLS><<<hg, LTB, 0, c.stream>>>(a, stamp);                    \
+            k_lv_heavy<IM, MD, 2048><<<2048, LTB, 0, c.stream>>>(a, stamp, 0);                   \
+            if (max_deg > 1024) k_lv_heavy<IM, MD, 4096><<<1280, LTB, 0, c.stream>>>(a, stamp, 1); \
+            if (max_deg > 2048) k_lv_heavy<IM, MD, HLS><<<512, LTB, 0, c.stream>>>(a, stamp, 2); \
+            if (max_deg > 4096) k_lv_heavy<IM, MD, 2048><<<hg, LTB, 0, c.stream>>>(a, stamp, 3); \
             timer_end(c, 6, t6);                                                                 \
         }                                                                                        \
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
@@ -1307,22 +1333,29 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         int32_t* tcol = I32(B_TCOL, ubtot + 1);
         int32_t* tw = I32(B_TW, ubtot + 1);
         int32_t* olen = I32(B_OLEN, nUn + 1);
-        int32_t* agh = I32(B_AGH, nUn + 1);
-        FC_HIP(hipMemsetAsync(hcnt, 0, 4, c.stream));
+        int32_t* agh = I32(B_AGH, NTIER * (nUn + 1));
+        FC_HIP(hipMemsetAsync(hcnt, 0, 4 * NTIER, c.stream));
         const unsigned agb = nb(nUn, LTB / 64);
-        if (impl) k_ag_rows<true><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
-        else k_ag_rows<false><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+        const int64_t ahc = nUn + 1;
+        if (impl) k_ag_rows<true><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc);
+        else k_ag_rows<false><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc);
         if (ubmax > LIGHT) {
             int64_t hs = 64;
             if (ubmax > HLIGHT)
                 while (hs < 2 * ubmax) hs <<= 1;
             a.hslots = hs;
             const int hg = heavy_grid(hs);
-            const bool small = ubmax <= HLS / 4;
-            if (impl && small) k_ag_rows_heavy<true, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
-            else if (impl) k_ag_rows_heavy<true, HLS><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
-            else if (small) k_ag_rows_heavy<false, HLS / 2><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
-            else k_ag_rows_heavy<false, HLS><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt);
+            // by length tier (heavy_tier): LDS tables sized for the tier, global tables past 4096
+#define AG_HEAVY(IM)                                                                                              \
+    do {                                                                                                          \
+        k_ag_rows_heavy<IM, 2048><<<2048, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc, 0); \
+        if (ubmax > 1024) k_ag_rows_heavy<IM, 4096><<<1280, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc, 1); \
+        if (ubmax > 2048) k_ag_rows_heavy<IM, HLS><<<512, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc, 2); \
+        if (ubmax > 4096) k_ag_rows_heavy<IM, 2048><<<hg, LTB, 0, c.stream>>>(a, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc, 3); \
+    } while (0)
+            if (impl) AG_HEAVY(true);
+            else AG_HEAVY(false);
+#undef AG_HEAVY
         }
         int64_t* len64 = I64(B_LEN64, nUn + 1);
         k_ag_len64<<<nb(nUn + 1), LTB, 0, c.stream>>>(nUn, olen, len64);
@@ -1377,10 +1410,20 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             ++lv_sweeps;
             const auto t_sw = std::chrono::steady_clock::now();
             const unsigned long long mvs = sweep(MODE_MOVE, level + 1, sw + 1);
-            if (c.trace)
-                fprintf(stderr, "[fc] leiden level %d sweep %d: %llu moves, %.2f ms\n", level + 1, sw, mvs,
+            if (c.trace) {
+                // algorithmic bytes of the decide / heavy launches so far (the work the sweep did)
+                std::vector<unsigned long long> hb(2 * MSH);
+                FC_HIP(hipMemcpy(hb.data(), a.lvb, 16 * MSH, hipMemcpyDeviceToHost));
+                unsigned long long bd = 0, bh = 0;
+                for (int k = 0; k < MSH; ++k) { bd += hb[k]; bh += hb[MSH + k]; }
+                static unsigned long long pd = 0, ph = 0;
+                if (bd < pd || bh < ph) pd = ph = 0;
+                fprintf(stderr, "[fc] leiden level %d sweep %d: %llu moves, %.2f ms, decide %.1f MB, heavy %.1f MB\n",
+                        level + 1, sw, mvs,
                         1e-3 * (double)std::chrono::duration_cast<std::chrono::microseconds>(
-                                   std::chrono::steady_clock::now() - t_sw).count());
+                                   std::chrono::steady_clock::now() - t_sw).count(), (bd - pd) / 1e6, (bh - ph) / 1e6);
+                pd = bd; ph = bh;
+            }
             if (mvs == 0) break;
         }
         if (c.trace) {
