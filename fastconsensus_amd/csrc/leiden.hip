@@ -55,6 +55,8 @@ __host__ __device__ constexpr int heavy_tier(int64_t d) { return d <= 1024 ? 0 :
 constexpr int MODE_MOVE = 0, MODE_REFINE = 1, MODE_INFO = 2;   // Leiden move / refine; Infomap move
 constexpr int MSH = 256;          // move-counter shards
 constexpr int MAX_LEVELS = 64;
+constexpr int UNR = 4;            // k_lv_heavy: entries / table slots per thread with their gathers in flight
+                                  // (1 in k_lv_decide: its VGPRs cost more occupancy than the overlap gains)
 
 inline unsigned nb(int64_t n, int tb = LTB) { return (unsigned)std::max<int64_t>(1, (n + tb - 1) / tb); }
 
@@ -198,14 +200,28 @@ __device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* k
     const long long Q = a.qrep[r];
     const longlong2 mo = *(const longlong2*)(a.mod + 2 * (int64_t)own);
     const InfoA A = info_a(a.inv, Q, mo.y, mo.x, kvx, svx, wown);
-    for (uint32_t s = gl; s < ts; s += GL) {
-        const int32_t k = keys[s];
-        if (k < 0 || k == own) continue;
-        ++ncand;
-        const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);   // one gather: flow and exit
-        const double d = info_b(a.inv, A, Q, mk.y, mk.x, kvx, svx, vals[s]);
-        const uint32_t h = tie_of(a, r, x, k);
-        if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = vals[s]; }
+    constexpr int UNR = 1;
+    for (uint32_t s0 = gl; s0 < ts; s0 += GL * UNR) {
+        int32_t k[UNR], v[UNR];
+        longlong2 mk[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t s = s0 + u * GL;
+            k[u] = s < ts ? keys[s] : -1;
+            v[u] = s < ts ? vals[s] : 0;
+            if (k[u] == own) k[u] = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u)
+            mk[u] = k[u] >= 0 ? *(const longlong2*)(a.mod + 2 * (int64_t)k[u]) : make_longlong2(0, 0);   // flow, exit
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (k[u] < 0) continue;
+            ++ncand;
+            const double d = info_b(a.inv, A, Q, mk[u].y, mk[u].x, kvx, svx, v[u]);
+            const uint32_t h = tie_of(a, r, x, k[u]);
+            if (info_better(d, h, k[u], bd, bh, bc)) { bd = d; bh = h; bc = k[u]; bw = v[u]; }
+        }
     }
     for (int off = GL / 2; off; off >>= 1) {
         const double d2 = __shfl_xor(bd, off);
@@ -228,6 +244,45 @@ __device__ __forceinline__ int tins(int32_t* keys, int32_t* vals, uint32_t nslot
         if (prev == -1) { atomicAdd(&vals[h], w); return (int)h; }
         if (prev == k) { atomicAdd(&vals[h], w); return -1; }
         h = (h + 1 == nslots) ? 0 : h + 1;
+    }
+}
+
+// One row's entries j = j0, j0 + ST, ... < re into the table, UNR entries per thread in flight
+// (columns and weights, then the label gathers, then the inserts: a thread's gathers overlap
+// instead of forming a chain of UNR round trips).  Entries in the own community are summed
+// into wl; refine only counts neighbours inside the move-phase community pc.  Global tables
+// (lst != nullptr) list the slots they create.
+template <int MODE, int UNR>
+__device__ __forceinline__ void row_insert(const LvArgs& a, int64_t base, int64_t j0, int64_t re, int ST, int32_t own,
+                                           int32_t pc, int32_t* keys, int32_t* vals, uint32_t ts, long long& wl,
+                                           uint32_t& c_ent, int32_t* lst, int* s_n) {
+    for (int64_t j = j0; j < re; j += (int64_t)ST * UNR) {
+        int64_t y[UNR];
+        int32_t wy[UNR], cy[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const int64_t jj = j + (int64_t)u * ST;
+            const bool ok = jj < re;
+            y[u] = ok ? base + a.col[jj] : -1;
+            wy[u] = ok ? (a.w ? a.w[jj] : 1) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) cy[u] = y[u] >= 0 ? a.P[y[u]] : -1;
+        if (MODE == MODE_REFINE) {
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) cy[u] = (y[u] >= 0 && cy[u] == pc) ? a.R[y[u]] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (y[u] < 0) continue;
+            ++c_ent;
+            if (cy[u] < 0) continue;
+            // entries in the own community are summed in registers, not inserted: on aggregated
+            // levels they are a large share of a row, all on one LDS address
+            if (cy[u] == own) { wl += wy[u]; continue; }
+            const int sl = tins(keys, vals, ts, true, cy[u], wy[u]);
+            if (lst && sl >= 0) lst[atomicAdd(s_n, 1)] = sl;
+        }
     }
 }
 
@@ -260,16 +315,27 @@ __device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, 
                                           int32_t own, long long kvx, int32_t r, int64_t x, long long& bs,
                                           uint32_t& bh, int32_t& bc, long long& wown, int& ncand) {
     const int gl = threadIdx.x & (GL - 1);
-    bs = LLONG_MIN; bh = 0; bc = -1; wown = 0;
-    for (uint32_t s = gl; s < ts; s += GL) {
-        const int32_t k = keys[s];
-        if (k < 0) continue;
-        const long long val = vals[s];
-        if (k == own) { wown = val; continue; }
-        ++ncand;
-        const long long sc = val * a.M2 - kvx * a.tot[k];
-        const uint32_t h = tie_of(a, r, x, k);
-        if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
+    bs = LLONG_MIN; bh = 0; bc = -1;   // wown: this lane's own-community weight (not in the table)
+    constexpr int UNR = 1;
+    for (uint32_t s0 = gl; s0 < ts; s0 += GL * UNR) {
+        int32_t k[UNR];
+        long long val[UNR], tk[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t s = s0 + u * GL;
+            k[u] = s < ts ? keys[s] : -1;
+            val[u] = s < ts ? vals[s] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) tk[u] = k[u] >= 0 ? a.tot[k[u]] : 0;
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            if (k[u] < 0) continue;
+            ++ncand;
+            const long long sc = val[u] * a.M2 - kvx * tk[u];
+            const uint32_t h = tie_of(a, r, x, k[u]);
+            if (lv_better(sc, h, k[u], bs, bh, bc)) { bs = sc; bh = h; bc = k[u]; }
+        }
     }
     for (int off = GL / 2; off; off >>= 1) {
         const long long s2 = __shfl_xor(bs, off);
@@ -364,15 +430,7 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         const int32_t pc = valid ? a.P[x] : -1;
         long long wl = 0;   // Infomap: weight to the own module
         c_vtx += (valid && gl == 0) ? 1u : 0u;
-        for (int64_t j = rb + gl; j < re; j += GL) {
-            ++c_ent;
-            const int64_t y = base + a.col[j];
-            const int32_t wy = a.w ? a.w[j] : 1;
-            if (MODE == MODE_REFINE && a.P[y] != pc) continue;
-            const int32_t cy = MODE == MODE_REFINE ? a.R[y] : a.P[y];
-            if (MODE == MODE_INFO && cy == own) { wl += wy; continue; }
-            tins(keys, vals, ts, true, cy, wy);
-        }
+        row_insert<MODE, 1>(a, base, rb + gl, re, GL, own, pc, keys, vals, ts, wl, c_ent, nullptr, nullptr);
         wsync();
         const long long kvx = valid ? kv_of<IMPL>(a, x) : 0;
         const int32_t rx = valid ? rep_of<IMPL>(a, x) : 0;
@@ -392,6 +450,7 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             if (!(bd < -INFO_MIN_GAIN)) bc = -1;
             bs = 0;
         } else {
+            wown = wl;
             wave_scan<GL>(a, keys, vals, ts, own, kvx, rx, x, bs, bh, bc, wown, ncand);
         }
         c_cand += valid ? (uint32_t)ncand : 0u;
@@ -504,21 +563,13 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
         const int32_t pc = a.P[x];
         long long wl = 0;
         c_vtx += threadIdx.x == 0 ? 1u : 0u;
-        for (int64_t j = rb + threadIdx.x; j < re; j += LTB) {
-            ++c_ent;
-            const int64_t y = base + a.col[j];
-            const int32_t wy = a.w ? a.w[j] : 1;
-            if (MODE == MODE_REFINE && a.P[y] != pc) continue;
-            const int32_t cy = MODE == MODE_REFINE ? a.R[y] : a.P[y];
-            if (MODE == MODE_INFO && cy == own) { wl += wy; continue; }
-            const int s = tins(keys, vals, ts, true, cy, wy);
-            if (!lds && s >= 0) lst[atomicAdd(&s_n, 1)] = s;
-        }
+        row_insert<MODE, UNR>(a, base, rb + threadIdx.x, re, LTB, own, pc, keys, vals, ts, wl, c_ent, lds ? nullptr : lst,
+                         &s_n);
         if (MODE == MODE_INFO && wl) atomicAdd((unsigned long long*)&s_wown, (unsigned long long)wl);
         __syncthreads();
         const long long kvx = kv_of<IMPL>(a, x);
         const int32_t r = rep_of<IMPL>(a, x);
-        long long bs = LLONG_MIN, wown = MODE == MODE_INFO ? s_wown : 0;
+        long long bs = LLONG_MIN, wown = MODE == MODE_INFO ? s_wown : wl;   // move/refine: summed by block_best
         double bd = 0.0;
         uint32_t bh = 0;
         int32_t bc = -1, bw = 0;
@@ -528,24 +579,46 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
             const longlong2 mo = *(const longlong2*)(a.mod + 2 * (int64_t)own);
             IA = info_a(a.inv, a.qrep[r], mo.y, mo.x, kvx, sv_of<IMPL>(a, x), wown);
         }
-        for (int q = threadIdx.x; q < cnt; q += LTB) {
-            const int s = lds ? q : lst[q];
-            const int32_t k = keys[s];
-            if (k < 0) continue;
-            const long long val = vals[s];
-            if (!lds) { gkey[s] = -1; gval[s] = 0; }   // clear for the next vertex (read before)
-            c_cand += (MODE == MODE_INFO || k != own) ? 1u : 0u;
-            if (MODE == MODE_INFO) {
-                const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);
-                const double d = info_b(a.inv, IA, a.qrep[r], mk.y, mk.x, kvx, sv_of<IMPL>(a, x), val);
-                const uint32_t h = tie_of(a, r, x, k);
-                if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = (int32_t)val; }
-                continue;
+        const long long qr = MODE == MODE_INFO ? a.qrep[r] : 0;
+        const long long svx = MODE == MODE_INFO ? sv_of<IMPL>(a, x) : 0;
+        for (int q0 = threadIdx.x; q0 < cnt; q0 += LTB * UNR) {   // UNR slots' gathers in flight
+            int32_t k[UNR];
+            long long val[UNR], tk[UNR], tk2[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int q = q0 + u * LTB;
+                k[u] = -1; val[u] = 0;
+                if (q < cnt) {
+                    const int sl = lds ? q : lst[q];
+                    k[u] = keys[sl];
+                    val[u] = vals[sl];
+                    if (!lds) { gkey[sl] = -1; gval[sl] = 0; }   // clear for the next vertex (read before)
+                }
             }
-            if (k == own) { wown = val; continue; }
-            const long long sc = val * a.M2 - kvx * a.tot[k];
-            const uint32_t h = tie_of(a, r, x, k);
-            if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                tk[u] = tk2[u] = 0;
+                if (k[u] < 0) continue;
+                if (MODE == MODE_INFO) {
+                    const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k[u]);
+                    tk[u] = mk.x; tk2[u] = mk.y;
+                } else {
+                    tk[u] = a.tot[k[u]];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                if (k[u] < 0) continue;
+                ++c_cand;
+                const uint32_t h = tie_of(a, r, x, k[u]);
+                if (MODE == MODE_INFO) {
+                    const double d = info_b(a.inv, IA, qr, tk2[u], tk[u], kvx, svx, val[u]);
+                    if (info_better(d, h, k[u], bd, bh, bc)) { bd = d; bh = h; bc = k[u]; bw = (int32_t)val[u]; }
+                } else {
+                    const long long sc = val[u] * a.M2 - kvx * tk[u];
+                    if (lv_better(sc, h, k[u], bs, bh, bc)) { bs = sc; bh = h; bc = k[u]; }
+                }
+            }
         }
         if (MODE == MODE_INFO) {
             block_best_info(redi, bd, bh, bc, bw);
