@@ -193,6 +193,23 @@ def load_traffic(config):
     return d.get("decide_hbm_bytes_per_launch"), "traffic from %s (csrc %s)" % (os.path.basename(p), prof)
 
 
+def load_lv_traffic(config, kernel):
+    """Leiden / Infomap: HBM bytes per launch of `kernel` from a same-hash PMC profile."""
+    from fastconsensus_amd.build import built_hash
+    p = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
+    if not os.path.exists(p):
+        return None, "no PMC profile for %s" % config
+    with open(p) as f:
+        d = json.load(f)
+    lib, prof = built_hash(), d.get("csrc_hash")
+    if not lib or prof != lib:
+        return None, "PMC profile %s is from csrc %s, the timed library from %s: traffic not attached" % (
+            os.path.basename(p), prof, lib)
+    t = d.get("lv_hbm_bytes_per_launch", {}).get(kernel)
+    return t, ("traffic of %s from %s (csrc %s)" % (kernel, os.path.basename(p), prof)) if t else \
+        "no %s counters in %s" % (kernel, os.path.basename(p))
+
+
 # ------------------------------------------------------------------------------- launcher
 def _free_port():
     s = socket.socket()
@@ -414,7 +431,7 @@ def main():
                                        "ms_per_step": tim["lv_%s_ms" % k] / args.steps}
             if lv:
                 dom = max(lv, key=lambda k: lv[k]["ms_per_step"])
-                traffic, traffic_note = None, "no PMC profile of %s attached" % dom
+                traffic, traffic_note = load_lv_traffic(args.config, dom)
                 roof = {"bound": "hbm", "achieved": lv[dom]["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": lv[dom]["frac"], "traffic": traffic, "traffic_note": traffic_note, "kernel": dom,
                         "note": "the %s CD's dominant kernel by time in the timed region; level 0 of Leiden runs the "

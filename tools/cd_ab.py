@@ -51,6 +51,9 @@ def child(lib, config, algo, reps):
             cds.append(t)
         lab = eng.get_labels(n_p)
         out["labels_sha"] = hashlib.sha1(lab.tobytes()).hexdigest()[:16]
+        if os.environ.get("FC_AB_CDONLY") == "1":     # PMC passes: the CD batches only
+            print(json.dumps(out), flush=True)
+            return
         out["cd_ms"] = min(t["cd_ms"] for t in cds)
         out["decide_ms"] = min(t["decide_ms"] for t in cds)
         out["decide_launches"] = cds[0]["decide_launches"]

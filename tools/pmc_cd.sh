@@ -7,7 +7,7 @@ OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 PROG="python3 tools/cd_ab.py --child $LIB $CFG $ALGO 1"
-KRE="k_decide_light|k_apply|k_cd_tail"
+KRE=${FC_PMC_KRE:-"k_decide_light|k_apply|k_cd_tail"}
 run() {  # run <name> <rocprof args...>
     local name=$1; shift
     echo "== $name"

@@ -34,6 +34,8 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
             if "k_decide_light" in kern:   # per instance: <true, int> is the consensus runs' Louvain kernel
                 targs = kern.split("<", 1)[1].split(">")[0].replace(" ", "")
                 short = "k_decide_light<%s>" % {"true,int": "louvain", "false,int": "lpa"}.get(targs, targs)
+            elif "k_lv_" in kern:       # Leiden / Infomap kernels: one entry per kernel (all instances)
+                short = short.split("::")[-1]
             counters[short][r.get("Counter_Name", "?")].append(float(r.get("Counter_Value", "nan")))
     per = {}
     for kern, cs in counters.items():
@@ -54,6 +56,11 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
         hit, miss = d.get("TCC_HIT_sum", (None,))[0], d.get("TCC_MISS_sum", (None,))[0]
         if hit is not None and miss:
             summary["decide_l2_hit_rate"] = hit / (hit + miss)
+    # Leiden / Infomap: per-launch HBM bytes of their own kernels (bench attaches the dominant one)
+    for kern in ("k_lv_decide", "k_lv_heavy"):
+        d = per.get(kern)
+        if d and "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            summary.setdefault("lv_hbm_bytes_per_launch", {})[kern] = (2.0 * d["FETCH_SIZE"][0] + d["WRITE_SIZE"][0]) * 1024.0
     with open(os.path.join(out_dir, "pmc_%s.json" % config), "w") as f:
         json.dump(summary, f, indent=1)
     # the rocprofv3 --stats summary itself, copied verbatim
