@@ -245,6 +245,8 @@ def main():
     ap.add_argument("--relabel", type=int, default=-1, help="internal vertex numbering (engine option; -1 = default)")
     ap.add_argument("--store", type=int, default=-1, help="label storage order (engine option; -1 = default)")
     ap.add_argument("--coarsen", type=int, default=-1, help="experimental coarse rounds, largest g (engine option)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="experiment: any engine option (fastconsensus_amd._lib option names), repeatable")
     ap.add_argument("--n-p", type=int, default=0, help="experiment: override the config's n_p")
     ap.add_argument("--resident", action="store_true",
                     help="experiment: time the loop only (graph loaded once before timing)")
@@ -317,6 +319,9 @@ def main():
             val = getattr(args, name)
             if val >= 0:
                 eng.set_option(name, val)
+        for kv in args.opt:
+            name, val = kv.split("=", 1)
+            eng.set_option(name, int(val))
     algo = ALGORITHMS[cfg["algo"]]
 
     # the final labelings land in ONE host array, allocated and faulted in before timing: a

@@ -201,7 +201,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
         case FC_OPT_SEED: c.seed = (uint64_t)value; break;
         case FC_OPT_CLOSURE_ROUNDS: FC_REQUIRE(value >= 1, FC_EINVAL, "closure_rounds >= 1"); c.closure_rounds = (int)value; break;
-        case FC_OPT_PRUNE_MARK: FC_REQUIRE(value == 0 || value == 1, FC_EINVAL, "prune_mark must be 0 or 1"); c.prune_mark = (int)value; break;
+        case FC_OPT_PRUNE_MARK: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "prune_mark must be 0, 1 or 2"); c.prune_mark = (int)value; break;
         case FC_OPT_INFOMAP_TRIALS: FC_REQUIRE(value >= 1, FC_EINVAL, "infomap trials >= 1"); c.infomap_trials = (int)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};

@@ -1379,7 +1379,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // graph: 1.5 % of the vertices marked after sweep 1, covering 99.6-100 % of sweep 2's
     // movers, against 85 % marked by "every neighbour of a mover").  Sweep 2 is already
     // filtered, so no unfiltered sweep is left for the pull -> push transition: lm is pull-only.
-    a.lm = (g.max_w > 1 && c.prune && c.prune_mark == 1) ? 1 : 0;
+    a.lm = ((g.max_w > 1 || c.prune_mark == 2) && c.prune && c.prune_mark >= 1) ? 1 : 0;
     if (a.lm) a.push_div = 0;
     a.mvf = nullptr;
     if (a.lm) {

@@ -135,7 +135,7 @@ struct Ctx {
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
     int closure_rounds = 8;         // FC_OPT_CLOSURE_ROUNDS
-    int prune_mark = 1;             // FC_OPT_PRUNE_MARK: 1 Leiden-style marks on consensus graphs, 0 every neighbour
+    int prune_mark = 1;             // FC_OPT_PRUNE_MARK: 1 Leiden-style marks on consensus graphs, 2 on every graph, 0 every neighbour
     DevBuf sort_tmp;                // hipcub temporary storage
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)

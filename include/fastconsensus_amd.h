@@ -136,7 +136,8 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 tracking starts at sweep 1 and, at each tracked sweep's end, a
                                 mover marks only the neighbours whose label differs from its own
                                 (fast local moving, Traag et al. 2019); unit-weight graphs keep
-                                0.  0: every neighbour of a mover, tracking from the first sweep
+                                0.  2: the same marks on every graph (the input graph too).
+                                0: every neighbour of a mover, tracking from the first sweep
                                 that moves < n/4 vertices.                                       */
 #define FC_OPT_INFOMAP_TRIALS 13 /* independent Infomap runs per replica, the smallest codelength kept
                                     (default 10, igraph community_infomap's trials)              */

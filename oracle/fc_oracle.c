@@ -1032,7 +1032,7 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
         M2 += s;
     }
     /* engine cd_run: Leiden-style marks on consensus graphs (weights > 1; LPA too) */
-    const int lm = max_w > 1 && prune && prune_mark == 1;
+    const int lm = (max_w > 1 || prune_mark == 2) && prune && prune_mark >= 1;
     (void)algo;
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {

@@ -188,6 +188,23 @@ def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen)
     eng.close()
 
 
+@pytest.mark.parametrize("coarsen", [0, 8])
+@pytest.mark.parametrize("tail", TAILS)
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cd_unit_prune_mark2_bit_exact_vs_twin(fcmod, algo, tail, coarsen):
+    """FC_OPT_PRUNE_MARK=2: the sweep-end marks (k_mark_lm) on the unit-weight input graph too."""
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=23)
+    eng.set_option("prune_mark", 2)
+    eng.set_option("tail_visits", tail)
+    eng.set_option("coarsen", coarsen)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    eng.cd(algo, 0, 6, 6, 2)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, 6, 0, 2, 23, coarsen=coarsen, prune_mark=2)
+    np.testing.assert_array_equal(eng.get_labels(6), exp)
+    eng.close()
+
+
 def _heavy_graph(seed, hub_deg):
     """Communities + a few hubs whose degree exceeds the light (64) and LDS (2048) paths."""
     rng = np.random.default_rng(seed)
