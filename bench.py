@@ -312,7 +312,7 @@ def main():
         from fastconsensus_amd.core import store_order_pays
         from fastconsensus_amd.distributed import shard
         r0, r1 = shard(cfg["n_p"], rank, world)
-        eng.set_option("store", store_order_pays(r1 - r0))   # --store overrides below
+        eng.set_option("store", store_order_pays(r1 - r0, ALGORITHMS[cfg["algo"]]))   # --store overrides below
         if args.buckets:
             eng.set_params(buckets=args.buckets)
         for name in ("chunk", "prune", "relabel", "store", "coarsen"):

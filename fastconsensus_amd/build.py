@@ -13,7 +13,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(OUT_DIR, "libfastconsensus_amd.so")
 SRC_HASH = LIB + ".srchash"     # the source hash the library was built from (profiles are matched to it)
-SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "leiden.hip", "capi.cpp", "gen.cpp"]
+SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "cd_rl.hip", "leiden.hip", "capi.cpp", "gen.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-fPIC", "-std=c++17", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",

@@ -362,11 +362,15 @@ def labels_to_output(algorithm, node_labels, labels):
     return out
 
 
-def store_order_pays(replicas):
+def store_order_pays(replicas, algorithm=None):
     """Label storage order (FC_OPT_STORE) for a GPU that will hold `replicas` replicas: the
-    one-replica ordering pass at load costs ~4 ms on LFR-1M and saves gather misses in
-    proportion to the replicas (measured: n_p=8 61.7 ms without vs 63.0 with, n_p=16 89.0 vs
-    87.0, n_p=64 saves ~20 ms)."""
+    one-replica ordering pass at load costs ~4 ms on LFR-1M and saves gather misses of the
+    CLASSIC CD engine in proportion to the replicas (measured: n_p=8 61.7 ms without vs 63.0
+    with, n_p=16 89.0 vs 87.0, n_p=64 saves ~20 ms).  The default replica-lane engine, which
+    runs the louvain / lpm batches, reads labels node-major and gains nothing from it; Leiden's
+    level-0 move phase still runs on the classic engine."""
+    if algorithm in (FC_ALGO_LOUVAIN, FC_ALGO_LPM, FC_ALGO_LOUVAIN_NC, "louvain", "lpm"):
+        return 0
     return 1 if replicas >= 12 else 0
 
 
@@ -399,7 +403,7 @@ def fast_consensus(G, algorithm='louvain', n_p=20, thresh=0.2, delta=0.02, *, se
         raise NotImplementedError("algorithm='leiden' is modelled for integer node labels only "
                                   "(fast_consensus.py:97, :214-217)")
     with Engine(device=device, seed=seed) as eng:
-        eng.set_option("store", store_order_pays(n_p))
+        eng.set_option("store", store_order_pays(n_p, algo))
         eng.load_graph(g.n, g.u, g.v)
         labels, stats = eng.run(algo, int(n_p), float(thresh), float(delta))
     out = labels_to_output(algorithm, g.labels, labels)

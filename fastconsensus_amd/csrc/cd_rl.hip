@@ -1,0 +1,898 @@
+// cd_rl.hip -- replica-lane community detection: the default engine for the louvain and lpm
+// CD batches (python-louvain level 0, fast_consensus.py:148 / :384; igraph LPA, :270 / :392).
+//
+// The classic engine (cd.hip) gives every replica its own random visit order, so a bucket of
+// one replica and a bucket of another hold different vertices: every neighbour-label gather
+// is a random 4-byte read of that replica's label row, one 128-byte line each.  Here every
+// replica of a CD batch visits the vertices in the SAME per-(iteration, sweep) random order
+// (replicas still differ: ties are broken by per-replica hashes, and each replica keeps its
+// own pruning state and stop).  A bucket is then one vertex set for all replicas, and labels
+// are stored node-major, labT[v][ldT] (one replica per lane): deciding vertex v for up to 64
+// replicas costs ONE row walk and, per neighbour u, ONE coalesced 256-byte read of u's labels
+// for all of them -- 2 lines per neighbour for 64 visits instead of 64 lines.  Community
+// totals are node-major too (totT[c][ldT]); with shared orders the replicas mostly agree on
+// community names, so Sigma reads coalesce as well.
+//
+// Statistical effect of the shared order (CPU engine model, tests/test_engine_semantics.py):
+// LFR-1k louvain consensus NMI 0.917 +- 0.03 (per-replica orders 0.906; reference loop 0.905),
+// lpm recovery 24/30 (20/30; reference 14/30), LFR-100k louvain 0.971 (0.968; reference-
+// semantics loop 0.968).  Every decision is exactly the classic rule; the CPU twin
+// (oracle/fc_oracle.c tw_replica, shared = 1, coarsen = 0) reproduces the engine bit for bit.
+//
+// Lanes: a wave holds VPW = 64 / LG vertices ("sub-groups") x LG replica lanes, LG the
+// smallest power of two >= the local replica count (at least 8, at most 64); more than 64
+// local replicas form banks of 64 (one unit = one vertex of one bank).  Per unit, light rows
+// (degree <= DM): the row's labels are staged in LDS as L[j][lane] (conflict-free columns),
+// equal labels are merged per lane by a triangular scan (duplicates marked), the candidates of
+// maximal weight compacted in place, and only their Sigma gathered (score = w*2M - k_v*Sigma
+// <= w*2M: a lighter candidate can only win if k_v*Sigma >= 2M, handled exactly by a rare
+// per-lane fallback).  Longer rows: one workgroup per unit (k_rl_heavy).
+#include <hipcub/hipcub.hpp>
+
+#include <chrono>
+
+#include "fc_ctx.h"
+#include "fc_device.h"
+
+namespace fc {
+
+template <class T> void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n);
+
+namespace {
+
+constexpr int RTB = 64;                 // decide / apply / mark blocks: one wave
+constexpr int DM = 64;                  // light rows: degree <= DM
+constexpr int VPWMAX = 8;               // sub-groups per wave (lane groups of >= 8 replicas)
+constexpr int RL_CHUNK = 16;            // = cd.hip CHUNK (chunked visit orders)
+constexpr int32_t DONE = -1;            // merged / own / empty table entry (labels are >= 0)
+constexpr uint32_t SHARED_RG = 0xffffffffu;   // stream key of the shared visit order (oracle TW_SHARED_RG)
+constexpr int NSH = 16;                 // counter shards per replica
+constexpr int RF = 8;                   // fields: 0 dq, 1 unstable, 2 moves, 3 visits, 4 entries, 5 cands, 6 units
+constexpr double DQ_SCALE = 1099511627776.0;   // 2^40 fixed point for predicted dQ (as cd.hip)
+constexpr int HSLOTS = 4096;            // heavy-row LDS table
+constexpr int HTB = 256;
+constexpr int HEAVY_GRID = 256;
+constexpr int LTB = 256;                // list kernels
+constexpr int LPER = 8;                 // vertices per thread in the list kernels
+
+struct RL {
+    int64_t N, S, PN;
+    int chunk;
+    uint32_t perm_n;
+    int B;
+    int n_r, rbase, LG, VPW, banks, ldT;
+    uint32_t iter;
+    uint64_t seed;
+    const int64_t* rowptr;
+    const int32_t* col;
+    const int32_t* cw;
+    const int4* vrec;            // row start, degree, k_v (int32: 2M < 2^31), slot
+    const int64_t* kdeg;
+    int64_t M2;
+    int unitw;
+    int32_t* lab;                // labT [N][ldT]
+    int32_t* tot;                // totT [N][ldT] (louvain)
+    int32_t* dec;                // [PN][ldT]: target community or -1, per list entry and replica
+    int32_t* list;               // [PN] the sweep's vertices, bucket-major
+    uint64_t* lmask;             // [PN][banks] visiting replicas of each entry
+    uint64_t* vmask;             // [N][banks] list-build scratch
+    int32_t* boff;               // [B+1] bucket offsets | cursors [B] | heavy count
+    int32_t* cursor;
+    uint64_t* aff;               // [banks][N] affected flags (pruning), one bit per replica
+    uint64_t* mvf;               // [banks][N] movers of a tracked sweep (lm)
+    int32_t* active;             // [n_r]
+    int32_t* track;              // [n_r] moves tracked this sweep | [n_r..2n_r) this sweep's list filters
+    int prune, lm, track_div;
+    unsigned long long* red;     // [n_r][NSH][RF]
+    unsigned long long* sacc;    // [n_r][4] visits / entries / cands / units over the run
+    int32_t* heavy;              // heavy units (entry * banks + bank) of the bucket
+    int32_t* heavy_cnt;
+    int32_t* hscratch;           // global tables for rows past the LDS table
+    int64_t hslots;
+    double min_dq;
+};
+
+__device__ __forceinline__ Perm rl_perm(const RL& a, int sweep) {
+    Perm P = make_perm(a.perm_n, stream_key(a.seed, SHARED_RG, a.iter, (uint32_t)sweep, 1));
+    if (a.chunk) P.off = stream_key(a.seed, SHARED_RG, a.iter, (uint32_t)sweep, 3) & (RL_CHUNK - 1);
+    return P;
+}
+__device__ __forceinline__ uint32_t rl_bucket(const RL& a, const Perm& P, uint32_t v) {
+    uint32_t pos;
+    if (!a.chunk) pos = perm_invert(P, v);
+    else {
+        const uint32_t w = v + P.off;
+        pos = perm_invert(P, w / RL_CHUNK) * RL_CHUNK + w % RL_CHUNK;
+    }
+    return pos / (uint32_t)a.S;
+}
+__device__ __forceinline__ unsigned long long* rl_red(const RL& a, int r, int f) {
+    return a.red + ((size_t)r * NSH + (blockIdx.x & (NSH - 1))) * RF + f;
+}
+__device__ __forceinline__ bool rl_better(long long s1, uint32_t h1, int32_t c1, long long s2, uint32_t h2,
+                                          int32_t c2) {
+    if (s1 != s2) return s1 > s2;
+    if (h1 != h2) return h1 > h2;
+    return c1 < c2;
+}
+__device__ __forceinline__ int wave_max(int x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off));
+    return x;
+}
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// ------------------------------------------------------------------ init / export
+__global__ void k_rl_init(int64_t N, int ldT, const int64_t* kdeg, int32_t* lab, int32_t* tot) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * ldT) return;
+    const int64_t v = i / ldT;
+    lab[i] = (int32_t)v;
+    if (tot) tot[i] = (int32_t)kdeg[v];
+}
+// labT [N][ldT] -> lab [n_r][N] in slot order (what labels_to_host and the Leiden code read):
+// 64 slots x 64 replicas per tile through LDS, label rows read and slot rows written as whole
+// 256-byte runs (the inverse of cd.hip k_transpose)
+__global__ __launch_bounds__(256) void k_rl_export(int64_t N, int n_r, int ldT, const int32_t* labT, const int32_t* sinv,
+                                                   int32_t* lab) {
+    __shared__ int32_t t[64][65];
+    __shared__ int32_t sv[64];
+    const int64_t s0 = (int64_t)blockIdx.x * 64;
+    const int r0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+    if (ty == 0) sv[tx] = s0 + tx < N ? sinv[s0 + tx] : -1;
+    __syncthreads();
+    for (int ss = ty; ss < 64; ss += 4) {
+        const int32_t v = sv[ss];
+        const int r = r0 + tx;
+        if (v >= 0 && r < n_r) t[ss][tx] = labT[(int64_t)v * ldT + r];
+    }
+    __syncthreads();
+    for (int rr = ty; rr < 64; rr += 4) {
+        const int r = r0 + rr;
+        if (r < n_r && s0 + tx < N) lab[(int64_t)r * N + s0 + tx] = t[tx][rr];
+    }
+}
+
+// ------------------------------------------------------------------ visit lists
+// Per vertex and bank: the replicas visiting it this sweep -- active ones in a full sweep,
+// plus filtered ones whose affected bit is set (every neighbour of a tracked mover, or with
+// lm the neighbours that ended in another community).  A listed sweep (prune, sweep > 0)
+// consumes the flags (oracle tw_replica clears them at the sweep start).  Dynamic LDS:
+// B ints + 2 * banks u64.
+__global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int listed, int32_t* bcnt) {
+    extern __shared__ unsigned long long s_dyn[];
+    uint64_t* s_act = (uint64_t*)s_dyn;
+    uint64_t* s_flt = s_act + a.banks;
+    int* s_b = (int*)(s_flt + a.banks);
+    for (int k = threadIdx.x; k < a.B; k += LTB) s_b[k] = 0;
+    for (int b = threadIdx.x; b < a.banks; b += LTB) { s_act[b] = 0; s_flt[b] = 0; }
+    __syncthreads();
+    for (int r = threadIdx.x; r < a.n_r; r += LTB) {
+        if (!a.active[r]) continue;
+        atomicOr((unsigned long long*)&s_act[r >> 6], 1ull << (r & 63));
+        if (a.prune && a.track[a.n_r + r]) atomicOr((unsigned long long*)&s_flt[r >> 6], 1ull << (r & 63));
+    }
+    __syncthreads();
+    const Perm P = rl_perm(a, sweep);
+    const int64_t v0 = (int64_t)blockIdx.x * LTB * LPER + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < LPER; ++i) {
+        const int64_t v = v0 + (int64_t)i * LTB;
+        if (v >= a.N) break;
+        bool any = false;
+        for (int b = 0; b < a.banks; ++b) {
+            uint64_t f = a.aff[(int64_t)b * a.N + v];
+            if (listed && f) a.aff[(int64_t)b * a.N + v] = 0;
+            const uint64_t m = s_act[b] & (~s_flt[b] | f);
+            a.vmask[v * a.banks + b] = m;
+            any |= m != 0;
+        }
+        if (any) atomicAdd(&s_b[rl_bucket(a, P, (uint32_t)v)], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < a.B; k += LTB)
+        if (s_b[k]) atomicAdd(&bcnt[k], s_b[k]);
+}
+__global__ void k_rl_list_plan(int B, const int32_t* bcnt, int32_t* boff, int32_t* cursor) {
+    if (threadIdx.x != 0) return;
+    int32_t acc = 0;
+    for (int k = 0; k < B; ++k) { boff[k] = acc; cursor[k] = acc; acc += bcnt[k]; }
+    boff[B] = acc;
+}
+__global__ __launch_bounds__(LTB) void k_rl_list_fill(RL a, int sweep) {
+    extern __shared__ int s_lb[];
+    int* s_cnt = s_lb;
+    int* s_base = s_lb + a.B;
+    for (int k = threadIdx.x; k < a.B; k += LTB) s_cnt[k] = 0;
+    __syncthreads();
+    const Perm P = rl_perm(a, sweep);
+    int bk[LPER], loc[LPER];
+    const int64_t v0 = (int64_t)blockIdx.x * LTB * LPER + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < LPER; ++i) {
+        const int64_t v = v0 + (int64_t)i * LTB;
+        bk[i] = -1;
+        if (v >= a.N) continue;
+        bool any = false;
+        for (int b = 0; b < a.banks; ++b) any |= a.vmask[v * a.banks + b] != 0;
+        if (!any) continue;
+        bk[i] = (int)rl_bucket(a, P, (uint32_t)v);
+        loc[i] = atomicAdd(&s_cnt[bk[i]], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < a.B; k += LTB) s_base[k] = s_cnt[k] ? atomicAdd(&a.cursor[k], s_cnt[k]) : 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < LPER; ++i) {
+        if (bk[i] < 0) continue;
+        const int64_t v = v0 + (int64_t)i * LTB;
+        const int64_t e = s_base[bk[i]] + loc[i];
+        a.list[e] = (int32_t)v;
+        for (int b = 0; b < a.banks; ++b) a.lmask[e * a.banks + b] = a.vmask[v * a.banks + b];
+    }
+}
+
+// ------------------------------------------------------------------ unit mapping
+// Wave item w of a bucket whose entries are [e0, e1): one bank -> VPW consecutive entries
+// (sub-group s takes entry e0 + w*VPW + s); several banks -> entry e0 + w / banks, bank w % banks.
+struct Unit {
+    int64_t e;
+    int bank, s, rl, r;
+    bool valid;
+};
+__device__ __forceinline__ Unit rl_unit(const RL& a, int64_t e0, int64_t e1, int64_t w) {
+    Unit u;
+    const int lane = threadIdx.x & 63;
+    u.s = lane / a.LG;
+    u.rl = lane - u.s * a.LG;
+    if (a.banks == 1) { u.e = e0 + w * a.VPW + u.s; u.bank = 0; }
+    else { u.e = e0 + w / a.banks; u.bank = (int)(w % a.banks); }
+    u.r = u.bank * 64 + u.rl;
+    u.valid = u.e < e1 && u.s < a.VPW;
+    return u;
+}
+__device__ __forceinline__ int64_t rl_items(const RL& a, int64_t n) {
+    return a.banks == 1 ? (n + a.VPW - 1) / a.VPW : n * a.banks;
+}
+
+// ------------------------------------------------------------------ decide (light rows)
+struct RLShared {
+    int32_t L[DM][64];           // row labels per lane; merged / own entries DONE; then the candidates
+    int32_t C[VPWMAX][DM];       // the sub-groups' rows (neighbour ids)
+    int32_t W[VPWMAX][DM];       // their weights (weighted graphs)
+};
+
+template <bool LOUV>
+__global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int k, int sweep) {
+    __shared__ RLShared sh;
+    const int lane = threadIdx.x & 63;
+    const int64_t e0 = a.boff[k], e1 = a.boff[k + 1];
+    const int64_t items = rl_items(a, e1 - e0);
+    const int LG = a.LG, VPW = a.VPW;
+    // per-lane counters, flushed once per wave
+    unsigned long long c_dq = 0, c_unst = 0, c_vis = 0, c_ent = 0, c_cand = 0, c_units = 0;
+    int last_r = -1;
+    auto flush = [&](int r) {
+        if (r < 0) return;
+        // lanes with the same replica (one per sub-group) are folded first
+        for (int off = LG; off < 64; off <<= 1) {
+            c_dq += __shfl_xor(c_dq, off); c_unst += __shfl_xor(c_unst, off); c_vis += __shfl_xor(c_vis, off);
+            c_ent += __shfl_xor(c_ent, off); c_cand += __shfl_xor(c_cand, off); c_units += __shfl_xor(c_units, off);
+        }
+        if (lane < LG && r < a.n_r) {
+            if (c_dq) atomicAdd(rl_red(a, r, 0), c_dq);
+            if (c_unst) atomicAdd(rl_red(a, r, 1), c_unst);
+            if (c_vis) atomicAdd(rl_red(a, r, 3), c_vis);
+            if (c_ent) atomicAdd(rl_red(a, r, 4), c_ent);
+            if (c_cand) atomicAdd(rl_red(a, r, 5), c_cand);
+            if (c_units) atomicAdd(rl_red(a, r, 6), c_units);
+        }
+        c_dq = c_unst = c_vis = c_ent = c_cand = c_units = 0;
+    };
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        const Unit u = rl_unit(a, e0, e1, w);
+        if (a.banks > 1 && u.r != last_r) { flush(last_r); }
+        last_r = a.banks > 1 ? u.r : lane % LG;
+        const int rr = u.bank * 64 + u.rl;                      // local replica of this lane
+        int32_t v = -1;
+        uint64_t msk = 0;
+        if (u.valid) {
+            v = a.list[u.e];
+            msk = a.lmask[u.e * a.banks + u.bank];
+        }
+        const bool on = u.valid && rr < a.n_r && ((msk >> u.rl) & 1ull);
+        int64_t rb = 0;
+        int d = 0, kvi = 0;
+        if (u.valid) {
+            const int4 vr = a.vrec[v];
+            rb = (int64_t)(uint32_t)vr.x;
+            d = vr.y;
+            kvi = vr.z;
+        }
+        const bool heavy = u.valid && d > DM;
+        if (heavy && u.rl == 0 && msk) a.heavy[atomicAdd(a.heavy_cnt, 1)] = (int32_t)(u.e * a.banks + u.bank);
+        const bool work = on && !heavy && d > 0;
+        const int ds = (u.valid && !heavy && msk) ? d : 0;     // the sub-group's staged row length
+        const int64_t lrow = (int64_t)v * a.ldT + rr;
+        int32_t own = -1;
+        int32_t tot_own = 0;
+        if (work) own = a.lab[lrow];
+        // sub-group rows, flattened over the wave: prefix of the row lengths
+        int o[VPWMAX], dsub[VPWMAX];
+        int E = 0, dmax = 0;
+#pragma unroll
+        for (int t = 0; t < VPWMAX; ++t) {
+            dsub[t] = t < VPW ? __shfl(ds, t * LG) : 0;
+            o[t] = E;
+            E += dsub[t];
+            dmax = max(dmax, dsub[t]);
+        }
+        if (E == 0) {                                           // wave-uniform: nothing light here
+            if (u.valid && rr < a.n_r) a.dec[u.e * a.ldT + rr] = -1;
+            continue;
+        }
+        // row starts of the sub-groups, read while every lane is active (a shuffle from a
+        // lane that has left the loop below would read garbage)
+        int64_t rbs[VPWMAX];
+#pragma unroll
+        for (int t = 0; t < VPWMAX; ++t) rbs[t] = t < VPW ? __shfl(rb, t * LG) : 0;
+        for (int f = lane; f < E; f += 64) {
+            int t = 0;
+#pragma unroll
+            for (int q = 1; q < VPWMAX; ++q) t += (q < VPW && f >= o[q]) ? 1 : 0;
+            int64_t rbt = rbs[0];
+            int ot = o[0];
+#pragma unroll
+            for (int q = 1; q < VPWMAX; ++q)
+                if (t == q) { rbt = rbs[q]; ot = o[q]; }
+            const int j = f - ot;
+            sh.C[t][j] = a.col[rbt + j];
+            if (!a.unitw) sh.W[t][j] = a.cw[rbt + j];
+        }
+        if (LOUV && work) tot_own = a.tot[(int64_t)own * a.ldT + rr];
+        wsync();
+        // stage the labels: 32 gathers in flight per lane, own-community entries summed (louvain)
+        long long kown = 0;
+        for (int j0 = 0; j0 < dmax; j0 += 32) {
+            int32_t lb[32];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                const int j = j0 + q;
+                lb[q] = (work && j < ds) ? a.lab[(int64_t)sh.C[u.s][j] * a.ldT + rr] : DONE;
+            }
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                const int j = j0 + q;
+                if (j >= dmax) break;
+                int32_t c = lb[q];
+                if (LOUV && c >= 0 && c == own) {
+                    kown += a.unitw ? 1 : sh.W[u.s][j];
+                    c = DONE;
+                }
+                sh.L[j][lane] = c;
+            }
+        }
+        wsync();
+        // merge equal labels: the first occurrence sums its duplicates and marks them; the
+        // candidates of maximal weight are compacted into L[0..nc)
+        int vm = INT_MIN, nc = 0;
+        for (int j1 = 0; j1 < dmax; ++j1) {
+            const int32_t c1 = sh.L[j1][lane];
+            if (__ballot(c1 >= 0) == 0) continue;               // wave-uniform
+            int acc = 0;
+            if (c1 >= 0) {
+                acc = a.unitw ? 1 : sh.W[u.s][j1];
+                for (int j2 = j1 + 1; j2 < dmax; ++j2) {
+                    if (sh.L[j2][lane] == c1) {
+                        acc += a.unitw ? 1 : sh.W[u.s][j2];
+                        sh.L[j2][lane] = DONE;
+                    }
+                }
+                if (!LOUV && c1 == own) kown = acc;
+                if (acc > vm) { vm = acc; nc = 0; }
+                if (acc == vm) { sh.L[nc][lane] = c1; ++nc; }
+            }
+        }
+        wsync();
+        const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)v);
+        int32_t dcs = -1;
+        if (LOUV) {
+            // Sigma of the maximal-weight candidates, 8 gathers in flight per lane
+            long long best_s = LLONG_MIN;
+            uint32_t best_h = 0;
+            int32_t best_c = INT_MAX;
+            const long long kv = kvi;
+            const int ncm = wave_max(work ? nc : 0);
+            for (int i0 = 0; i0 < ncm; i0 += 8) {
+                int32_t cq[8], tq[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    cq[q] = (work && i0 + q < nc) ? sh.L[i0 + q][lane] : -1;
+                    tq[q] = cq[q] >= 0 ? a.tot[(int64_t)cq[q] * a.ldT + rr] : 0;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (cq[q] < 0) continue;
+                    const long long sc = (long long)vm * a.M2 - kv * (long long)tq[q];
+                    const uint32_t h = hash32(tvh ^ (uint32_t)cq[q]);
+                    if (best_c == INT_MAX || rl_better(sc, h, cq[q], best_s, best_h, best_c)) {
+                        best_s = sc; best_h = h; best_c = cq[q];
+                    }
+                }
+            }
+            if (work) c_cand += (unsigned long long)nc;
+            // a lighter candidate scores <= (vm - 1) * 2M: it can only reach the best when
+            // k_v * Sigma_min >= 2M (rare) -- then the lane re-evaluates every candidate
+            const bool slow = work && nc > 0 && (long long)(vm - 1) * a.M2 >= best_s;
+            if (__ballot(slow)) {                               // wave-uniform
+                if (slow) {
+                    for (int j1 = 0; j1 < d; ++j1) {
+                        const int32_t c1 = a.lab[(int64_t)a.col[rb + j1] * a.ldT + rr];
+                        if (c1 == own) continue;
+                        bool dup = false;
+                        for (int j2 = 0; j2 < j1 && !dup; ++j2) dup = a.lab[(int64_t)a.col[rb + j2] * a.ldT + rr] == c1;
+                        if (dup) continue;
+                        long long val = 0;
+                        for (int j2 = j1; j2 < d; ++j2)
+                            if (a.lab[(int64_t)a.col[rb + j2] * a.ldT + rr] == c1) val += a.unitw ? 1 : a.cw[rb + j2];
+                        if (val >= vm) continue;                // evaluated above
+                        const long long sc = val * a.M2 - kv * (long long)a.tot[(int64_t)c1 * a.ldT + rr];
+                        const uint32_t h = hash32(tvh ^ (uint32_t)c1);
+                        ++c_cand;
+                        if (rl_better(sc, h, c1, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = c1; }
+                    }
+                }
+            }
+            if (work && nc > 0) {
+                const long long G = best_s - kown * a.M2 + kv * ((long long)tot_own - kv);
+                if (G > 0) {
+                    const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+                    c_dq += (unsigned long long)llrint(dqd * DQ_SCALE);
+                    dcs = best_c;
+                }
+            }
+        } else {
+            // LPA: the most frequent label (own included), ties by the replica's hash
+            uint32_t best_h = 0;
+            int32_t best_c = -1;
+            for (int i = 0; i < nc; ++i) {
+                const int32_t c = sh.L[i][lane];
+                const uint32_t h = hash32(tvh ^ (uint32_t)c);
+                if (best_c < 0 || h > best_h) { best_h = h; best_c = c; }
+            }
+            if (work) {
+                c_cand += (unsigned long long)nc;
+                if (nc > 0) {
+                    c_unst += (kown != (long long)vm) ? 1 : 0;
+                    dcs = best_c != own ? best_c : -1;
+                }
+            }
+        }
+        if (work) { c_vis += 1; c_ent += (unsigned long long)d; }
+        if (u.valid && u.rl == 0 && msk && !heavy) c_units += 1;
+        if (u.valid && rr < a.n_r) a.dec[u.e * a.ldT + rr] = work ? dcs : -1;
+        wsync();                                                // L is reused by the next item
+    }
+    flush(last_r);
+}
+
+// ------------------------------------------------------------------ decide (heavy rows)
+template <bool LOUV>
+__global__ __launch_bounds__(HTB) void k_rl_heavy(RL a, int sweep) {
+    __shared__ int32_t key[HSLOTS], val[HSLOTS];
+    __shared__ long long s_s[HTB], s_k[HTB];
+    __shared__ uint32_t s_h[HTB];
+    __shared__ int32_t s_c[HTB];
+    const int cnt = *a.heavy_cnt;
+    for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
+        const int32_t unit = a.heavy[item];
+        const int64_t e = unit / a.banks;
+        const int bank = unit % a.banks;
+        const int32_t v = a.list[e];
+        const uint64_t msk = a.lmask[e * a.banks + bank];
+        const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
+        uint32_t slots = 1;
+        while (slots < 2 * (uint32_t)d) slots <<= 1;
+        int32_t* keys = key;
+        int32_t* vals = val;
+        if (slots > HSLOTS) {
+            slots = (uint32_t)a.hslots;
+            keys = a.hscratch + (int64_t)blockIdx.x * 2 * a.hslots;
+            vals = keys + slots;
+        }
+        const long long kv = a.kdeg[v];
+        for (int rl = 0; rl < 64; ++rl) {                      // block-uniform
+            const int rr = bank * 64 + rl;
+            if (rr >= a.n_r || !((msk >> rl) & 1ull)) continue;
+            for (uint32_t s = threadIdx.x; s < slots; s += HTB) { keys[s] = -1; vals[s] = 0; }
+            __syncthreads();
+            for (int64_t j = rb + threadIdx.x; j < rb + d; j += HTB) {
+                const int32_t c = a.lab[(int64_t)a.col[j] * a.ldT + rr];
+                const int32_t w = a.unitw ? 1 : a.cw[j];
+                uint32_t h = hash32((uint32_t)c) & (slots - 1);
+                while (true) {
+                    const int32_t prev = atomicCAS(&keys[h], -1, c);
+                    if (prev == -1 || prev == c) { atomicAdd(&vals[h], w); break; }
+                    h = (h + 1) & (slots - 1);
+                }
+            }
+            __syncthreads();
+            const int32_t own = a.lab[(int64_t)v * a.ldT + rr];
+            const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)v);
+            long long best_s = LLONG_MIN, kown = 0;
+            uint32_t best_h = 0;
+            int32_t best_c = INT_MAX;
+            int ncand = 0;
+            for (uint32_t s = threadIdx.x; s < slots; s += HTB) {
+                const int32_t c = keys[s];
+                if (c < 0) continue;
+                const long long w = vals[s];
+                if (c == own) kown = w;
+                long long sc;
+                if (LOUV) {
+                    if (c == own) continue;
+                    sc = w * a.M2 - kv * (long long)a.tot[(int64_t)c * a.ldT + rr];
+                } else {
+                    sc = w;
+                }
+                ++ncand;
+                const uint32_t h = hash32(tvh ^ (uint32_t)c);
+                if (best_c == INT_MAX || rl_better(sc, h, c, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = c; }
+            }
+            s_s[threadIdx.x] = best_s; s_h[threadIdx.x] = best_h; s_c[threadIdx.x] = best_c; s_k[threadIdx.x] = kown;
+            if (ncand) atomicAdd(rl_red(a, rr, 5), (unsigned long long)ncand);
+            __syncthreads();
+            for (int off = HTB / 2; off > 0; off >>= 1) {
+                if ((int)threadIdx.x < off) {
+                    const int t2 = threadIdx.x + off;
+                    if (s_c[t2] != INT_MAX && (s_c[threadIdx.x] == INT_MAX ||
+                                               rl_better(s_s[t2], s_h[t2], s_c[t2], s_s[threadIdx.x], s_h[threadIdx.x],
+                                                         s_c[threadIdx.x]))) {
+                        s_s[threadIdx.x] = s_s[t2]; s_h[threadIdx.x] = s_h[t2]; s_c[threadIdx.x] = s_c[t2];
+                    }
+                    s_k[threadIdx.x] += s_k[t2];
+                }
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) {
+                int32_t dcs = -1;
+                if (s_c[0] != INT_MAX) {
+                    if (LOUV) {
+                        const long long tot_own = a.tot[(int64_t)own * a.ldT + rr];
+                        const long long G = s_s[0] - s_k[0] * a.M2 + kv * (tot_own - kv);
+                        if (G > 0) {
+                            const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+                            atomicAdd(rl_red(a, rr, 0), (unsigned long long)llrint(dqd * DQ_SCALE));
+                            dcs = s_c[0];
+                        }
+                    } else {
+                        if (s_k[0] != s_s[0]) atomicAdd(rl_red(a, rr, 1), 1ull);
+                        dcs = s_c[0] != own ? s_c[0] : -1;
+                    }
+                }
+                a.dec[e * a.ldT + rr] = dcs;
+                atomicAdd(rl_red(a, rr, 3), 1ull);
+                atomicAdd(rl_red(a, rr, 4), (unsigned long long)d);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ apply
+// A bucket's moves: label, community totals (int32 atomics, order-free), and while tracking
+// either every neighbour flagged (one 64-bit OR per neighbour for all the sub-group's movers)
+// or, with lm, the movers listed for k_rl_mark_lm.
+template <bool LOUV>
+__global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.heavy_cnt = 0;   // the bucket's heavy list is consumed
+    const int lane = threadIdx.x & 63;
+    const int64_t e0 = a.boff[k], e1 = a.boff[k + 1];
+    const int64_t items = rl_items(a, e1 - e0);
+    const int LG = a.LG;
+    unsigned long long moves = 0;
+    int last_r = -1;
+    auto flush = [&](int r) {
+        if (r < 0) return;
+        for (int off = LG; off < 64; off <<= 1) moves += __shfl_xor(moves, off);
+        if (lane < LG && r < a.n_r && moves) atomicAdd(rl_red(a, r, 2), moves);
+        moves = 0;
+    };
+    const uint64_t gmask = LG == 64 ? ~0ull : ((1ull << LG) - 1ull);
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        const Unit u = rl_unit(a, e0, e1, w);
+        if (a.banks > 1 && u.r != last_r) flush(last_r);
+        last_r = a.banks > 1 ? u.r : lane % LG;
+        const int rr = u.r;
+        int32_t t = -1, v = -1;
+        if (u.valid) {
+            v = a.list[u.e];
+            if (rr < a.n_r) t = a.dec[u.e * a.ldT + rr];
+        }
+        const bool moved = t >= 0;
+        if (moved) {
+            const int64_t lrow = (int64_t)v * a.ldT + rr;
+            const int32_t old = a.lab[lrow];
+            a.lab[lrow] = t;
+            if (LOUV) {
+                const int32_t kv = a.vrec[v].z;
+                atomicAdd(&a.tot[(int64_t)old * a.ldT + rr], -kv);
+                atomicAdd(&a.tot[(int64_t)t * a.ldT + rr], kv);
+            }
+            ++moves;
+        }
+        const bool trk = moved && a.track[rr];
+        const uint64_t bal = __ballot(trk);
+        const uint64_t ms = (bal >> (u.s * LG)) & gmask;        // the sub-group's tracked movers
+        if (!bal) continue;                                     // wave-uniform
+        if (a.lm) {
+            if (u.valid && u.rl == 0 && ms) a.mvf[(int64_t)u.bank * a.N + v] = ms;
+        } else if (u.valid && ms) {
+            const int4 vr = a.vrec[v];
+            const int64_t rb = (int64_t)(uint32_t)vr.x;
+            for (int j = u.rl; j < vr.y; j += LG)
+                atomicOr((unsigned long long*)&a.aff[(int64_t)u.bank * a.N + a.col[rb + j]], (unsigned long long)ms);
+        }
+    }
+    flush(last_r);
+}
+
+// End of a tracked lm sweep: each mover marks the neighbours whose label now differs from its
+// own (oracle tw_replica; cd.hip k_mark_lm), comparing the labels the sweep left.
+__global__ __launch_bounds__(RTB) void k_rl_mark_lm(RL a) {
+    const int lane = threadIdx.x & 63;
+    const int LG = a.LG, VPW = a.VPW;
+    const int s = lane / LG, rl = lane - s * LG;
+    const int64_t per = a.banks == 1 ? VPW : 1;
+    const int64_t items = a.banks == 1 ? (a.N + VPW - 1) / VPW : a.N * a.banks;
+    const uint64_t gmask = LG == 64 ? ~0ull : ((1ull << LG) - 1ull);
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        int64_t v;
+        int bank;
+        if (a.banks == 1) { v = w * per + s; bank = 0; }
+        else { v = w / a.banks; bank = (int)(w % a.banks); }
+        const bool valid = s < VPW && v < a.N;
+        uint64_t m = valid ? a.mvf[(int64_t)bank * a.N + v] : 0;
+        if (__ballot(m != 0) == 0) continue;                    // wave-uniform
+        if (valid && rl == 0 && m) a.mvf[(int64_t)bank * a.N + v] = 0;
+        const int rr = bank * 64 + rl;
+        const bool mine = valid && ((m >> rl) & 1ull);
+        const int32_t dl = mine ? a.lab[v * a.ldT + rr] : -1;
+        int d = 0;
+        int64_t rb = 0;
+        if (valid && m) {
+            const int4 vr = a.vrec[v];
+            rb = (int64_t)(uint32_t)vr.x;
+            d = vr.y;
+        }
+        const int dmax = wave_max(d);
+        for (int j = 0; j < dmax; ++j) {
+            const bool in = j < d;
+            const int32_t nb = in ? a.col[rb + j] : 0;
+            const bool diff = mine && in && a.lab[(int64_t)nb * a.ldT + rr] != dl;
+            const uint64_t bs = (__ballot(diff) >> (s * LG)) & gmask;
+            if (in && rl == 0 && bs) atomicOr((unsigned long long*)&a.aff[(int64_t)bank * a.N + nb], (unsigned long long)bs);
+        }
+    }
+}
+
+// End of a sweep, per replica (cd.hip k_sweep_end without the push / transition modes):
+// python-louvain stops a level when the pass gained < min_dq or moved nothing; igraph LPA
+// when no visited vertex was unstable.  n_active_out: [0] active after, [2..3] u64 moves,
+// [4..5] u64 replica-sweeps so far, [6..7] u64 visits of this sweep.
+template <bool LOUV>
+__global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
+    __shared__ int cnt, cnt0;
+    __shared__ unsigned long long mv, vis;
+    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; mv = 0; vis = 0; }
+    __syncthreads();
+    for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
+        unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long* base = a.red + (size_t)r * NSH * RF;
+        for (int sh = 0; sh < NSH; ++sh)
+            for (int q = 0; q < RF; ++q) { f[q] += base[sh * RF + q]; base[sh * RF + q] = 0; }
+        a.sacc[4 * r + 0] += f[3]; a.sacc[4 * r + 1] += f[4]; a.sacc[4 * r + 2] += f[5]; a.sacc[4 * r + 3] += f[6];
+        atomicAdd(&mv, f[2]);
+        atomicAdd(&vis, f[3]);
+        if (a.prune) {   // lists filter next sweep iff moves were tracked this sweep
+            a.track[a.n_r + r] = a.track[r];
+            if (a.lm || f[2] * (unsigned long long)a.track_div < (unsigned long long)a.N) a.track[r] = 1;
+        }
+        if (a.active[r]) {
+            atomicAdd(&cnt0, 1);
+            bool stop;
+            if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < a.min_dq;
+            else stop = f[1] == 0;
+            if (stop) a.active[r] = 0;
+            else atomicAdd(&cnt, 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        n_active_out[0] = cnt;
+        *(unsigned long long*)(n_active_out + 2) = mv;
+        *(unsigned long long*)(n_active_out + 4) += (unsigned long long)cnt0;
+        *(unsigned long long*)(n_active_out + 6) = vis;
+    }
+}
+
+inline unsigned nb(int64_t n, int tb) {
+    int64_t b = (n + tb - 1) / tb;
+    return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+// Replica-lane layout of a batch of n_r local replicas: lane group LG (power of two, 8..64),
+// vertices per wave 64 / LG, banks of 64 past 64 replicas; label rows of ldT int32.
+void rl_layout(int n_r, int* LG, int* VPW, int* banks, int* ldT) {
+    int lg = 8;
+    while (lg < n_r && lg < 64) lg <<= 1;
+    *LG = lg;
+    *VPW = 64 / lg;
+    *banks = (n_r + 63) / 64;
+    *ldT = n_r > 64 ? 64 * *banks : lg;
+}
+
+bool cd_rl_supported(const Ctx& c, int algo) {
+    return c.cd_engine == 1 && !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && c.g.M2 <= 0x7fffffffll &&
+           c.g.m < (int64_t(1) << 31) && (c.chunk == 0 || c.chunk == RL_CHUNK);
+}
+
+void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+    FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
+    FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
+    const int sl0 = timer_begin(c);
+    const bool louv = is_louvain(algo);
+    const int64_t N = c.N;
+    Graph& g = c.g;
+    c.n_r = rcount; c.rbase = rbegin; c.n_p_total = n_p_total;
+    int LG, VPW, banks, ldT;
+    rl_layout(rcount, &LG, &VPW, &banks, &ldT);
+    const int CH = c.chunk;
+    const int64_t NC = CH ? (N + 2 * CH - 2) / CH : N;   // room for the chunk-grid shift (as cd.hip)
+    const int B = (int)std::min<int64_t>(c.buckets, NC);
+    const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
+    const int64_t PN = CH ? NC * CH : N;
+
+    RL a;
+    a.N = N; a.S = S; a.PN = PN; a.chunk = CH; a.perm_n = (uint32_t)NC; a.B = B;
+    a.n_r = rcount; a.rbase = rbegin; a.LG = LG; a.VPW = VPW; a.banks = banks; a.ldT = ldT;
+    a.iter = (uint32_t)iteration; a.seed = c.seed;
+    a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
+    a.vrec = g.vrec.as<int4>(); a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
+    a.unitw = (!louv || (g.max_w == 1 && g.M2 == 2 * g.m)) ? 1 : 0;
+    a.lab = ensure<int32_t>(c.labT, (size_t)N * ldT);
+    a.tot = louv ? ensure<int32_t>(c.tot, (size_t)N * ldT) : nullptr;
+    a.dec = ensure<int32_t>(c.dec, (size_t)PN * ldT);
+    a.list = ensure<int32_t>(c.vlist, (size_t)PN);
+    a.lmask = (uint64_t*)ensure<uint64_t>(c.rl_lmask, (size_t)PN * banks);
+    a.vmask = (uint64_t*)ensure<uint64_t>(c.rl_vmask, (size_t)N * banks);
+    int32_t* plan = ensure<int32_t>(c.vcnt, 3 * (size_t)B + 8);
+    int32_t* bcnt = plan;
+    a.boff = bcnt + B;
+    a.cursor = a.boff + B + 1;
+    a.aff = (uint64_t*)ensure<uint64_t>(c.rl_aff, (size_t)banks * N);
+    a.mvf = (uint64_t*)ensure<uint64_t>(c.rl_mvf, (size_t)banks * N);
+    FC_HIP(hipMemsetAsync(a.aff, 0, 8 * (size_t)banks * N, c.stream));
+    FC_HIP(hipMemsetAsync(a.mvf, 0, 8 * (size_t)banks * N, c.stream));
+    a.prune = c.prune;
+    a.track_div = c.track_div;
+    // Leiden-style marks (cd.hip): consensus graphs, or every graph with prune_mark = 2
+    a.lm = ((g.max_w > 1 || c.prune_mark == 2) && c.prune && c.prune_mark >= 1) ? 1 : 0;
+    a.min_dq = c.cd_min_dq;
+    // per-replica state: active i32 [n_r] | track i32 [2 n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active [8]
+    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * (12 + 8 * NSH * RF + 32) + 512);
+    a.active = (int32_t*)rs;
+    a.track = a.active + rcount;
+    a.red = (unsigned long long*)(rs + (((size_t)rcount * 12 + 255) & ~size_t(255)));
+    a.sacc = a.red + (size_t)rcount * NSH * RF;
+    int32_t* n_active = (int32_t*)(a.sacc + 4 * (size_t)rcount);
+    const size_t zero_bytes = (char*)(n_active + 8) - (char*)a.red;
+    FC_HIP(hipMemsetAsync(a.track, 0, 8 * (size_t)rcount, c.stream));
+    FC_HIP(hipMemsetAsync(a.red, 0, zero_bytes, c.stream));
+    {
+        std::vector<int32_t> ones(rcount, (g.M2 > 0) ? 1 : 0);
+        FC_HIP(hipMemcpyAsync(a.active, ones.data(), sizeof(int32_t) * rcount, hipMemcpyHostToDevice, c.stream));
+        sync(c);   // `ones` is pageable host memory
+    }
+    // heavy rows: one entry per heavy vertex and bank per bucket
+    const bool hv = g.max_deg > DM;
+    a.heavy = ensure<int32_t>(c.heavy_list, (size_t)banks * (size_t)std::min<int64_t>(N, PN) + 8);
+    a.heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
+    FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
+    a.hslots = 1;
+    while (a.hslots < 2 * (int64_t)g.max_deg) a.hslots <<= 1;
+    a.hscratch = nullptr;
+    if (a.hslots > HSLOTS) a.hscratch = ensure<int32_t>(c.heavy_scratch, (size_t)HEAVY_GRID * 2 * a.hslots);
+
+    k_rl_init<<<nb(N * ldT, 256), 256, 0, c.stream>>>(N, ldT, g.kdeg.as<int64_t>(), a.lab, a.tot);
+
+    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // boff [B+1] | n_active copy
+    std::vector<int32_t> hb(B + 1);
+    const unsigned lgrid = nb(N, LTB * LPER);
+    const size_t lcount_lds = sizeof(unsigned long long) * 2 * banks + sizeof(int) * B;
+    int sweep = 0;
+    for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
+        const int listed = (c.prune && sweep > 0) ? 1 : 0;
+        FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * B, c.stream));
+        k_rl_list_count<<<lgrid, LTB, lcount_lds, c.stream>>>(a, sweep, listed, bcnt);
+        k_rl_list_plan<<<1, 64, 0, c.stream>>>(B, bcnt, a.boff, a.cursor);
+        FC_HIP(hipMemcpyAsync(hb.data(), a.boff, sizeof(int32_t) * (B + 1), hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hinfo, n_active, 4, hipMemcpyDeviceToHost, c.stream));
+        sync(c);
+        if (hb[B] == 0 || (sweep > 0 && hinfo[0] == 0)) break;   // every replica has stopped
+        k_rl_list_fill<<<lgrid, LTB, 2 * sizeof(int) * B, c.stream>>>(a, sweep);
+        for (int k = 0; k < B; ++k) {
+            const int64_t n = hb[k + 1] - hb[k];
+            if (n <= 0) continue;
+            const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
+            const unsigned grid = (unsigned)std::min<int64_t>(items, 8192);
+            const int ev = timer_begin(c);
+            if (louv) k_rl_decide<true><<<grid, RTB, 0, c.stream>>>(a, k, sweep);
+            else k_rl_decide<false><<<grid, RTB, 0, c.stream>>>(a, k, sweep);
+            timer_end(c, 4, ev);
+            if (hv) {
+                if (louv) k_rl_heavy<true><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, sweep);
+                else k_rl_heavy<false><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, sweep);
+            }
+            const unsigned agrid = (unsigned)std::min<int64_t>(items, 8192);
+            if (louv) k_rl_apply<true><<<agrid, RTB, 0, c.stream>>>(a, k);
+            else k_rl_apply<false><<<agrid, RTB, 0, c.stream>>>(a, k);
+        }
+        if (a.lm) {
+            const int64_t items = banks == 1 ? (N + VPW - 1) / VPW : N * banks;
+            k_rl_mark_lm<<<(unsigned)std::min<int64_t>(items, 8192), RTB, 0, c.stream>>>(a);
+        }
+        if (louv) k_rl_sweep_end<true><<<1, 256, 0, c.stream>>>(a, n_active);
+        else k_rl_sweep_end<false><<<1, 256, 0, c.stream>>>(a, n_active);
+        if (c.trace) {
+            sync(c);
+            static auto t_last = std::chrono::steady_clock::now();
+            const auto t_now = std::chrono::steady_clock::now();
+            int32_t st8[8];
+            FC_HIP(hipMemcpy(st8, n_active, sizeof(st8), hipMemcpyDeviceToHost));
+            fprintf(stderr, "[fc] rl it=%d sweep=%d entries=%d visits=%llu moves=%llu active=%d dt_us=%.0f\n", iteration,
+                    sweep, hb[B], *(unsigned long long*)(st8 + 6), *(unsigned long long*)(st8 + 2), st8[0],
+                    1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
+            t_last = t_now;
+        }
+    }
+    // labels for the consensus kernels (labT, native) and the slot-order rows everything else reads
+    int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
+    k_rl_export<<<dim3(nb(N, 64), (rcount + 63) / 64), 256, 0, c.stream>>>(N, rcount, ldT, a.lab, c.sinv.as<int32_t>(), lab);
+    c.ldT = ldT;
+    c.labT_valid = true;
+    // statistics: replica-sweeps, visits, and the decide kernel's algorithmic bytes
+    std::vector<unsigned long long> sa(4 * (size_t)rcount + 4);
+    FC_HIP(hipMemcpyAsync(sa.data(), a.sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    sync(c);
+    const unsigned long long rep_sweeps = sa[4 * (size_t)rcount + 2];
+    unsigned long long vis = 0, ent = 0, cand = 0, units = 0;
+    for (int r = 0; r < rcount; ++r) { vis += sa[4 * r]; ent += sa[4 * r + 1]; cand += sa[4 * r + 2]; units += sa[4 * r + 3]; }
+    if (c.trace)
+        fprintf(stderr, "[fc] rl it=%d done: %d sweeps, %.2f sweeps per replica, %llu visits in %llu units\n", iteration,
+                sweep, (double)rep_sweeps / rcount, vis, units);
+    // algorithmic bytes of the light decide kernel: per unit (vertex x bank) its record 16 B
+    // and row (col 4 B, weight 4 B unless unit) per entry -- read once for every replica of
+    // the unit; per visit (vertex x replica) its own label 4 + own total 4 + decision 4, the
+    // neighbour labels 4 B per entry, and per Sigma gathered 4 B (louvain)
+    const unsigned long long rowb = a.unitw ? 4 : 8;
+    const unsigned long long db = louv ? units * 16 + (ent / std::max<unsigned long long>(1, vis)) * units * rowb +
+                                             vis * 12 + ent * 4 + cand * 4
+                                       : units * 16 + (ent / std::max<unsigned long long>(1, vis)) * units * rowb +
+                                             vis * 8 + ent * 4;
+    for (fc_stats* s : {&c.acc, &c.prof}) {
+        s->cd_sweeps += (int64_t)rep_sweeps;
+        s->cd_vertex_visits += (int64_t)vis;
+        s->cd_edge_visits += (int64_t)ent;
+        s->decide_bytes += (int64_t)db;
+    }
+    timer_end(c, 0, sl0);
+}
+
+}  // namespace fc

@@ -110,6 +110,10 @@ struct Ctx {
     DevBuf nlab;                    // int32 [n_r][2m]: label of each adjacency entry's neighbour
     DevBuf aff, vlist, vcnt, track; // pruning: affected flags, per-sweep visit lists, list lengths, modes
     DevBuf mvf;                     // movers of a tracked sweep (prune_mark = 1 on weighted Louvain graphs)
+    // replica-lane engine (cd_rl.hip): per-entry replica masks, list-build scratch, affected /
+    // mover bits [banks][N]; labels and totals node-major in labT / tot ([N][ldT])
+    DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf;
+    int cd_engine = 1;              // FC_OPT_CD_ENGINE: 1 replica-lane (cd_rl.hip), 0 classic (cd.hip)
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable
@@ -177,6 +181,9 @@ void graph_merge_next(Ctx& c, int64_t n_added);
 void graph_copy(Ctx& c, Graph& dst, const Graph& src);
 // cd.cpp
 void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
+// cd_rl.hip: the replica-lane engine (louvain / lpm batches when cd_rl_supported)
+bool cd_rl_supported(const Ctx& c, int algo);
+void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
 void store_order(Ctx& c);             // Ctx::spos from a one-replica Louvain run (FC_OPT_STORE)
 void slot_maps(Ctx& c);               // Ctx::sinv / tpos / snpos from spos
 void graph_slots(Ctx& c, Graph& g);   // g.colp = spos[g.col]

@@ -889,9 +889,14 @@ static int tw_coarse(i64 N, i64 V, int B, int gmax) {
     return g;
 }
 
+/* shared: the replica-lane engine (cd_rl.hip) -- every replica visits the vertices in the SAME
+ * per-(iteration, sweep) order (its stream key uses TW_SHARED_RG in place of the replica
+ * index); tie keys stay per replica.  0: the classic engine's per-replica orders. */
+#define TW_SHARED_RG 0xffffffffu
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
                       u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
-                      int coarsen, int lm, i32* lab) {
+                      int coarsen, int lm, int shared, i32* lab) {
+    const uint32_t prg = shared ? TW_SHARED_RG : rg;   /* key of the visit order */
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
@@ -912,9 +917,9 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     int active = M2 > 0, sweep = 0;
     int track_now = 0, prune_now = 0;   /* adaptive pruning state (engine: k_sweep_end) */
     for (; sweep < max_sweeps && active; ++sweep) {
-        const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, rg, iter, (uint32_t)sweep, 1));
+        const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, prg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
-        const uint32_t off = tw_chunk_off(chunk, seed, rg, iter, (uint32_t)sweep);
+        const uint32_t off = tw_chunk_off(chunk, seed, prg, iter, (uint32_t)sweep);
         unsigned long long dq = 0, moves = 0, unstable = 0;
         const int listed = prune && sweep > 0;
         if (listed) {   /* all lists are built (and flags cleared) at the sweep start;
@@ -1021,7 +1026,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
  * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
 void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
                    int iteration, u64 seed, int buckets, int max_sweeps, int chunk, int prune, int coarsen,
-                   int prune_mark, i32* lab, int* sweeps) {
+                   int prune_mark, int shared, i32* lab, int* sweeps) {
     i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
     i64 M2 = 0;
     i32 max_w = 0;
@@ -1037,7 +1042,7 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
-                            buckets, max_sweeps, chunk, prune, coarsen, lm, lab + (i64)r * N);
+                            buckets, max_sweeps, chunk, prune, coarsen, lm, shared, lab + (i64)r * N);
         if (sweeps) sweeps[r] = sw;
     }
     free(kdeg);

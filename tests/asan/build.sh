@@ -15,5 +15,5 @@ done
 OBJ=$ROOT/fastconsensus_amd/lib/obj
 $HIPCC --offload-arch=gfx950 $SAN -g -o "$OUT/asan_driver" \
     -x c "$ROOT/tests/asan/asan_driver.c" -x none "$OUT/capi.cpp.o" "$OUT/gen.cpp.o" \
-    "$OBJ/graph.hip.o" "$OBJ/consensus.hip.o" "$OBJ/cd.hip.o" "$OBJ/leiden.hip.o"
+    "$OBJ/graph.hip.o" "$OBJ/consensus.hip.o" "$OBJ/cd.hip.o" "$OBJ/cd_rl.hip.o" "$OBJ/leiden.hip.o"
 echo "built $OUT/asan_driver"

@@ -12,14 +12,17 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1):
-        """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity."""
+    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=0, prune_mark=1, shared=1):
+        """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity.  Defaults:
+        the default CD engine (replica-lane, cd_rl.hip: shared visit order, no coarse rounds);
+        shared=0, coarsen=8 model the classic engine (FC_OPT_CD_ENGINE=0)."""
         self.seed = int(seed)
         self.buckets = buckets
         self.chunk = chunk
         self.prune = prune
         self.coarsen = coarsen
         self.prune_mark = prune_mark
+        self.shared = shared
         self.sigma = None if sigma is None else np.asarray(sigma, np.int32)
         self.lab = None
 
@@ -61,7 +64,7 @@ class OracleEngine:
         else:
             self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
                                         chunk=self.chunk, prune=self.prune, coarsen=self.coarsen,
-                                        prune_mark=self.prune_mark)
+                                        prune_mark=self.prune_mark, shared=self.shared)
         self.r0 = r0
 
     def consensus_partial(self, algo, out):

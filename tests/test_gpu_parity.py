@@ -156,29 +156,43 @@ def _lfr1k_graph():
 
 
 # tail: FC_OPT_TAIL_VISITS -- 0 keeps every sweep on the multi-kernel path; a huge value
-# hands every sweep after the first two to the per-replica tail kernel
+# hands every sweep after the first two to the per-replica tail kernel (classic engine)
 TAILS = [0, 1 << 40]
+# FC_OPT_CD_ENGINE: 1 replica-lane (default, cd_rl.hip; twin shared=1, coarsen=0), 0 classic (cd.hip)
+ENGINES = [1, 0]
 
 
+def _engine(eng, engine, tail=0, coarsen=0):
+    """Select the CD engine; returns the twin's keyword arguments.  The replica-lane engine has
+    no tail kernel or coarse rounds: its tail / coarsen variants are duplicates and skipped."""
+    if engine == 1:
+        if tail != TAILS[0] or coarsen != 0:
+            pytest.skip("replica-lane engine: no tail kernel / coarse rounds")
+        return {"shared": 1, "coarsen": 0}
+    eng.set_option("cd_engine", 0)
+    eng.set_option("tail_visits", tail)
+    eng.set_option("coarsen", coarsen)
+    return {"shared": 0, "coarsen": coarsen}
+
+
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("buckets,chunk,prune", [(32, 0, 0), (5, 0, 0), (32, 16, 0), (7, 16, 0), (32, 0, 1),
                                                  (5, 16, 1)])
-def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen):
+def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen, engine):
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=99)
+    kw = _engine(eng, engine, tail, coarsen)
     eng.set_params(buckets=buckets)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
-    eng.set_option("tail_visits", tail)
-    eng.set_option("coarsen", coarsen)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 4)
     got = eng.get_labels(n_r)
-    exp, sw = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune,
-                    coarsen=coarsen)
+    exp, sw = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 4, 99, buckets=buckets, chunk=chunk, prune=prune, **kw)
     np.testing.assert_array_equal(got, exp)
     # sharding invariance: replicas 2..4 alone give the same labelings
     eng.cd(algo, 2, 3, n_r, 4)
@@ -188,19 +202,37 @@ def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen)
     eng.close()
 
 
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("n_r", [1, 13, 33, 64, 70, 130])
+def test_cd_replica_lanes_bit_exact_vs_twin(fcmod, algo, n_r):
+    """Replica-lane engine at every lane layout: lane groups of 8 (up to 8 vertices per wave),
+    16, 64, and banks of 64 past 64 local replicas; a shard [r0, r0 + k) of a larger batch."""
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=41)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    eng.cd(algo, 0, n_r, n_r, 1)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 1, 41)
+    np.testing.assert_array_equal(eng.get_labels(n_r), exp)
+    if n_r > 2:
+        k = n_r // 2
+        eng.cd(algo, 1, k, n_r, 1)
+        np.testing.assert_array_equal(eng.get_labels(k), exp[1:1 + k])
+    eng.close()
+
+
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
-def test_cd_unit_prune_mark2_bit_exact_vs_twin(fcmod, algo, tail, coarsen):
+def test_cd_unit_prune_mark2_bit_exact_vs_twin(fcmod, algo, tail, coarsen, engine):
     """FC_OPT_PRUNE_MARK=2: the sweep-end marks (k_mark_lm) on the unit-weight input graph too."""
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=23)
+    kw = _engine(eng, engine, tail, coarsen)
     eng.set_option("prune_mark", 2)
-    eng.set_option("tail_visits", tail)
-    eng.set_option("coarsen", coarsen)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     eng.cd(algo, 0, 6, 6, 2)
-    exp, _ = _twin(eng, algo, case.N, case.edges_file, 6, 0, 2, 23, coarsen=coarsen, prune_mark=2)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, 6, 0, 2, 23, prune_mark=2, **kw)
     np.testing.assert_array_equal(eng.get_labels(6), exp)
     eng.close()
 
@@ -223,19 +255,20 @@ def _heavy_graph(seed, hub_deg):
     return N, e
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("hub_deg,chunk,prune", [(300, 0, 0), (3000, 0, 0), (3000, 16, 0), (3000, 0, 1)])
-def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune, tail):
+def test_cd_heavy_rows_bit_exact(fcmod, algo, hub_deg, chunk, prune, tail, engine):
     N, e = _heavy_graph(5, hub_deg)
     eng = fcmod.Engine(seed=7)
+    kw = _engine(eng, engine, tail)
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
-    eng.set_option("tail_visits", tail)
     eng.load_graph(N, e[:, 0], e[:, 1])
     eng.cd(algo, 0, 4, 4, 1)
     got = eng.get_labels(4)
-    exp, _ = _twin(eng, algo, N, e, 4, 0, 1, 7, chunk=chunk, prune=prune)
+    exp, _ = _twin(eng, algo, N, e, 4, 0, 1, 7, chunk=chunk, prune=prune, **kw)
     np.testing.assert_array_equal(got, exp)
     eng.close()
 
@@ -258,19 +291,19 @@ def _weighted_consensus_engine(fcmod, seed):
     return case, eng
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
 @pytest.mark.parametrize("prune_mark", [0, 1])
 @pytest.mark.parametrize("algo", [0, 1])
-def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, algo, prune_mark, tail, coarsen):
+def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, algo, prune_mark, tail, coarsen, engine):
     """CD (Louvain and LPA) on a weighted consensus graph, where FC_OPT_PRUNE_MARK=1 (default) tracks from sweep 1
     and marks at sweep end only the neighbours that ended in another community (k_mark_lm, and
-    the tail kernel's mover list): bit-exact against the twin in both modes, on the multi-kernel
-    path and the tail kernel, with and without coarse rounds."""
+    the tail kernel's mover list): bit-exact against the twin in both modes, on both engines, on
+    the multi-kernel path and the tail kernel, with and without coarse rounds."""
     case, eng = _weighted_consensus_engine(fcmod, 31)
+    kw = _engine(eng, engine, tail, coarsen)
     eng.set_option("prune_mark", prune_mark)
-    eng.set_option("tail_visits", tail)
-    eng.set_option("coarsen", coarsen)
     u, v, w, _ = eng.get_graph()
     assert w.max() > 1
     sigma = eng.node_map()
@@ -281,7 +314,7 @@ def test_cd_weighted_prune_mark_bit_exact_vs_twin(fcmod, algo, prune_mark, tail,
     n_r = 6
     eng.cd(algo, 0, n_r, n_r, 3)
     got = eng.get_labels(n_r)
-    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 31, coarsen=coarsen, prune_mark=prune_mark)
+    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 31, prune_mark=prune_mark, **kw)
     np.testing.assert_array_equal(got, exp[:, sigma])
     eng.close()
 
@@ -413,7 +446,8 @@ def test_closure_sampler_properties(fcmod):
                           (0, 20, 0.2, 0, 0, 1, 0), (0, 10, 0.2, 0, 1, 1, 16384), (1, 6, 0.8, 16, 1, 1, 0),
                           (1, 6, 0.8, 16, 1, 1, 16384), (0, 10, 0.2, 16, 1, 1, 0), (0, 10, 0.2, 16, 1, 1, 16384),
                           (2, 10, 0.2, 16, 1, 1, 16384), (2, 12, 0.2, 0, 0, 0, 0)])
-def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel, tail):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel, tail, engine):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
     loop (bucketed CD twin, consensus rule, Philox closure sampler, repair, ages): final
     partitions AND the final graph are identical (n_p=10 runs 9 iterations)."""
@@ -422,16 +456,20 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     case, _ = _lfr1k_graph()
     e = case.edges_file
     eng = fcmod.Engine(seed=17)
+    if engine == 0:
+        eng.set_option("cd_engine", 0)
+        eng.set_option("tail_visits", tail)
+    elif tail:
+        pytest.skip("replica-lane engine: no tail kernel")
     eng.set_option("chunk", chunk)
     eng.set_option("prune", prune)
     eng.set_option("relabel", relabel)
-    eng.set_option("tail_visits", tail)
     eng.set_params(max_iters=50)
     eng.load_graph(case.N, e[:, 0], e[:, 1])
     sigma = eng.node_map()
     if not relabel:
         assert np.array_equal(sigma, np.arange(case.N))
-    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune, sigma=sigma)
+    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune, sigma=sigma, shared=engine, coarsen=0 if engine else 8)
     cpu.load_graph(case.N, e[:, 0], e[:, 1])
     exp_labels, exp_st = run_sharded(cpu, algo, n_p, tau, 0.02, device="cpu", max_iters=50)
     labels, st = eng.run(algo, n_p, tau, 0.02)
