@@ -408,9 +408,14 @@ def main():
             traffic, traffic_note = load_traffic(args.config)
         else:
             traffic, traffic_note = None, "the PMC summary is for the config's n_p"
+        cd_engine = 1                          # FC_OPT_CD_ENGINE default (replica-lane)
+        for kv in args.opt:
+            if kv.split("=", 1)[0] == "cd_engine":
+                cd_engine = int(kv.split("=", 1)[1])
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
-                "kernel": "k_decide_light<%s>" % ("true" if algo != 1 else "false"),
+                "kernel": "%s<%s>" % ("k_rl_decide" if cd_engine == 1 and cfg["algo"] in ("louvain", "lpm")
+                                      else "k_decide_light", "true" if algo != 1 else "false"),
                 "note": (None if cfg["algo"] in ("louvain", "lpm") else
                          "the %s CD runs its own kernels (leiden.hip); this roofline covers the Louvain-engine "
                          "decide launches only" % cfg["algo"]),

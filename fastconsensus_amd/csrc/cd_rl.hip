@@ -54,6 +54,10 @@ constexpr int HTB = 256;
 constexpr int HEAVY_GRID = 256;
 constexpr int LTB = 256;                // list kernels
 constexpr int LPER = 8;                 // vertices per thread in the list kernels
+// Degree classes of a bucket's entries (the list is bucket-major, class-minor): rows of <= 16,
+// <= 32, <= DM entries are decided by sorting networks of that width, longer ones by k_rl_heavy.
+constexpr int NCLS = 4;
+__host__ __device__ __forceinline__ int rl_class(int d) { return d <= 16 ? 0 : d <= 32 ? 1 : d <= DM ? 2 : 3; }
 
 struct RL {
     int64_t N, S, PN;
@@ -61,6 +65,7 @@ struct RL {
     uint32_t perm_n;
     int B;
     int n_r, rbase, LG, VPW, banks, ldT;
+    int lgs;                     // log2(LG)
     uint32_t iter;
     uint64_t seed;
     const int64_t* rowptr;
@@ -70,14 +75,21 @@ struct RL {
     const int64_t* kdeg;
     int64_t M2;
     int unitw;
+    int wbits;                   // bits of the largest edge weight (key packing)
     int32_t* lab;                // labT [N][ldT]
     int32_t* tot;                // totT [N][ldT] (louvain)
     int32_t* dec;                // [PN][ldT]: target community or -1, per list entry and replica
-    int32_t* list;               // [PN] the sweep's vertices, bucket-major
+    int4* list;                  // [PN] the sweep's entries, bucket-major: vertex, row start, degree, k_v
+                                 // (the vertex record travels with the entry: no dependent vrec read)
     uint64_t* lmask;             // [PN][banks] visiting replicas of each entry
     uint64_t* vmask;             // [N][banks] list-build scratch
-    int32_t* boff;               // [B+1] bucket offsets | cursors [B] | heavy count
-    int32_t* cursor;
+    int32_t* boff;               // [B*NCLS+1] segment offsets (segment = bucket * NCLS + degree class)
+    int32_t* cursor;             // [B*NCLS] fill cursors
+    // visit mode (sparse sweeps): one lane per (entry, replica) visit instead of one wave per
+    // entry; visits of segment s are voff[s]..voff[s+1] in vlist (entry << 7 | local replica)
+    int32_t* voff;               // [B*NCLS+1]
+    int32_t* vcursor;            // [B*NCLS]
+    int64_t* vlist;
     uint64_t* aff;               // [banks][N] affected flags (pruning), one bit per replica
     uint64_t* mvf;               // [banks][N] movers of a tracked sweep (lm)
     int32_t* active;             // [n_r]
@@ -85,8 +97,6 @@ struct RL {
     int prune, lm, track_div;
     unsigned long long* red;     // [n_r][NSH][RF]
     unsigned long long* sacc;    // [n_r][4] visits / entries / cands / units over the run
-    int32_t* heavy;              // heavy units (entry * banks + bank) of the bucket
-    int32_t* heavy_cnt;
     int32_t* hscratch;           // global tables for rows past the LDS table
     int64_t hslots;
     double min_dq;
@@ -114,6 +124,11 @@ __device__ __forceinline__ bool rl_better(long long s1, uint32_t h1, int32_t c1,
     if (s1 != s2) return s1 > s2;
     if (h1 != h2) return h1 > h2;
     return c1 < c2;
+}
+// base[i] through a 32-bit byte offset (global_load saddr + voffset: one VGPR per address;
+// every node-major table here is < 4 GiB)
+__device__ __forceinline__ int32_t ld_off(const int32_t* base, uint32_t i) {
+    return *reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(base) + (i << 2));
 }
 __device__ __forceinline__ int wave_max(int x) {
 #pragma unroll
@@ -163,12 +178,13 @@ __global__ __launch_bounds__(256) void k_rl_export(int64_t N, int n_r, int ldT, 
 // lm the neighbours that ended in another community).  A listed sweep (prune, sweep > 0)
 // consumes the flags (oracle tw_replica clears them at the sweep start).  Dynamic LDS:
 // B ints + 2 * banks u64.
-__global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int listed, int32_t* bcnt) {
+__global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int listed, int32_t* bcnt, int32_t* vcnt) {
     extern __shared__ unsigned long long s_dyn[];
     uint64_t* s_act = (uint64_t*)s_dyn;
     uint64_t* s_flt = s_act + a.banks;
     int* s_b = (int*)(s_flt + a.banks);
-    for (int k = threadIdx.x; k < a.B; k += LTB) s_b[k] = 0;
+    int* s_v = s_b + a.B * NCLS;
+    for (int k = threadIdx.x; k < a.B * NCLS; k += LTB) { s_b[k] = 0; s_v[k] = 0; }
     for (int b = threadIdx.x; b < a.banks; b += LTB) { s_act[b] = 0; s_flt[b] = 0; }
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += LTB) {
@@ -183,31 +199,66 @@ __global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int list
     for (int i = 0; i < LPER; ++i) {
         const int64_t v = v0 + (int64_t)i * LTB;
         if (v >= a.N) break;
-        bool any = false;
+        int nv = 0;
         for (int b = 0; b < a.banks; ++b) {
             uint64_t f = a.aff[(int64_t)b * a.N + v];
             if (listed && f) a.aff[(int64_t)b * a.N + v] = 0;
             const uint64_t m = s_act[b] & (~s_flt[b] | f);
             a.vmask[v * a.banks + b] = m;
-            any |= m != 0;
+            nv += __popcll(m);
         }
-        if (any) atomicAdd(&s_b[rl_bucket(a, P, (uint32_t)v)], 1);
+        if (nv) {
+            const int sg = rl_bucket(a, P, (uint32_t)v) * NCLS + rl_class(a.vrec[v].y);
+            atomicAdd(&s_b[sg], 1);
+            atomicAdd(&s_v[sg], nv);
+        }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < a.B; k += LTB)
+    for (int k = threadIdx.x; k < a.B * NCLS; k += LTB) {
         if (s_b[k]) atomicAdd(&bcnt[k], s_b[k]);
+        if (s_v[k]) atomicAdd(&vcnt[k], s_v[k]);
+    }
 }
-__global__ void k_rl_list_plan(int B, const int32_t* bcnt, int32_t* boff, int32_t* cursor) {
+__global__ void k_rl_list_plan(int nseg, const int32_t* bcnt, int32_t* boff, int32_t* cursor, const int32_t* vcnt,
+                               int32_t* voff, int32_t* vcursor) {
     if (threadIdx.x != 0) return;
-    int32_t acc = 0;
-    for (int k = 0; k < B; ++k) { boff[k] = acc; cursor[k] = acc; acc += bcnt[k]; }
-    boff[B] = acc;
+    int32_t acc = 0, vacc = 0;
+    for (int k = 0; k < nseg; ++k) {
+        boff[k] = acc; cursor[k] = acc; acc += bcnt[k];
+        voff[k] = vacc; vcursor[k] = vacc; vacc += vcnt[k];
+    }
+    boff[nseg] = acc;
+    voff[nseg] = vacc;
 }
+// Visit mode: each listed entry's replicas as (entry, replica) pairs.  The entries are
+// segment-major, so an exclusive scan of the per-entry visit counts lays the visits out
+// segment-major too (segment s starts at the scan value of its first entry, = voff[s]).
+__global__ __launch_bounds__(LTB) void k_rl_visits_count(RL a, int64_t n_entries, int32_t* nv) {
+    const int64_t e = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    if (e >= n_entries) return;
+    int c = 0;
+    for (int b = 0; b < a.banks; ++b) c += __popcll(a.lmask[e * a.banks + b]);
+    nv[e] = c;
+}
+__global__ __launch_bounds__(LTB) void k_rl_visits_fill(RL a, int64_t n_entries, const int32_t* vpos) {
+    const int64_t e = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    if (e >= n_entries) return;
+    int64_t pos = vpos[e];
+    for (int b = 0; b < a.banks; ++b) {
+        uint64_t m = a.lmask[e * a.banks + b];
+        while (m) {
+            const int bit = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            a.vlist[pos++] = (e << 14) | (int64_t)(b * 64 + bit);
+        }
+    }
+}
+
 __global__ __launch_bounds__(LTB) void k_rl_list_fill(RL a, int sweep) {
     extern __shared__ int s_lb[];
     int* s_cnt = s_lb;
-    int* s_base = s_lb + a.B;
-    for (int k = threadIdx.x; k < a.B; k += LTB) s_cnt[k] = 0;
+    int* s_base = s_lb + a.B * NCLS;
+    for (int k = threadIdx.x; k < a.B * NCLS; k += LTB) s_cnt[k] = 0;
     __syncthreads();
     const Perm P = rl_perm(a, sweep);
     int bk[LPER], loc[LPER];
@@ -220,18 +271,19 @@ __global__ __launch_bounds__(LTB) void k_rl_list_fill(RL a, int sweep) {
         bool any = false;
         for (int b = 0; b < a.banks; ++b) any |= a.vmask[v * a.banks + b] != 0;
         if (!any) continue;
-        bk[i] = (int)rl_bucket(a, P, (uint32_t)v);
+        bk[i] = (int)rl_bucket(a, P, (uint32_t)v) * NCLS + rl_class(a.vrec[v].y);
         loc[i] = atomicAdd(&s_cnt[bk[i]], 1);
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < a.B; k += LTB) s_base[k] = s_cnt[k] ? atomicAdd(&a.cursor[k], s_cnt[k]) : 0;
+    for (int k = threadIdx.x; k < a.B * NCLS; k += LTB) s_base[k] = s_cnt[k] ? atomicAdd(&a.cursor[k], s_cnt[k]) : 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < LPER; ++i) {
         if (bk[i] < 0) continue;
         const int64_t v = v0 + (int64_t)i * LTB;
         const int64_t e = s_base[bk[i]] + loc[i];
-        a.list[e] = (int32_t)v;
+        const int4 vr = a.vrec[v];
+        a.list[e] = make_int4((int32_t)v, vr.x, vr.y, vr.z);
         for (int b = 0; b < a.banks; ++b) a.lmask[e * a.banks + b] = a.vmask[v * a.banks + b];
     }
 }
@@ -247,9 +299,9 @@ struct Unit {
 __device__ __forceinline__ Unit rl_unit(const RL& a, int64_t e0, int64_t e1, int64_t w) {
     Unit u;
     const int lane = threadIdx.x & 63;
-    u.s = lane / a.LG;
-    u.rl = lane - u.s * a.LG;
-    if (a.banks == 1) { u.e = e0 + w * a.VPW + u.s; u.bank = 0; }
+    u.s = lane >> a.lgs;
+    u.rl = lane & (a.LG - 1);
+    if (a.banks == 1) { u.e = e0 + (w << (6 - a.lgs)) + u.s; u.bank = 0; }
     else { u.e = e0 + w / a.banks; u.bank = (int)(w % a.banks); }
     u.r = u.bank * 64 + u.rl;
     u.valid = u.e < e1 && u.s < a.VPW;
@@ -260,17 +312,351 @@ __device__ __forceinline__ int64_t rl_items(const RL& a, int64_t n) {
 }
 
 // ------------------------------------------------------------------ decide (light rows)
+// Per unit the lanes' header: the entry's vertex, the lane's replica bit, the row.  Rows
+// longer than DM are listed for k_rl_heavy (one entry per unit, by the sub-group's lane 0).
+struct Hdr {
+    int32_t v;
+    uint64_t msk;
+    int64_t rb;
+    int d, kvi, ds, rr;
+    bool on, heavy, work;
+};
+// The entry record and replica mask of a unit (prefetched one item ahead by the decide kernel).
+struct Rec {
+    int4 e;
+    uint64_t msk;
+};
+__device__ __forceinline__ Rec rl_fetch(const RL& a, const Unit& u) {
+    Rec r;
+    r.e = make_int4(-1, 0, 0, 0);
+    r.msk = 0;
+    if (u.valid) {
+        r.e = a.list[u.e];
+        r.msk = a.lmask[u.e * a.banks + u.bank];
+    }
+    return r;
+}
+__device__ __forceinline__ Hdr rl_header(const RL& a, const Unit& u, const Rec& rec) {
+    Hdr h;
+    h.rr = u.bank * 64 + u.rl;
+    h.v = rec.e.x;
+    h.msk = rec.msk;
+    h.rb = (int64_t)(uint32_t)rec.e.y;
+    h.d = rec.e.z;
+    h.kvi = rec.e.w;
+    h.on = u.valid && h.rr < a.n_r && ((h.msk >> u.rl) & 1ull);
+    h.heavy = u.valid && h.d > DM;
+    h.work = h.on && !h.heavy && h.d > 0;
+    h.ds = (u.valid && !h.heavy && h.msk) ? h.d : 0;
+    return h;
+}
+
+// Bitonic sort of K keys held in registers (compile-time indices: 2 VALU per compare-exchange).
+template <int K>
+__device__ __forceinline__ void bitonic_sort(int32_t (&x)[K]) {
+#pragma unroll
+    for (int k = 2; k <= K; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const int32_t p = x[i], q = x[l];
+                    if ((i & k) == 0) { x[i] = min(p, q); x[l] = max(p, q); }
+                    else { x[i] = max(p, q); x[l] = min(p, q); }
+                }
+            }
+}
+
+// One lane's decision from its row (K >= the wave's longest light row).  Keys are
+// (label << wb) | weight (wb = 0 on unit graphs), -1 for empty and (louvain) own-community
+// entries; sorted, a run of equal labels is one neighbour community with its summed weight.
+// Pass A: the largest weight vm (louvain: foreign communities only; LPA: own included).
+// Pass B: the runs of weight vm are the candidates; their Sigma is gathered (16 positions per
+// batch, batches without a candidate skipped wave-wide) and the best score wins (score =
+// vm*2M - k_v*Sigma, ties by the replica's hash, then the smaller id).  A lighter run scores
+// <= (vm - 1)*2M: only when that still reaches the best are the lighter runs evaluated (rare).
+// A lighter neighbour community may still reach the best score (k_v * Sigma_min >= 2M, rare):
+// the lane re-evaluates every community of weight < vm from its row in global memory (O(d^2)
+// reads, cached), so the sorted keys need not stay live for it.
+__device__ __forceinline__ void rl_slow(const RL& a, const Hdr& h, int32_t own, int vm, uint32_t tvh,
+                                                  long long& best_s, uint32_t& best_h, int32_t& best_c,
+                                                  unsigned long long& c_cand, bool slow) {
+    if (!slow) return;
+    const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
+    const long long kv = h.kvi;
+    for (int j1 = 0; j1 < h.d; ++j1) {
+        const int32_t c1 = ld_off(a.lab, (uint32_t)a.col[h.rb + j1] * ldT + rr);
+        if (c1 == own) continue;
+        bool dup = false;
+        for (int j2 = 0; j2 < j1 && !dup; ++j2) dup = ld_off(a.lab, (uint32_t)a.col[h.rb + j2] * ldT + rr) == c1;
+        if (dup) continue;
+        long long val = 0;
+        for (int j2 = j1; j2 < h.d; ++j2)
+            if (ld_off(a.lab, (uint32_t)a.col[h.rb + j2] * ldT + rr) == c1) val += a.unitw ? 1 : a.cw[h.rb + j2];
+        if (val >= vm || val * a.M2 < best_s) continue;         // weight vm: evaluated already
+        const long long sc = val * a.M2 - kv * (long long)ld_off(a.tot, (uint32_t)c1 * ldT + rr);
+        const uint32_t hh = hash32(tvh ^ (uint32_t)c1);
+        ++c_cand;
+        if (rl_better(sc, hh, c1, best_s, best_h, best_c)) { best_s = sc; best_h = hh; best_c = c1; }
+    }
+}
+
+template <bool LOUV, int K, bool UNITW>
+__device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
+                                             unsigned long long& c_unst, unsigned long long& c_cand) {
+    const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
+    const int wb = UNITW ? 0 : a.wbits;
+    const int32_t wm = (1 << wb) - 1;
+    const bool wk = h.work;
+    // padding / idle lanes read a slot of their own vertex's row (cached, distinct per wave)
+    // instead of branching; never a shared row, which every wave would hit on one L2 channel
+    const uint32_t home = (h.v >= 0 ? (uint32_t)h.v : 0u) * ldT + rr;
+    const int32_t own0 = ld_off(a.lab, home);
+    const int32_t own = wk ? own0 : -1;
+    // entry j of the lane's row is live iff j < dsw: the selects below test that, not the
+    // loaded values, so a neighbour id is dead once its label load is issued (one register
+    // per entry)
+    const int dsw = wk ? h.ds : 0;
+    int32_t x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)                                 // idle / padding lanes read col[rb] (a hit)
+        x[j] = ld_off(a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
+    int32_t tot_own = 0;
+    if (LOUV) {
+        const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
+        tot_own = wk ? t0 : 0;
+    }
+    long long kown = 0;
+    if constexpr (UNITW) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)x[j] * ldT + rr : home);
+            x[j] = j < dsw ? lj : -1;
+        }
+        if (LOUV) {
+            int ko = 0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const bool mine = x[j] == own && x[j] >= 0;
+                ko += mine ? 1 : 0;
+                x[j] = mine ? -1 : x[j];
+            }
+            kown = ko;
+        }
+    } else {
+        int32_t wv[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t wj = ld_off(a.cw, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
+            wv[j] = j < dsw ? wj : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)x[j] * ldT + rr : home);
+            x[j] = j < dsw ? lj : -1;
+        }
+        int ko = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const bool mine = LOUV && x[j] == own && x[j] >= 0;
+            ko += mine ? wv[j] : 0;
+            x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wv[j]);
+        }
+        kown = ko;
+    }
+    bitonic_sort<K>(x);
+    // run ends and summed weights: e = bit q set when the run of equal labels ends at q
+    // pass A: the largest weight vm
+    int vm = INT_MIN;
+    {
+        int acc = 0;
+        int32_t kl = (int32_t)kown;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const int32_t l = x[q] >> wb;
+            const int w = UNITW ? 1 : (x[q] & wm);
+            acc = (q > 0 && l == (x[q - 1] >> wb)) ? acc + w : w;
+            const bool end = x[q] >= 0 && (q == K - 1 || (x[q + 1] >> wb) != l);
+            vm = end ? max(vm, acc) : vm;
+            if (!LOUV) kl = (end && l == own) ? acc : kl;
+        }
+        if (!LOUV) kown = kl;
+    }
+    // pass B: candidate runs (the runs of weight vm), as bits of cm
+    uint32_t cm_lo = 0, cm_hi = 0;
+    {
+        int acc = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const int32_t l = x[q] >> wb;
+            const int w = UNITW ? 1 : (x[q] & wm);
+            acc = (q > 0 && l == (x[q - 1] >> wb)) ? acc + w : w;
+            const bool cand = x[q] >= 0 && (q == K - 1 || (x[q + 1] >> wb) != l) && acc == vm;
+            if (q < 32) cm_lo |= (uint32_t)cand << (q & 31);
+            else cm_hi |= (uint32_t)cand << (q & 31);
+        }
+    }
+    const int ncand = __popc(cm_lo) + __popc(cm_hi);
+    if (wk) c_cand += (unsigned long long)ncand;
+    const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + h.rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)h.v);
+    int32_t dcs = -1;
+    if (LOUV) {
+        const long long kv = h.kvi;
+        // among the candidates (all of weight vm) score = vm*2M - k_v*Sigma: the best is the
+        // smallest Sigma (every Sigma taken as 0 when k_v = 0), then the largest hash -- one
+        // unsigned 64-bit minimum of (Sigma << 32) | ~hash; the hash is a bijection of the id
+        // (no id tie is left), inverted for the winner
+        uint64_t bkey = ~0ull;
+#pragma unroll
+        for (int c0 = 0; c0 < K; c0 += 16) {
+            const uint32_t bits = ((c0 < 32 ? cm_lo : cm_hi) >> (c0 & 31)) & 0xffffu;
+            if (__ballot(bits != 0) == 0) continue;             // wave-uniform
+            int32_t tq[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {                     // non-candidates read the lane's own slot (a hit)
+                const bool b = (bits >> i) & 1u;
+                tq[i] = ld_off(a.tot, b ? (uint32_t)(x[c0 + i] >> wb) * ldT + rr : home);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bool b = (bits >> i) & 1u;
+                const uint32_t hh = hash32(tvh ^ (uint32_t)(x[c0 + i] >> wb));
+                const uint64_t key = ((uint64_t)(kv ? (uint32_t)tq[i] : 0u) << 32) | (uint32_t)~hh;
+                bkey = (b && key < bkey) ? key : bkey;
+            }
+        }
+        long long best_s = LLONG_MIN;
+        uint32_t best_h = 0;
+        int32_t best_c = INT_MAX;
+        if (ncand != 0) {
+            best_h = ~(uint32_t)bkey;
+            best_c = (int32_t)(hash32_inv(best_h) ^ tvh);
+            best_s = (long long)vm * a.M2 - kv * (long long)(uint32_t)(bkey >> 32);
+        }
+        const bool slow = ncand != 0 && (long long)(vm - 1) * a.M2 >= best_s;
+        if (__ballot(slow)) rl_slow(a, h, own, vm, tvh, best_s, best_h, best_c, c_cand, slow);   // wave-uniform, rare
+        if (wk && ncand != 0) {
+            const long long G = best_s - kown * a.M2 + kv * ((long long)tot_own - kv);
+            if (G > 0) {
+                const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+                c_dq += (unsigned long long)llrint(dqd * DQ_SCALE);
+                dcs = best_c;
+            }
+        }
+    } else {
+        uint32_t best_h = 0;
+        int32_t best_c = -1;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const bool b = ((q < 32 ? cm_lo : cm_hi) >> (q & 31)) & 1u;
+            const uint32_t hh = hash32(tvh ^ (uint32_t)x[q]);
+            const bool take = b && (best_c < 0 || hh > best_h);
+            best_h = take ? hh : best_h;
+            best_c = take ? x[q] : best_c;
+        }
+        if (wk && ncand != 0) {
+            c_unst += (kown != (long long)vm) ? 1 : 0;
+            dcs = best_c != own ? best_c : -1;
+        }
+    }
+    return dcs;
+}
+
+// Light rows with sortable keys (label and weight fit 31 bits): no LDS, one sorting network
+// per lane, K chosen per wave from its longest row.
+template <bool LOUV, int K, bool UNITW>
+__global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int seg, int sweep) {
+    const int lane = threadIdx.x & 63;
+    const int64_t e0 = a.boff[seg], e1 = a.boff[seg + 1];
+    const int64_t items = rl_items(a, e1 - e0);
+    const int LG = a.LG;
+    unsigned long long c_dq = 0, c_unst = 0, c_vis = 0, c_ent = 0, c_cand = 0, c_units = 0;
+    int last_r = -1;
+    auto flush = [&](int r) {
+        if (r < 0) return;
+        for (int off = LG; off < 64; off <<= 1) {
+            c_dq += __shfl_xor(c_dq, off); c_unst += __shfl_xor(c_unst, off); c_vis += __shfl_xor(c_vis, off);
+            c_ent += __shfl_xor(c_ent, off); c_cand += __shfl_xor(c_cand, off); c_units += __shfl_xor(c_units, off);
+        }
+        if (lane < LG && r < a.n_r) {
+            if (c_dq) atomicAdd(rl_red(a, r, 0), c_dq);
+            if (c_unst) atomicAdd(rl_red(a, r, 1), c_unst);
+            if (c_vis) atomicAdd(rl_red(a, r, 3), c_vis);
+            if (c_ent) atomicAdd(rl_red(a, r, 4), c_ent);
+            if (c_cand) atomicAdd(rl_red(a, r, 5), c_cand);
+            if (c_units) atomicAdd(rl_red(a, r, 6), c_units);
+        }
+        c_dq = c_unst = c_vis = c_ent = c_cand = c_units = 0;
+    };
+    Rec nxt = rl_fetch(a, rl_unit(a, e0, e1, blockIdx.x));
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        const Unit u = rl_unit(a, e0, e1, w);
+        if (a.banks > 1 && u.r != last_r) flush(last_r);
+        last_r = a.banks > 1 ? u.r : (lane & (LG - 1));
+        const Rec cur = nxt;
+        nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
+        const Hdr h = rl_header(a, u, cur);
+        const int32_t dcs = rl_sorted<LOUV, K, UNITW>(a, h, sweep, c_dq, c_unst, c_cand);
+        if (h.work) { c_vis += 1; c_ent += (unsigned long long)h.d; }
+        if (u.valid && u.rl == 0 && h.msk) c_units += 1;
+        if (u.valid && h.rr < a.n_r) a.dec[u.e * a.ldT + h.rr] = h.work ? dcs : -1;
+    }
+    flush(last_r);
+}
+
+// Visit mode: lane = one (entry, replica) visit -- rows are per lane (no sharing), for the
+// sparse sweeps where most replicas of an entry are idle and a wave per entry would run mostly
+// empty lanes.  Same decision code; counters go straight to the per-replica shards.
+template <bool LOUV, int K, bool UNITW>
+__global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
+    const int64_t v0 = a.voff[seg], v1 = a.voff[seg + 1];
+    for (int64_t base = (int64_t)blockIdx.x * 64; base < v1 - v0; base += (int64_t)gridDim.x * 64) {
+        const int64_t i = base + (threadIdx.x & 63);
+        const bool valid = i < v1 - v0;
+        int64_t vp = 0;
+        if (valid) vp = a.vlist[v0 + i];
+        const int64_t e = vp >> 14;
+        Hdr h;
+        h.rr = (int)(vp & 16383);
+        const int4 er = valid ? a.list[e] : make_int4(-1, 0, 0, 0);
+        h.v = er.x;
+        h.rb = (int64_t)(uint32_t)er.y;
+        h.d = er.z;
+        h.kvi = er.w;
+        h.msk = 0;
+        h.on = valid;
+        h.heavy = false;
+        h.work = valid && h.d > 0;
+        h.ds = valid ? h.d : 0;
+        unsigned long long c_dq = 0, c_unst = 0, c_cand = 0;
+        const int32_t dcs = rl_sorted<LOUV, K, UNITW>(a, h, sweep, c_dq, c_unst, c_cand);
+        if (valid) {
+            a.dec[e * a.ldT + h.rr] = h.work ? dcs : -1;
+            if (c_dq) atomicAdd(rl_red(a, h.rr, 0), c_dq);
+            if (c_unst) atomicAdd(rl_red(a, h.rr, 1), c_unst);
+            if (h.work) {
+                atomicAdd(rl_red(a, h.rr, 3), 1ull);
+                atomicAdd(rl_red(a, h.rr, 4), (unsigned long long)h.d);
+            }
+            if (c_cand) atomicAdd(rl_red(a, h.rr, 5), c_cand);
+        }
+    }
+}
+
+// Fallback for keys that do not pack into 31 bits (huge graphs or weights): the row's labels
+// staged in LDS as L[j][lane], equal labels merged per lane by a triangular scan.
 struct RLShared {
     int32_t L[DM][64];           // row labels per lane; merged / own entries DONE; then the candidates
     int32_t C[VPWMAX][DM];       // the sub-groups' rows (neighbour ids)
     int32_t W[VPWMAX][DM];       // their weights (weighted graphs)
 };
-
 template <bool LOUV>
-__global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int k, int sweep) {
+__global__ __launch_bounds__(RTB) void k_rl_decide_lds(RL a, int k, int sweep) {
     __shared__ RLShared sh;
     const int lane = threadIdx.x & 63;
-    const int64_t e0 = a.boff[k], e1 = a.boff[k + 1];
+    const int64_t e0 = a.boff[k * NCLS], e1 = a.boff[k * NCLS + NCLS - 1];   // the light classes
     const int64_t items = rl_items(a, e1 - e0);
     const int LG = a.LG, VPW = a.VPW;
     // per-lane counters, flushed once per wave
@@ -296,25 +682,20 @@ __global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int k, int sweep) {
     for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
         const Unit u = rl_unit(a, e0, e1, w);
         if (a.banks > 1 && u.r != last_r) { flush(last_r); }
-        last_r = a.banks > 1 ? u.r : lane % LG;
+        last_r = a.banks > 1 ? u.r : (lane & (LG - 1));
         const int rr = u.bank * 64 + u.rl;                      // local replica of this lane
         int32_t v = -1;
         uint64_t msk = 0;
+        int4 er = make_int4(-1, 0, 0, 0);
         if (u.valid) {
-            v = a.list[u.e];
+            er = a.list[u.e];
+            v = er.x;
             msk = a.lmask[u.e * a.banks + u.bank];
         }
         const bool on = u.valid && rr < a.n_r && ((msk >> u.rl) & 1ull);
-        int64_t rb = 0;
-        int d = 0, kvi = 0;
-        if (u.valid) {
-            const int4 vr = a.vrec[v];
-            rb = (int64_t)(uint32_t)vr.x;
-            d = vr.y;
-            kvi = vr.z;
-        }
+        const int64_t rb = (int64_t)(uint32_t)er.y;
+        const int d = er.z, kvi = er.w;
         const bool heavy = u.valid && d > DM;
-        if (heavy && u.rl == 0 && msk) a.heavy[atomicAdd(a.heavy_cnt, 1)] = (int32_t)(u.e * a.banks + u.bank);
         const bool work = on && !heavy && d > 0;
         const int ds = (u.valid && !heavy && msk) ? d : 0;     // the sub-group's staged row length
         const int64_t lrow = (int64_t)v * a.ldT + rr;
@@ -482,17 +863,17 @@ __global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int k, int sweep) {
 
 // ------------------------------------------------------------------ decide (heavy rows)
 template <bool LOUV>
-__global__ __launch_bounds__(HTB) void k_rl_heavy(RL a, int sweep) {
+__global__ __launch_bounds__(HTB) void k_rl_heavy(RL a, int k, int sweep) {
     __shared__ int32_t key[HSLOTS], val[HSLOTS];
     __shared__ long long s_s[HTB], s_k[HTB];
     __shared__ uint32_t s_h[HTB];
     __shared__ int32_t s_c[HTB];
-    const int cnt = *a.heavy_cnt;
-    for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
-        const int32_t unit = a.heavy[item];
-        const int64_t e = unit / a.banks;
-        const int bank = unit % a.banks;
-        const int32_t v = a.list[e];
+    const int64_t h0 = a.boff[k * NCLS + NCLS - 1], h1 = a.boff[k * NCLS + NCLS];   // the heavy class
+    const int64_t cnt = (h1 - h0) * a.banks;
+    for (int64_t item = blockIdx.x; item < cnt; item += gridDim.x) {
+        const int64_t e = h0 + item / a.banks;
+        const int bank = (int)(item % a.banks);
+        const int32_t v = a.list[e].x;
         const uint64_t msk = a.lmask[e * a.banks + bank];
         const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
         uint32_t slots = 1;
@@ -589,9 +970,8 @@ __global__ __launch_bounds__(HTB) void k_rl_heavy(RL a, int sweep) {
 // or, with lm, the movers listed for k_rl_mark_lm.
 template <bool LOUV>
 __global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.heavy_cnt = 0;   // the bucket's heavy list is consumed
     const int lane = threadIdx.x & 63;
-    const int64_t e0 = a.boff[k], e1 = a.boff[k + 1];
+    const int64_t e0 = a.boff[k * NCLS], e1 = a.boff[k * NCLS + NCLS];
     const int64_t items = rl_items(a, e1 - e0);
     const int LG = a.LG;
     unsigned long long moves = 0;
@@ -606,12 +986,16 @@ __global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
     for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
         const Unit u = rl_unit(a, e0, e1, w);
         if (a.banks > 1 && u.r != last_r) flush(last_r);
-        last_r = a.banks > 1 ? u.r : lane % LG;
+        last_r = a.banks > 1 ? u.r : (lane & (LG - 1));
         const int rr = u.r;
-        int32_t t = -1, v = -1;
+        int32_t t = -1, v = -1, kvr = 0;
+        int4 er = make_int4(-1, 0, 0, 0);
         if (u.valid) {
-            v = a.list[u.e];
-            if (rr < a.n_r) t = a.dec[u.e * a.ldT + rr];
+            er = a.list[u.e];
+            v = er.x;
+            kvr = er.w;
+            const uint64_t msk = a.lmask[u.e * a.banks + u.bank];
+            if (rr < a.n_r && ((msk >> u.rl) & 1ull)) t = a.dec[u.e * a.ldT + rr];
         }
         const bool moved = t >= 0;
         if (moved) {
@@ -619,9 +1003,8 @@ __global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
             const int32_t old = a.lab[lrow];
             a.lab[lrow] = t;
             if (LOUV) {
-                const int32_t kv = a.vrec[v].z;
-                atomicAdd(&a.tot[(int64_t)old * a.ldT + rr], -kv);
-                atomicAdd(&a.tot[(int64_t)t * a.ldT + rr], kv);
+                atomicAdd(&a.tot[(int64_t)old * a.ldT + rr], -kvr);
+                atomicAdd(&a.tot[(int64_t)t * a.ldT + rr], kvr);
             }
             ++moves;
         }
@@ -632,9 +1015,8 @@ __global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
         if (a.lm) {
             if (u.valid && u.rl == 0 && ms) a.mvf[(int64_t)u.bank * a.N + v] = ms;
         } else if (u.valid && ms) {
-            const int4 vr = a.vrec[v];
-            const int64_t rb = (int64_t)(uint32_t)vr.x;
-            for (int j = u.rl; j < vr.y; j += LG)
+            const int64_t rb = (int64_t)(uint32_t)er.y;
+            for (int j = u.rl; j < er.z; j += LG)
                 atomicOr((unsigned long long*)&a.aff[(int64_t)u.bank * a.N + a.col[rb + j]], (unsigned long long)ms);
         }
     }
@@ -762,20 +1144,31 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     RL a;
     a.N = N; a.S = S; a.PN = PN; a.chunk = CH; a.perm_n = (uint32_t)NC; a.B = B;
     a.n_r = rcount; a.rbase = rbegin; a.LG = LG; a.VPW = VPW; a.banks = banks; a.ldT = ldT;
+    a.lgs = 0;
+    while ((1 << a.lgs) < LG) ++a.lgs;
     a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
     a.vrec = g.vrec.as<int4>(); a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;
     a.unitw = (!louv || (g.max_w == 1 && g.M2 == 2 * g.m)) ? 1 : 0;
+    a.wbits = 0;
+    while (a.wbits < 31 && ((int64_t)g.max_w >> a.wbits) != 0) ++a.wbits;
+    // sortable keys (label << wbits | weight) need N << wbits < 2^31; else the LDS merge
+    const bool pack = ((int64_t)(N - 1) << (a.unitw ? 0 : a.wbits)) < (int64_t(1) << 31);
     a.lab = ensure<int32_t>(c.labT, (size_t)N * ldT);
     a.tot = louv ? ensure<int32_t>(c.tot, (size_t)N * ldT) : nullptr;
     a.dec = ensure<int32_t>(c.dec, (size_t)PN * ldT);
-    a.list = ensure<int32_t>(c.vlist, (size_t)PN);
+    a.list = (int4*)ensure<int4>(c.vlist, (size_t)PN);
     a.lmask = (uint64_t*)ensure<uint64_t>(c.rl_lmask, (size_t)PN * banks);
     a.vmask = (uint64_t*)ensure<uint64_t>(c.rl_vmask, (size_t)N * banks);
-    int32_t* plan = ensure<int32_t>(c.vcnt, 3 * (size_t)B + 8);
+    const int nseg = B * NCLS;
+    int32_t* plan = ensure<int32_t>(c.vcnt, 6 * (size_t)nseg + 16);
     int32_t* bcnt = plan;
-    a.boff = bcnt + B;
-    a.cursor = a.boff + B + 1;
+    a.boff = bcnt + nseg;
+    a.cursor = a.boff + nseg + 1;
+    int32_t* vcnt = a.cursor + nseg;
+    a.voff = vcnt + nseg;
+    a.vcursor = a.voff + nseg + 1;
+    a.vlist = nullptr;
     a.aff = (uint64_t*)ensure<uint64_t>(c.rl_aff, (size_t)banks * N);
     a.mvf = (uint64_t*)ensure<uint64_t>(c.rl_mvf, (size_t)banks * N);
     FC_HIP(hipMemsetAsync(a.aff, 0, 8 * (size_t)banks * N, c.stream));
@@ -800,11 +1193,6 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         FC_HIP(hipMemcpyAsync(a.active, ones.data(), sizeof(int32_t) * rcount, hipMemcpyHostToDevice, c.stream));
         sync(c);   // `ones` is pageable host memory
     }
-    // heavy rows: one entry per heavy vertex and bank per bucket
-    const bool hv = g.max_deg > DM;
-    a.heavy = ensure<int32_t>(c.heavy_list, (size_t)banks * (size_t)std::min<int64_t>(N, PN) + 8);
-    a.heavy_cnt = ensure<int32_t>(c.heavy_cnt, 4);
-    FC_HIP(hipMemsetAsync(a.heavy_cnt, 0, sizeof(int32_t), c.stream));
     a.hslots = 1;
     while (a.hslots < 2 * (int64_t)g.max_deg) a.hslots <<= 1;
     a.hscratch = nullptr;
@@ -813,36 +1201,86 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     k_rl_init<<<nb(N * ldT, 256), 256, 0, c.stream>>>(N, ldT, g.kdeg.as<int64_t>(), a.lab, a.tot);
 
     int32_t* hinfo = (int32_t*)(c.hpin + 8);   // boff [B+1] | n_active copy
-    std::vector<int32_t> hb(B + 1);
+    std::vector<int32_t> hb(2 * (nseg + 1));   // boff | voff
     const unsigned lgrid = nb(N, LTB * LPER);
-    const size_t lcount_lds = sizeof(unsigned long long) * 2 * banks + sizeof(int) * B;
+    const size_t lcount_lds = sizeof(unsigned long long) * 2 * banks + 2 * sizeof(int) * nseg;
     int sweep = 0;
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         const int listed = (c.prune && sweep > 0) ? 1 : 0;
-        FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * B, c.stream));
-        k_rl_list_count<<<lgrid, LTB, lcount_lds, c.stream>>>(a, sweep, listed, bcnt);
-        k_rl_list_plan<<<1, 64, 0, c.stream>>>(B, bcnt, a.boff, a.cursor);
-        FC_HIP(hipMemcpyAsync(hb.data(), a.boff, sizeof(int32_t) * (B + 1), hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * nseg, c.stream));
+        FC_HIP(hipMemsetAsync(vcnt, 0, sizeof(int32_t) * nseg, c.stream));
+        k_rl_list_count<<<lgrid, LTB, lcount_lds, c.stream>>>(a, sweep, listed, bcnt, vcnt);
+        k_rl_list_plan<<<1, 64, 0, c.stream>>>(nseg, bcnt, a.boff, a.cursor, vcnt, a.voff, a.vcursor);
+        FC_HIP(hipMemcpyAsync(hb.data(), a.boff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hb.data() + nseg + 1, a.voff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost,
+                              c.stream));
         FC_HIP(hipMemcpyAsync(hinfo, n_active, 4, hipMemcpyDeviceToHost, c.stream));
         sync(c);
-        if (hb[B] == 0 || (sweep > 0 && hinfo[0] == 0)) break;   // every replica has stopped
-        k_rl_list_fill<<<lgrid, LTB, 2 * sizeof(int) * B, c.stream>>>(a, sweep);
-        for (int k = 0; k < B; ++k) {
-            const int64_t n = hb[k + 1] - hb[k];
-            if (n <= 0) continue;
+        if (hb[nseg] == 0 || (sweep > 0 && hinfo[0] == 0)) break;   // every replica has stopped
+        k_rl_list_fill<<<lgrid, LTB, 2 * sizeof(int) * nseg, c.stream>>>(a, sweep);
+        // visit mode when the replicas of an entry are mostly idle (few visits per listed entry):
+        // a wave per entry would run mostly empty lanes
+        const int64_t n_ent = hb[nseg], n_vis = hb[2 * nseg + 1];
+        const bool vmode = pack && c.rl_visit_div > 0 && n_vis * c.rl_visit_div < n_ent * (int64_t)std::min(rcount, 64);
+        if (vmode) {
+            a.vlist = ensure<int64_t>(c.rl_vlist, (size_t)n_vis + 1);
+            int32_t* nvv = ensure<int32_t>(c.rl_vcount, 2 * (size_t)n_ent + 2);
+            k_rl_visits_count<<<nb(n_ent, LTB), LTB, 0, c.stream>>>(a, n_ent, nvv);
+            exclusive_scan(c, (const int32_t*)nvv, nvv + n_ent + 1, n_ent);
+            k_rl_visits_fill<<<nb(n_ent, LTB), LTB, 0, c.stream>>>(a, n_ent, nvv + n_ent + 1);
+        }
+        auto grid_of = [&](int64_t n) {
             const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
-            const unsigned grid = (unsigned)std::min<int64_t>(items, 8192);
+            return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
+        };
+        for (int k = 0; k < B; ++k) {
+            const int64_t nb_all = hb[(k + 1) * NCLS] - hb[k * NCLS];
+            if (nb_all <= 0) continue;
             const int ev = timer_begin(c);
-            if (louv) k_rl_decide<true><<<grid, RTB, 0, c.stream>>>(a, k, sweep);
-            else k_rl_decide<false><<<grid, RTB, 0, c.stream>>>(a, k, sweep);
-            timer_end(c, 4, ev);
-            if (hv) {
-                if (louv) k_rl_heavy<true><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, sweep);
-                else k_rl_heavy<false><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, sweep);
+            if (pack && vmode) {
+                for (int cls = 0; cls < NCLS - 1; ++cls) {
+                    const int seg = k * NCLS + cls;
+                    const int64_t n = hb[nseg + 1 + seg + 1] - hb[nseg + 1 + seg];
+                    if (n <= 0) continue;
+                    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 63) / 64, 8192));
+#define RL_LAUNCH(L, KK, U) k_rl_decide_v<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep)
+#define RL_LAUNCH_K(L, U) \
+    do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
+                    if (louv && a.unitw) RL_LAUNCH_K(true, true);
+                    else if (louv) RL_LAUNCH_K(true, false);
+                    else RL_LAUNCH_K(false, true);
+#undef RL_LAUNCH_K
+#undef RL_LAUNCH
+                }
+            } else if (pack) {
+                for (int cls = 0; cls < NCLS - 1; ++cls) {
+                    const int seg = k * NCLS + cls;
+                    const int64_t n = hb[seg + 1] - hb[seg];
+                    if (n <= 0) continue;
+                    const unsigned grid = grid_of(n);
+#define RL_LAUNCH(L, KK, U) k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep)
+#define RL_LAUNCH_K(L, U) \
+    do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
+                    if (louv && a.unitw) RL_LAUNCH_K(true, true);
+                    else if (louv) RL_LAUNCH_K(true, false);
+                    else RL_LAUNCH_K(false, true);
+#undef RL_LAUNCH_K
+#undef RL_LAUNCH
+                }
+            } else {
+                const int64_t n = hb[k * NCLS + NCLS - 1] - hb[k * NCLS];
+                if (n > 0) {
+                    if (louv) k_rl_decide_lds<true><<<grid_of(n), RTB, 0, c.stream>>>(a, k, sweep);
+                    else k_rl_decide_lds<false><<<grid_of(n), RTB, 0, c.stream>>>(a, k, sweep);
+                }
             }
-            const unsigned agrid = (unsigned)std::min<int64_t>(items, 8192);
-            if (louv) k_rl_apply<true><<<agrid, RTB, 0, c.stream>>>(a, k);
-            else k_rl_apply<false><<<agrid, RTB, 0, c.stream>>>(a, k);
+            timer_end(c, 4, ev);
+            if (hb[(k + 1) * NCLS] > hb[k * NCLS + NCLS - 1]) {
+                if (louv) k_rl_heavy<true><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
+                else k_rl_heavy<false><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
+            }
+            if (louv) k_rl_apply<true><<<grid_of(nb_all), RTB, 0, c.stream>>>(a, k);
+            else k_rl_apply<false><<<grid_of(nb_all), RTB, 0, c.stream>>>(a, k);
         }
         if (a.lm) {
             const int64_t items = banks == 1 ? (N + VPW - 1) / VPW : N * banks;
@@ -857,7 +1295,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             int32_t st8[8];
             FC_HIP(hipMemcpy(st8, n_active, sizeof(st8), hipMemcpyDeviceToHost));
             fprintf(stderr, "[fc] rl it=%d sweep=%d entries=%d visits=%llu moves=%llu active=%d dt_us=%.0f\n", iteration,
-                    sweep, hb[B], *(unsigned long long*)(st8 + 6), *(unsigned long long*)(st8 + 2), st8[0],
+                    sweep, hb[nseg], *(unsigned long long*)(st8 + 6), *(unsigned long long*)(st8 + 2), st8[0],
                     1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
             t_last = t_now;
         }

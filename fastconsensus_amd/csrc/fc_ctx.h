@@ -112,7 +112,9 @@ struct Ctx {
     DevBuf mvf;                     // movers of a tracked sweep (prune_mark = 1 on weighted Louvain graphs)
     // replica-lane engine (cd_rl.hip): per-entry replica masks, list-build scratch, affected /
     // mover bits [banks][N]; labels and totals node-major in labT / tot ([N][ldT])
-    DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf;
+    DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
+    // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
+    int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
     int cd_engine = 1;              // FC_OPT_CD_ENGINE: 1 replica-lane (cd_rl.hip), 0 classic (cd.hip)
     int ldT = 0;
     bool labT_valid = false;

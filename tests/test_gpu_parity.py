@@ -220,6 +220,34 @@ def test_cd_replica_lanes_bit_exact_vs_twin(fcmod, algo, n_r):
     eng.close()
 
 
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("visit_div", ["0", "1000000"])
+@pytest.mark.parametrize("n_r", [6, 64, 70])
+def test_cd_replica_lanes_visit_mode_bit_exact(fcmod, algo, visit_div, n_r, monkeypatch):
+    """Replica-lane engine with its sparse-sweep visit mode never (0) / always (huge) chosen:
+    one lane per (entry, replica) visit decides exactly as a wave per entry; weighted
+    consensus graph too (Leiden-style marks)."""
+    monkeypatch.setenv("FC_RL_VISIT_DIV", visit_div)
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=43)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    eng.cd(algo, 0, n_r, n_r, 2)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 2, 43)
+    np.testing.assert_array_equal(eng.get_labels(n_r), exp)
+    eng.close()
+    case, eng = _weighted_consensus_engine(fcmod, 47)
+    u, v, w, _ = eng.get_graph()
+    sigma = eng.node_map()
+    a_, b_ = sigma[u], sigma[v]
+    lo, hi = np.minimum(a_, b_), np.maximum(a_, b_)
+    o = np.lexsort((hi, lo))
+    g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
+    eng.cd(algo, 0, n_r, n_r, 3)
+    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 47)
+    np.testing.assert_array_equal(eng.get_labels(n_r), exp[:, sigma])
+    eng.close()
+
+
 @pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
