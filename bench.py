@@ -312,7 +312,8 @@ def main():
         from fastconsensus_amd.core import store_order_pays
         from fastconsensus_amd.distributed import shard
         r0, r1 = shard(cfg["n_p"], rank, world)
-        eng.set_option("store", store_order_pays(r1 - r0, ALGORITHMS[cfg["algo"]]))   # --store overrides below
+        eng.set_option("store", store_order_pays(r1 - r0, ALGORITHMS[cfg["algo"]],
+                                                int(dict(kv.split("=", 1) for kv in args.opt).get("cd_engine", 0))))
         if args.buckets:
             eng.set_params(buckets=args.buckets)
         for name in ("chunk", "prune", "relabel", "store", "coarsen"):
@@ -408,7 +409,7 @@ def main():
             traffic, traffic_note = load_traffic(args.config)
         else:
             traffic, traffic_note = None, "the PMC summary is for the config's n_p"
-        cd_engine = 1                          # FC_OPT_CD_ENGINE default (replica-lane)
+        cd_engine = 0                          # FC_OPT_CD_ENGINE default (classic)
         for kv in args.opt:
             if kv.split("=", 1)[0] == "cd_engine":
                 cd_engine = int(kv.split("=", 1)[1])

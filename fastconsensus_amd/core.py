@@ -362,14 +362,13 @@ def labels_to_output(algorithm, node_labels, labels):
     return out
 
 
-def store_order_pays(replicas, algorithm=None):
+def store_order_pays(replicas, algorithm=None, cd_engine=0):
     """Label storage order (FC_OPT_STORE) for a GPU that will hold `replicas` replicas: the
     one-replica ordering pass at load costs ~4 ms on LFR-1M and saves gather misses of the
-    CLASSIC CD engine in proportion to the replicas (measured: n_p=8 61.7 ms without vs 63.0
-    with, n_p=16 89.0 vs 87.0, n_p=64 saves ~20 ms).  The default replica-lane engine, which
-    runs the louvain / lpm batches, reads labels node-major and gains nothing from it; Leiden's
-    level-0 move phase still runs on the classic engine."""
-    if algorithm in (FC_ALGO_LOUVAIN, FC_ALGO_LPM, FC_ALGO_LOUVAIN_NC, "louvain", "lpm"):
+    classic CD engine (the default) in proportion to the replicas (measured: n_p=8 61.7 ms
+    without vs 63.0 with, n_p=16 89.0 vs 87.0, n_p=64 saves ~20 ms).  The replica-lane engine
+    (cd_engine=1) reads labels node-major and gains nothing from it for louvain / lpm."""
+    if cd_engine == 1 and algorithm in (FC_ALGO_LOUVAIN, FC_ALGO_LPM, FC_ALGO_LOUVAIN_NC, "louvain", "lpm"):
         return 0
     return 1 if replicas >= 12 else 0
 

@@ -115,7 +115,7 @@ struct Ctx {
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
-    int cd_engine = 1;              // FC_OPT_CD_ENGINE: 1 replica-lane (cd_rl.hip), 0 classic (cd.hip)
+    int cd_engine = 0;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip, default), 1 replica-lane (cd_rl.hip)
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable

@@ -141,13 +141,14 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 that moves < n/4 vertices.                                       */
 #define FC_OPT_INFOMAP_TRIALS 13 /* independent Infomap runs per replica, the smallest codelength kept
                                     (default 10, igraph community_infomap's trials)              */
-#define FC_OPT_CD_ENGINE 14  /* louvain / lpm CD batches.  1 (default): the replica-lane engine --
-                                every replica of a batch visits the vertices in ONE shared random
-                                order per sweep (ties broken per replica), labels node-major, one
-                                wave deciding a vertex for up to 64 replicas; no coarse rounds or
-                                tail kernel.  0: the classic engine, a random order per replica
-                                (FC_OPT_COARSEN / FC_OPT_TAIL_VISITS apply).  Both are bit-exact
-                                against oracle/fc_oracle.c orc_engine_cd (shared = 1 / 0).       */
+#define FC_OPT_CD_ENGINE 14  /* louvain / lpm CD batches.  0 (default): the classic engine, a random
+                                visit order per replica (FC_OPT_COARSEN / FC_OPT_TAIL_VISITS
+                                apply).  1: the replica-lane engine (cd_rl.hip) -- every replica of
+                                a batch visits the vertices in ONE shared random order per sweep
+                                (ties broken per replica), labels node-major, one wave deciding a
+                                vertex for up to 64 replicas; no coarse rounds or tail kernel.
+                                Both are bit-exact against oracle/fc_oracle.c orc_engine_cd
+                                (shared = 0 / 1).                                                */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

@@ -281,11 +281,11 @@ def infomap_full(g, seed, trials=10):
     return lab, L, core.value
 
 
-def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=0,
-              prune_mark=1, shared=1):
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8,
+              prune_mark=1, shared=0):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels).  Defaults = the
-    default (replica-lane) engine, cd_rl.hip: one visit order shared by every replica, no coarse
-    rounds.  The classic engine (FC_OPT_CD_ENGINE=0, cd.hip) is shared=0, coarsen=8 (fc_ctx.h)."""
+    default (classic) engine, cd.hip (fc_ctx.h).  The replica-lane engine (FC_OPT_CD_ENGINE=1,
+    cd_rl.hip) is shared=1 (one visit order shared by every replica), coarsen=0."""
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)

@@ -66,10 +66,10 @@ def test_cpu_twin_defaults_match_engine_defaults():
     from tests.cpu_engine import OracleEngine
     src = open(os.path.join(ROOT, "fastconsensus_amd", "csrc", "fc_ctx.h")).read()
     eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen", "prune_mark")}
-    # the default CD engine is the replica-lane one: one shared visit order, no coarse rounds
-    assert int(re.search(r"\bcd_engine = (\d+)", src).group(1)) == 1
-    eng["shared"] = 1
-    eng["coarsen"] = 0
+    # the default CD engine is the classic one (per-replica visit orders); the replica-lane
+    # engine is opt-in (FC_OPT_CD_ENGINE=1)
+    assert int(re.search(r"\bcd_engine = (\d+)", src).group(1)) == 0
+    eng["shared"] = 0
     twin = inspect.signature(orc.engine_cd).parameters
     model = inspect.signature(OracleEngine.__init__).parameters
     for k, v in eng.items():

@@ -158,8 +158,8 @@ def _lfr1k_graph():
 # tail: FC_OPT_TAIL_VISITS -- 0 keeps every sweep on the multi-kernel path; a huge value
 # hands every sweep after the first two to the per-replica tail kernel (classic engine)
 TAILS = [0, 1 << 40]
-# FC_OPT_CD_ENGINE: 1 replica-lane (default, cd_rl.hip; twin shared=1, coarsen=0), 0 classic (cd.hip)
-ENGINES = [1, 0]
+# FC_OPT_CD_ENGINE: 0 classic (default, cd.hip), 1 replica-lane (cd_rl.hip; twin shared=1, coarsen=0)
+ENGINES = [0, 1]
 
 
 def _engine(eng, engine, tail=0, coarsen=0):
@@ -168,6 +168,7 @@ def _engine(eng, engine, tail=0, coarsen=0):
     if engine == 1:
         if tail != TAILS[0] or coarsen != 0:
             pytest.skip("replica-lane engine: no tail kernel / coarse rounds")
+        eng.set_option("cd_engine", 1)
         return {"shared": 1, "coarsen": 0}
     eng.set_option("cd_engine", 0)
     eng.set_option("tail_visits", tail)
@@ -209,9 +210,10 @@ def test_cd_replica_lanes_bit_exact_vs_twin(fcmod, algo, n_r):
     16, 64, and banks of 64 past 64 local replicas; a shard [r0, r0 + k) of a larger batch."""
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=41)
+    eng.set_option("cd_engine", 1)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     eng.cd(algo, 0, n_r, n_r, 1)
-    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 1, 41)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 1, 41, shared=1, coarsen=0)
     np.testing.assert_array_equal(eng.get_labels(n_r), exp)
     if n_r > 2:
         k = n_r // 2
@@ -230,12 +232,14 @@ def test_cd_replica_lanes_visit_mode_bit_exact(fcmod, algo, visit_div, n_r, monk
     monkeypatch.setenv("FC_RL_VISIT_DIV", visit_div)
     case, g = _lfr1k_graph()
     eng = fcmod.Engine(seed=43)
+    eng.set_option("cd_engine", 1)
     eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
     eng.cd(algo, 0, n_r, n_r, 2)
-    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 2, 43)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 2, 43, shared=1, coarsen=0)
     np.testing.assert_array_equal(eng.get_labels(n_r), exp)
     eng.close()
     case, eng = _weighted_consensus_engine(fcmod, 47)
+    eng.set_option("cd_engine", 1)
     u, v, w, _ = eng.get_graph()
     sigma = eng.node_map()
     a_, b_ = sigma[u], sigma[v]
@@ -243,7 +247,7 @@ def test_cd_replica_lanes_visit_mode_bit_exact(fcmod, algo, visit_div, n_r, monk
     o = np.lexsort((hi, lo))
     g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
     eng.cd(algo, 0, n_r, n_r, 3)
-    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 47)
+    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 47, shared=1, coarsen=0)
     np.testing.assert_array_equal(eng.get_labels(n_r), exp[:, sigma])
     eng.close()
 
@@ -484,8 +488,8 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     case, _ = _lfr1k_graph()
     e = case.edges_file
     eng = fcmod.Engine(seed=17)
+    eng.set_option("cd_engine", engine)
     if engine == 0:
-        eng.set_option("cd_engine", 0)
         eng.set_option("tail_visits", tail)
     elif tail:
         pytest.skip("replica-lane engine: no tail kernel")
