@@ -267,20 +267,29 @@ class IdGraph:
     @staticmethod
     def from_networkx(G):
         """Node order = G.nodes(); for each node x, its later neighbours are emitted in
-        G.adj[x] order (that is the order G.copy() keeps, fast_consensus.py:131)."""
+        G.adj[x] order (that is the order G.copy() keeps, fast_consensus.py:131).  The
+        adjacency is read at C speed (dict keys chained into numpy) and mapped to indices by a
+        lookup array when the nodes are small non-negative integers (by a dict otherwise)."""
         if G.is_directed():
             raise TypeError("fast_consensus needs an undirected graph")
+        import itertools
         nodes = list(G.nodes())
-        idx = {x: i for i, x in enumerate(nodes)}
-        us, vs = [], []
-        for x in nodes:
-            ix = idx[x]
-            for z in G.adj[x]:
-                iz = idx[z]
-                if iz > ix:
-                    us.append(ix)
-                    vs.append(iz)
-        return IdGraph(nodes, np.array(us, np.int32), np.array(vs, np.int32))
+        n = len(nodes)
+        adj = G.adj
+        lens = np.fromiter((len(adj[x]) for x in nodes), np.int64, count=n)
+        tot = int(lens.sum())
+        flat = itertools.chain.from_iterable(adj[x] for x in nodes)
+        if n and all(type(x) is int for x in nodes[:1]) and all(isinstance(x, (int, np.integer)) for x in nodes) \
+                and min(nodes) >= 0 and max(nodes) < 4 * n + 1024:
+            lut = np.full(max(nodes) + 1, -1, np.int64)
+            lut[np.asarray(nodes, np.int64)] = np.arange(n, dtype=np.int64)
+            nbr = lut[np.fromiter(flat, np.int64, count=tot)]
+        else:
+            idx = {x: i for i, x in enumerate(nodes)}
+            nbr = np.fromiter((idx[z] for z in flat), np.int64, count=tot)
+        src = np.repeat(np.arange(n, dtype=np.int64), lens)
+        keep = nbr > src
+        return IdGraph(nodes, src[keep].astype(np.int32), nbr[keep].astype(np.int32))
 
     @staticmethod
     def from_edgelist_file(path):

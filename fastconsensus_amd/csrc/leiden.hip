@@ -1239,7 +1239,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         const int nblk = a.bmap ? a.bpr * a.nact : (int)nb(nU);
         const int hg = heavy_grid(a.hslots);
         const int hblk = 64;
-        for (int b = 0; b < B; ++b) {
+        for (int b = 0; b < a.B; ++b) {
             const uint32_t stamp = ++stamp_ctr;   // unique per bucket launch of this run (mvt)
             FC_HIP(hipMemsetAsync(hcnt, 0, 4 * NTIER, c.stream));
             // (timed per launch into spans 5 / 6 when timing is on: lv decide / lv heavy)
@@ -1478,6 +1478,13 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         k_lv_fill_u8<<<nb(nU), LTB, 0, c.stream>>>(nU, act, done, cur.rep);
         set_graph();
         a.P = P; a.R = R; a.tot = ptot; a.rsize = rsize; a.act = act;
+        // dense aggregate levels: more buckets, so that fewer neighbours of a vertex decide in
+        // the same bucket (FC_LV_DENSE_DIV: buckets >= average degree / div, up to 1024; 0 = B)
+        const int64_t avgdeg = cur.E / std::max<int64_t>(nU, 1);
+        int Bl = B;
+        if (c.lv_dense_div > 0)
+            while (Bl < 1024 && (int64_t)Bl * c.lv_dense_div < avgdeg) Bl <<= 1;
+        a.B = Bl;
         int sw = 0;
         for (; sw < c.max_sweeps; ++sw) {
             ++lv_sweeps;
@@ -1499,6 +1506,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             }
             if (mvs == 0) break;
         }
+        a.B = B;
         if (c.trace) {
             sync(c);
             static auto t_last = std::chrono::steady_clock::now();
