@@ -101,6 +101,33 @@ def test_networkx_input_order_is_adjacency_order():
     assert pairs.index((1, 2)) < pairs.index((1, 3))
 
 
+@pytest.mark.parametrize("labels", ["ints", "shuffled", "strings", "sparse_ints"])
+def test_networkx_conversion_matches_literal_walk(labels):
+    """The vectorised IdGraph.from_networkx equals the literal walk (every node in G.nodes()
+    order, its later neighbours in G.adj order) for integer, shuffled, string and sparse labels."""
+    import random
+    import networkx as nx
+    from fastconsensus_amd.core import IdGraph
+    G = nx.gnm_random_graph(600, 2500, seed=3)
+    if labels == "shuffled":
+        perm = list(G.nodes())
+        random.Random(5).shuffle(perm)
+        H = nx.Graph()
+        H.add_nodes_from(perm)
+        H.add_edges_from(G.edges())
+        G = H
+    elif labels == "strings":
+        G = nx.relabel_nodes(G, {i: "v%d" % (i * 7 % 600) for i in G.nodes()})
+    elif labels == "sparse_ints":
+        G = nx.relabel_nodes(G, {i: i * 100003 for i in G.nodes()})
+    nodes = list(G.nodes())
+    idx = {x: i for i, x in enumerate(nodes)}
+    exp = [(idx[x], idx[z]) for x in nodes for z in G.adj[x] if idx[z] > idx[x]]
+    g = IdGraph.from_networkx(G)
+    assert list(g.labels) == nodes
+    assert list(zip(g.u.tolist(), g.v.tolist())) == exp
+
+
 def test_unknown_and_out_of_scope_algorithms():
     import networkx as nx
     import fastconsensus_amd as fc
