@@ -5,6 +5,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -35,7 +36,8 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
                 targs = kern.split("<", 1)[1].split(">")[0].replace(" ", "")
                 short = "k_decide_light<%s>" % {"true,int": "louvain", "false,int": "lpa"}.get(targs, targs)
             elif "k_lv_" in kern:       # Leiden / Infomap kernels: one entry per kernel (all instances)
-                short = short.split("::")[-1]
+                # (anonymous-namespace names: "void fc::(anonymous namespace)::k_lv_decide<...>(...)")
+                short = re.search(r"(k_lv_\w+)", kern).group(1)
             counters[short][r.get("Counter_Name", "?")].append(float(r.get("Counter_Value", "nan")))
     per = {}
     for kern, cs in counters.items():
