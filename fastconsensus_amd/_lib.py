@@ -26,7 +26,8 @@ SYMBOLS = [
     "fc_last_error", "fc_version", "fc_create", "fc_destroy", "fc_set_stream", "fc_synchronize", "fc_set_timing",
     "fc_collect_timing", "fc_set_params", "fc_set_option", "fc_load_graph", "fc_graph_info", "fc_get_node_map", "fc_reset_graph", "fc_get_graph", "fc_get_nextgraph", "fc_run",
     "fc_cd", "fc_set_labels", "fc_replica_info", "fc_get_labels", "fc_consensus_partial", "fc_consensus_apply",
-    "fc_closure_sample", "fc_closure_set_pairs", "fc_closure_partial", "fc_closure_apply",
+    "fc_closure_sample", "fc_closure_set_pairs", "fc_closure_begin", "fc_closure_block_sample",
+    "fc_closure_block_add", "fc_closure_finish", "fc_closure_partial", "fc_closure_apply",
     "fc_generate_lfr", "fc_generate_sbm", "fc_read_edgelist",
 ]
 
@@ -96,6 +97,10 @@ def load():
     L.fc_consensus_apply.argtypes = [vp, c_int, c_int, dbl, dbl, vp, P(c_int), P(i64), P(i64)]
     L.fc_closure_sample.argtypes = [vp, i64, c_int, P(i64)]
     L.fc_closure_set_pairs.argtypes = [vp, i64, vp, c_int, P(i64)]
+    L.fc_closure_begin.argtypes = [vp, i64, c_int, P(c_int)]
+    L.fc_closure_block_sample.argtypes = [vp, c_int, i64, i64, vp, i64, P(i64)]
+    L.fc_closure_block_add.argtypes = [vp, c_int, vp, i64]
+    L.fc_closure_finish.argtypes = [vp, P(i64)]
     L.fc_closure_partial.argtypes = [vp, vp]
     L.fc_closure_apply.argtypes = [vp, c_int, c_int, dbl, vp, c_int, P(c_int), P(i64)]
     L.fc_generate_lfr.argtypes = [i64, dbl, dbl, dbl, dbl, i32, i32, i32, u64, i64, vp, vp, P(i64), vp]

@@ -24,6 +24,11 @@ def torch_int32():
     return torch.int32
 
 
+def torch_int64():
+    import torch
+    return torch.int64
+
+
 def algo_id(algorithm):
     if algorithm in ALGORITHMS:
         return ALGORITHMS[algorithm]
@@ -231,6 +236,33 @@ class Engine:
     def closure_sample(self, attempts, iteration):
         nc = ctypes.c_int64()
         check(self._L.fc_closure_sample(self._ctx, int(attempts), int(iteration), ctypes.byref(nc)))
+        return nc.value
+
+    # sharded closure (distributed.py, world > 1): same candidates as closure_sample
+    def closure_begin(self, attempts, iteration):
+        """Returns the number of closure blocks; block b covers attempts
+        [attempts*b//blocks, attempts*(b+1)//blocks)."""
+        nb = ctypes.c_int()
+        check(self._L.fc_closure_begin(self._ctx, int(attempts), int(iteration), ctypes.byref(nb)))
+        return nb.value
+
+    def closure_block_sample(self, block, t_lo, t_hi, dev_out):
+        """Draws attempts [t_lo, t_hi) of `block` into dev_out (int64 tensor, (key, first
+        attempt) pairs); returns the number of pairs."""
+        if dev_out.dtype != torch_int64() or dev_out.numel() < 2 * max(t_hi - t_lo, 0):
+            raise ValueError("dev_out must be an int64 tensor of >= %d elements" % (2 * (t_hi - t_lo)))
+        k = ctypes.c_int64()
+        check(self._L.fc_closure_block_sample(self._ctx, int(block), int(t_lo), int(t_hi), self._dev(dev_out),
+                                              int(dev_out.numel() // 2), ctypes.byref(k)))
+        self._written()
+        return k.value
+
+    def closure_block_add(self, block, dev_in, count):
+        check(self._L.fc_closure_block_add(self._ctx, int(block), self._dev(dev_in) if count else None, int(count)))
+
+    def closure_finish(self):
+        nc = ctypes.c_int64()
+        check(self._L.fc_closure_finish(self._ctx, ctypes.byref(nc)))
         return nc.value
 
     def closure_set_pairs(self, pairs, iteration):

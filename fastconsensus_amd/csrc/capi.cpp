@@ -342,6 +342,54 @@ int fc_closure_sample(fc_ctx* ctx, int64_t attempts, int iteration, int64_t* n_c
     FC_API_END
 }
 
+static int64_t closure_block_t(const Ctx& c, int block) { return c.clo_attempts * block / c.clo_R; }
+
+int fc_closure_begin(fc_ctx* ctx, int64_t attempts, int iteration, int* blocks) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    if (attempts < 0) attempts = c.m_original;
+    const int R = closure_begin(c, attempts, iteration);
+    if (blocks) *blocks = R;
+    FC_API_END
+}
+
+int fc_closure_block_sample(fc_ctx* ctx, int block, int64_t t_lo, int64_t t_hi, void* dev_out, int64_t capacity,
+                            int64_t* count) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.clo_next >= 0, FC_ESTATE, "fc_closure_begin first");
+    FC_REQUIRE(block == c.clo_next, FC_ESTATE,
+               "closure block " + std::to_string(block) + " sampled before block " + std::to_string(c.clo_next) +
+                   " was added");
+    FC_REQUIRE(block < c.clo_R, FC_EINVAL, "closure block out of range");
+    FC_REQUIRE(t_lo >= closure_block_t(c, block) && t_lo <= t_hi && t_hi <= closure_block_t(c, block + 1), FC_EINVAL,
+               "attempt range outside the block");
+    FC_REQUIRE(dev_out || t_hi == t_lo, FC_EINVAL, "null output buffer");
+    const int64_t k = closure_block_sample(c, block, t_lo, t_hi, (int64_t*)dev_out, capacity);
+    if (count) *count = k;
+    FC_API_END
+}
+
+int fc_closure_block_add(fc_ctx* ctx, int block, const void* dev_in, int64_t count) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.clo_next >= 0 && block == c.clo_next && block < c.clo_R, FC_ESTATE, "closure blocks go in order");
+    FC_REQUIRE(count >= 0 && count <= closure_block_t(c, block + 1) - closure_block_t(c, block), FC_EINVAL,
+               "more pairs than the block has attempts");
+    FC_REQUIRE(dev_in || count == 0, FC_EINVAL, "null input buffer");
+    closure_block_add(c, block, (const int64_t*)dev_in, count);
+    FC_API_END
+}
+
+int fc_closure_finish(fc_ctx* ctx, int64_t* n_cand) {
+    FC_CTX(ctx)
+    FC_API_BEGIN
+    FC_REQUIRE(c.clo_next >= 0 && c.clo_next == c.clo_R, FC_ESTATE, "closure blocks missing");
+    const int64_t k = closure_finish(c);
+    if (n_cand) *n_cand = k;
+    FC_API_END
+}
+
 int fc_closure_set_pairs(fc_ctx* ctx, int64_t npairs, const int32_t* pairs, int iteration, int64_t* n_cand) {
     FC_CTX(ctx)
     FC_API_BEGIN

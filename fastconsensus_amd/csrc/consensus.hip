@@ -396,61 +396,187 @@ static void finish_candidates(Ctx& c, int64_t n, uint64_t* k1, int64_t* v1, int 
     k_scatter_cand<<<nblk(n), TB, 0, c.stream>>>(n, fl, ps, k2, v2, c.key_bits, base, cu, cv, cage);
 }
 
+// Buffers of a closure over `attempts` (sized for the whole run: no reallocation between blocks)
+namespace {
+struct Clo {
+    int R;
+    int64_t rcap;
+    uint64_t hsize;
+    uint64_t* hkey;
+    uint32_t* hval;
+    int64_t *slot, *fl, *ps, *aval, *nacc;
+    uint64_t* akey;
+    int32_t *nrow, *ncur, *ncol;
+};
+}  // namespace
+static Clo clo_bufs(Ctx& c, int64_t attempts) {
+    Clo b;
+    const int64_t cap = attempts > 0 ? attempts : 1;
+    b.R = (int)std::max<int64_t>(1, std::min<int64_t>(c.closure_rounds, cap));
+    b.rcap = (cap + b.R - 1) / b.R + 1;                            // attempts per block (at most)
+    const int64_t N = c.N;
+    b.hsize = 1024;
+    while (b.hsize < 2 * (uint64_t)b.rcap) b.hsize <<= 1;          // one block's pairs, load <= 1/2
+    b.hkey = ensure<uint64_t>(c.clo_hkey, b.hsize);
+    b.hval = ensure<uint32_t>(c.clo_hval, b.hsize);
+    b.slot = ensure<int64_t>(c.clo_list, b.rcap);
+    b.fl = ensure<int64_t>(c.nodetmp, std::max<int64_t>(b.rcap + 1, N + 1));
+    b.ps = ensure<int64_t>(c.nodetmp2, std::max<int64_t>(b.rcap + 1, N + 1));
+    b.akey = ensure<uint64_t>(c.clo_akey, cap);
+    b.aval = ensure<int64_t>(c.clo_aval, cap);
+    b.nacc = ensure<int64_t>(c.clo_cnt, 4);                         // [0] candidates so far, [1] this block's first, [2..3] scratch
+    // the C graph (ping-pong; sized for every candidate: no reallocation inside the loop)
+    b.nrow = ensure<int32_t>(c.clo_nrow, 2 * (N + 1));             // a block's new-entry offsets | cursors
+    b.ncur = b.nrow + (N + 1);
+    b.ncol = ensure<int32_t>(c.clo_ncol, 2 * b.rcap);
+    if (b.R > 1)
+        for (DevBuf* d : {&c.clo_col, &c.clo_col2}) ensure<int32_t>(*d, 2 * cap);
+    for (DevBuf* d : {&c.clo_rowptr, &c.clo_rowptr2}) ensure<int64_t>(*d, N + 1);
+    return b;
+}
+static void clo_reset(Ctx& c, const Clo& b) {
+    FC_HIP(hipMemsetAsync(b.nacc, 0, 2 * sizeof(int64_t), c.stream));
+    FC_HIP(hipMemsetAsync(c.clo_rowptr.p, 0, sizeof(int64_t) * (c.N + 1), c.stream));   // empty C graph
+}
+static void clo_clear_table(Ctx& c, const Clo& b) {
+    FC_HIP(hipMemsetAsync(b.hkey, 0xff, sizeof(uint64_t) * b.hsize, c.stream));
+    FC_HIP(hipMemsetAsync(b.hval, 0xff, sizeof(uint32_t) * b.hsize, c.stream));
+}
+// attempts [t0, t0 + n) of block r drawn into the (cleared) table; slot[i] >= 0 lists a new pair
+static void clo_draw(Ctx& c, const Clo& b, int64_t t0, int64_t n, int iteration, int r) {
+    const uint64_t s = mix64(c.seed ^ 0xC105u);
+    k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
+                                                  c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
+                                                  r > 0 ? c.clo_rowptr.as<int64_t>() : nullptr,
+                                                  r > 0 ? c.clo_col.as<int32_t>() : nullptr, c.key_bits, b.hkey, b.hval,
+                                                  b.hsize - 1, b.slot);
+}
+// the listed slots of the table (slot[0..n)) appended to the accumulated candidates; unless r is
+// the last block, the C graph grows by them (rows ascending) for the next block
+static void clo_append(Ctx& c, const Clo& b, int64_t n, int64_t t0, int r) {
+    const int bits = c.key_bits;
+    const int64_t N = c.N;
+    k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, b.slot, b.fl, b.nacc);
+    exclusive_scan(c, b.fl, b.ps, n + 1);
+    k_append_cand<<<nblk(n + 1), TB, 0, c.stream>>>(n, b.slot, b.ps, b.hkey, b.hval, t0, b.nacc, b.akey, b.aval);
+    if (r + 1 == b.R) return;
+    FC_HIP(hipMemsetAsync(b.nrow, 0, sizeof(int32_t) * 2 * (N + 1), c.stream));
+    k_cgraph_ndeg<<<nblk(n), TB, 0, c.stream>>>(b.nacc, b.akey, bits, b.ncur);
+    exclusive_scan(c, b.ncur, b.nrow, N + 1);
+    FC_HIP(hipMemsetAsync(b.ncur, 0, sizeof(int32_t) * (N + 1), c.stream));
+    k_cgraph_nfill<<<nblk(n), TB, 0, c.stream>>>(b.nacc, b.akey, bits, b.nrow, b.ncur, b.ncol);
+    k_cgraph_merge<<<nblk(N + 1), TB, 0, c.stream>>>(N, c.clo_rowptr.as<int64_t>(), c.clo_col.as<int32_t>(), b.nrow,
+                                                     b.ncol, c.clo_rowptr2.as<int64_t>(), c.clo_col2.as<int32_t>());
+    std::swap(c.clo_rowptr, c.clo_rowptr2);
+    std::swap(c.clo_col, c.clo_col2);
+}
+
 void closure_sample(Ctx& c, int64_t attempts, int iteration) {
     const int sl = timer_begin(c);
-    const int64_t cap = attempts > 0 ? attempts : 1;
-    const int R = (int)std::max<int64_t>(1, std::min<int64_t>(c.closure_rounds, cap));
-    const int64_t rcap = (cap + R - 1) / R + 1;                   // attempts per block (at most)
-    const int64_t N = c.N;
-    uint64_t hsize = 1024;
-    while (hsize < 2 * (uint64_t)rcap) hsize <<= 1;                // one block's pairs, load <= 1/2
-    uint64_t* hkey = ensure<uint64_t>(c.clo_hkey, hsize);
-    uint32_t* hval = ensure<uint32_t>(c.clo_hval, hsize);
-    int64_t* slot = ensure<int64_t>(c.clo_list, rcap);
-    int64_t* fl = ensure<int64_t>(c.nodetmp, std::max<int64_t>(rcap + 1, N + 1));
-    int64_t* ps = ensure<int64_t>(c.nodetmp2, std::max<int64_t>(rcap + 1, N + 1));
-    uint64_t* akey = ensure<uint64_t>(c.clo_akey, cap);
-    int64_t* aval = ensure<int64_t>(c.clo_aval, cap);
-    int64_t* nacc = ensure<int64_t>(c.clo_cnt, 2);                 // [0] candidates so far, [1] this block's first
-    FC_HIP(hipMemsetAsync(nacc, 0, 2 * sizeof(int64_t), c.stream));
-    // the C graph (ping-pong; sized for every candidate: no reallocation inside the loop)
-    int32_t* nrow = ensure<int32_t>(c.clo_nrow, 2 * (N + 1));      // a block's new-entry offsets | cursors
-    int32_t* ncur = nrow + (N + 1);
-    int32_t* ncol = ensure<int32_t>(c.clo_ncol, 2 * rcap);
-    if (R > 1)
-        for (DevBuf* b : {&c.clo_col, &c.clo_col2}) ensure<int32_t>(*b, 2 * cap);
-    for (DevBuf* b : {&c.clo_rowptr, &c.clo_rowptr2}) ensure<int64_t>(*b, N + 1);
-    FC_HIP(hipMemsetAsync(c.clo_rowptr.p, 0, sizeof(int64_t) * (N + 1), c.stream));   // empty C graph
-    const uint64_t s = mix64(c.seed ^ 0xC105u);
-    const int bits = c.key_bits;
-    for (int r = 0; r < R; ++r) {
-        const int64_t t0 = attempts * r / R, t1 = attempts * (r + 1) / R, n = t1 - t0;
+    const Clo b = clo_bufs(c, attempts);
+    clo_reset(c, b);
+    for (int r = 0; r < b.R; ++r) {
+        const int64_t t0 = attempts * r / b.R, t1 = attempts * (r + 1) / b.R, n = t1 - t0;
         if (n <= 0) continue;
-        FC_HIP(hipMemsetAsync(hkey, 0xff, sizeof(uint64_t) * hsize, c.stream));
-        FC_HIP(hipMemsetAsync(hval, 0xff, sizeof(uint32_t) * hsize, c.stream));
-        k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
-                                                      c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
-                                                      r > 0 ? c.clo_rowptr.as<int64_t>() : nullptr,
-                                                      r > 0 ? c.clo_col.as<int32_t>() : nullptr, bits, hkey, hval,
-                                                      hsize - 1, slot);
-        k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, fl, nacc);
-        exclusive_scan(c, fl, ps, n + 1);
-        k_append_cand<<<nblk(n + 1), TB, 0, c.stream>>>(n, slot, ps, hkey, hval, t0, nacc, akey, aval);
-        if (r + 1 == R) continue;
-        // the C graph grows by this block's candidates (rows ascending), for the next block
-        FC_HIP(hipMemsetAsync(nrow, 0, sizeof(int32_t) * 2 * (N + 1), c.stream));
-        k_cgraph_ndeg<<<nblk(n), TB, 0, c.stream>>>(nacc, akey, bits, ncur);
-        exclusive_scan(c, ncur, nrow, N + 1);
-        FC_HIP(hipMemsetAsync(ncur, 0, sizeof(int32_t) * (N + 1), c.stream));
-        k_cgraph_nfill<<<nblk(n), TB, 0, c.stream>>>(nacc, akey, bits, nrow, ncur, ncol);
-        k_cgraph_merge<<<nblk(N + 1), TB, 0, c.stream>>>(N, c.clo_rowptr.as<int64_t>(), c.clo_col.as<int32_t>(), nrow,
-                                                         ncol, c.clo_rowptr2.as<int64_t>(), c.clo_col2.as<int32_t>());
-        std::swap(c.clo_rowptr, c.clo_rowptr2);
-        std::swap(c.clo_col, c.clo_col2);
+        clo_clear_table(c, b);
+        clo_draw(c, b, t0, n, iteration, r);
+        clo_append(c, b, n, t0, r);
     }
     // candidates in key order (first-sample ages ride along; the keys are distinct)
-    finish_candidates(c, read_i64(c, nacc), akey, aval, iteration);
+    finish_candidates(c, read_i64(c, b.nacc), b.akey, b.aval, iteration);
     timer_end(c, 2, sl);
+}
+
+// ---- the same closure with each block's attempts split over ranks (multi-GPU) ----------------
+// A block's draws depend only on the attempt index (Philox counter) and on the graph the block
+// draws from (kept graph + the C graph of the earlier blocks), so rank g can draw any sub-range
+// [t_lo, t_hi) of block r.  Its pairs (deduplicated, first attempt each) go out as int64
+// (key, attempt); the ranks' lists, all-gathered, are re-inserted into the table keeping the
+// smallest attempt per key (atomicMin, as a single rank drawing the whole block does), and
+// appended and grown exactly as closure_sample does: every rank ends with the same candidates.
+__global__ void k_emit_cand(int64_t n, const int64_t* slot, const int64_t* pos, const uint64_t* hkey,
+                            const uint32_t* hval, int64_t t0, int64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || slot[i] < 0) return;
+    const int64_t h = slot[i], p = pos[i];
+    out[2 * p] = (int64_t)hkey[h];
+    out[2 * p + 1] = t0 + (int64_t)hval[h];
+}
+__global__ void k_closure_insert(int64_t cnt, const int64_t* __restrict__ in, int64_t t0, uint64_t* hkey,
+                                 uint32_t* hval, uint64_t hmask, int64_t* slot) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cnt) return;
+    slot[i] = -1;
+    const uint64_t key = (uint64_t)in[2 * i];
+    const uint32_t a = (uint32_t)(in[2 * i + 1] - t0);
+    uint64_t h = clo_slot(key, hmask);
+    while (true) {
+        uint64_t k = hkey[h];
+        if (k == CLO_EMPTY) {
+            k = atomicCAS((unsigned long long*)&hkey[h], (unsigned long long)CLO_EMPTY, (unsigned long long)key);
+            if (k == CLO_EMPTY) {
+                atomicMin(&hval[h], a);
+                slot[i] = (int64_t)h;
+                return;
+            }
+        }
+        if (k == key) { atomicMin(&hval[h], a); return; }
+        h = (h + 1) & hmask;
+    }
+}
+
+int closure_begin(Ctx& c, int64_t attempts, int iteration) {
+    const int sl = timer_begin(c);
+    const Clo b = clo_bufs(c, attempts);
+    clo_reset(c, b);
+    c.clo_attempts = attempts;
+    c.clo_R = b.R;
+    c.clo_next = 0;
+    c.clo_iter = iteration;
+    timer_end(c, 2, sl);
+    return b.R;
+}
+
+int64_t closure_block_sample(Ctx& c, int r, int64_t t_lo, int64_t t_hi, int64_t* out, int64_t capacity) {
+    const int sl = timer_begin(c);
+    const Clo b = clo_bufs(c, c.clo_attempts);
+    const int64_t n = t_hi - t_lo;
+    int64_t count = 0;
+    if (n > 0) {
+        clo_clear_table(c, b);
+        clo_draw(c, b, t_lo, n, c.clo_iter, r);
+        k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, b.slot, b.fl, b.nacc + 2);   // its count snapshot into scratch
+        exclusive_scan(c, b.fl, b.ps, n + 1);
+        count = read_i64(c, b.ps + n);
+        FC_REQUIRE(count <= capacity, FC_EINVAL,
+                   "closure block output holds " + std::to_string(capacity) + " pairs; " + std::to_string(count) +
+                       " drawn");
+        if (count > 0) k_emit_cand<<<nblk(n), TB, 0, c.stream>>>(n, b.slot, b.ps, b.hkey, b.hval, t_lo, out);
+    }
+    timer_end(c, 2, sl);
+    return count;
+}
+
+void closure_block_add(Ctx& c, int r, const int64_t* in, int64_t count) {
+    const int sl = timer_begin(c);
+    const Clo b = clo_bufs(c, c.clo_attempts);
+    const int64_t t0 = c.clo_attempts * r / b.R;
+    if (count > 0) {
+        clo_clear_table(c, b);
+        k_closure_insert<<<nblk(count), TB, 0, c.stream>>>(count, in, t0, b.hkey, b.hval, b.hsize - 1, b.slot);
+        clo_append(c, b, count, t0, r);
+    }
+    c.clo_next = r + 1;
+    timer_end(c, 2, sl);
+}
+
+int64_t closure_finish(Ctx& c) {
+    const int sl = timer_begin(c);
+    const Clo b = clo_bufs(c, c.clo_attempts);
+    finish_candidates(c, read_i64(c, b.nacc), b.akey, b.aval, c.clo_iter);
+    c.clo_next = -1;
+    timer_end(c, 2, sl);
+    return c.n_cand;
 }
 
 void closure_from_pairs(Ctx& c, int64_t npairs, const int32_t* pairs, int iteration) {

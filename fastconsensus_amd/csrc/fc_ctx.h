@@ -141,6 +141,10 @@ struct Ctx {
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
     int closure_rounds = 8;         // FC_OPT_CLOSURE_ROUNDS
+    // sharded closure (fc_closure_begin / _block_sample / _block_add / _finish): the run's
+    // attempts and block count, the next block to add (blocks go in order), -1 = not begun
+    int64_t clo_attempts = 0;
+    int clo_R = 0, clo_next = -1, clo_iter = 0;
     int prune_mark = 1;             // FC_OPT_PRUNE_MARK: 1 Leiden-style marks on consensus graphs, 2 on every graph, 0 every neighbour
     DevBuf sort_tmp;                // hipcub temporary storage
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
@@ -204,6 +208,10 @@ void consensus_partial(Ctx& c, int algo, int32_t* out);
 void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept,
                      int64_t* unconv);
 void closure_sample(Ctx& c, int64_t attempts, int iteration);
+int closure_begin(Ctx& c, int64_t attempts, int iteration);
+int64_t closure_block_sample(Ctx& c, int block, int64_t t_lo, int64_t t_hi, int64_t* out, int64_t capacity);
+void closure_block_add(Ctx& c, int block, const int64_t* in, int64_t count);
+int64_t closure_finish(Ctx& c);
 void closure_from_pairs(Ctx& c, int64_t npairs, const int32_t* pairs, int iteration);
 void closure_partial(Ctx& c, int32_t* out);
 void closure_apply(Ctx& c, int algo, int n_p, const int32_t* counts, int iteration);

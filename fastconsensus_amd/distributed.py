@@ -8,8 +8,11 @@ copy of the graph; the only data-path exchanges are
   * per-candidate closure co-membership counts (SUM, louvain only);
 both travel as uint8 when n_p <= 255 (k_last + 1 and counts are in [0, n_p]): a quarter
 of the int32 bytes on every xGMI ring hop;
-after which threshold, check, closure (same counter-based RNG on every rank), repair and
-the graph rebuild run replicated and deterministically -- no graph broadcast.  The final
+after which threshold, check, repair and the graph rebuild run replicated and
+deterministically -- no graph broadcast.  The triadic closure is split: each of its blocks'
+attempts are divided over the ranks (the counter-based RNG is keyed by the attempt index),
+and the ranks' (pair, first attempt) lists are all-gathered once per block, so every rank
+appends the same candidates (_closure_sharded).  The final
 partitions are all-gathered to rank 0.  The loop mirrors fc_run (capi.cpp) step for step,
 so W ranks produce bit-identical results to one GPU.
 
@@ -50,16 +53,48 @@ def _all_reduce_small(t, op, n_p, world, shift):
     return t
 
 
-def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True, out=None):
+def _closure_sharded(engine, attempts, iteration, world, rank, device):
+    """fast_consensus.py:175-184 / :292-300 (the growing nextgraph) over W ranks: block b's
+    attempts [t0, t1) are split into W contiguous sub-ranges, each rank draws its own, and
+    the ranks' pair lists (int64 key, first attempt) are all-gathered -- a count exchange,
+    then the lists padded to the largest -- and added on every rank before block b + 1 draws
+    from the grown graph.  Same candidates as engine.closure_sample on one rank."""
+    blocks = engine.closure_begin(attempts, iteration)
+    for b in range(blocks):
+        t0, t1 = attempts * b // blocks, attempts * (b + 1) // blocks
+        lo, hi = t0 + (t1 - t0) * rank // world, t0 + (t1 - t0) * (rank + 1) // world
+        cap_pairs = (t1 - t0 + world - 1) // world + 1          # >= every rank's sub-range
+        mine = torch.empty(2 * cap_pairs, dtype=torch.int64, device=device)
+        k = engine.closure_block_sample(b, lo, hi, mine)
+        cnt = torch.tensor([k], dtype=torch.int64, device=device)
+        cnts = [torch.empty_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        cnts = [int(x) for x in torch.cat(cnts).tolist()]
+        top = max(cnts)
+        if top == 0:
+            engine.closure_block_add(b, None, 0)
+            continue
+        recv = [torch.empty(2 * top, dtype=torch.int64, device=device) for _ in range(world)]
+        dist.all_gather(recv, mine[:2 * top])
+        pairs = torch.cat([recv[g][:2 * cnts[g]] for g in range(world)])
+        engine.closure_block_add(b, pairs, sum(cnts))
+    return engine.closure_finish()
+
+
+def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True, out=None,
+                shard_closure=True):
     """Returns (labels [n_p][N] on rank 0 (None elsewhere), stats dict).  `out`: optional
-    C-contiguous int32 host array [n_p][N] that rank 0 downloads into (see Engine.run)."""
+    C-contiguous int32 host array [n_p][N] that rank 0 downloads into (see Engine.run).
+    shard_closure: split the closure's attempts over the ranks (world > 1); False draws all
+    of them on every rank (same result)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     r0, r1 = shard(n_p, rank, world)
     louv = algo in (LOUVAIN, LOUVAIN_NC)    # louvain loop: check #1, closure counts, repair
     on_gpu = str(device).startswith("cuda")
     if not on_gpu:
-        return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out)
+        return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out,
+                     shard_closure)
     # engine kernels and torch/RCCL ops on ONE explicit stream: no cross-stream races
     # (torch's default stream is the legacy null stream, which the engine cannot adopt)
     stream = torch.cuda.Stream(device=device)
@@ -67,13 +102,15 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     engine.set_stream(stream.cuda_stream)
     try:
         with torch.cuda.stream(stream):
-            return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out)
+            return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out,
+                         shard_closure)
     finally:
         stream.synchronize()
         engine.set_stream(None)
 
 
-def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out=None):
+def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out=None,
+          shard_closure=True):
     mine = r1 - r0
     engine.reset_graph()
     n, _, L = engine.graph_info()
@@ -105,7 +142,10 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
         if louv and conv1:
             st["exit_check"] = 1
             break
-        nc = engine.closure_sample(L, it)                            # :175-184 / :292-300
+        if world > 1 and shard_closure:                              # :175-184 / :292-300
+            nc = _closure_sharded(engine, L, it, world, rank, device)
+        else:
+            nc = engine.closure_sample(L, it)
         cnt = None
         if louv and nc > 0:
             cnt = torch.zeros(nc, dtype=torch.int32, device=device)

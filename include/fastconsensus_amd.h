@@ -210,6 +210,19 @@ int fc_consensus_apply(fc_ctx* ctx, int algo, int n_p, double tau, double delta,
 int fc_closure_sample(fc_ctx* ctx, int64_t attempts, int iteration, int64_t* n_cand);
 int fc_closure_set_pairs(fc_ctx* ctx, int64_t npairs, const int32_t* pairs, int iteration,
                          int64_t* n_cand);
+/* The same device closure (fast_consensus.py:175-184 / :292-300, the growing nextgraph) with
+ * each block's attempts split over ranks (multi-GPU: no rank draws all L attempts).
+ * fc_closure_begin returns the block count; block b covers attempts
+ * [L*b/blocks, L*(b+1)/blocks).  For b = 0, 1, ... in order: every rank draws its sub-range
+ * [t_lo, t_hi) with fc_closure_block_sample -> `count` int64 (key, first attempt) pairs in
+ * dev_out (FC_EINVAL if more than `capacity`); the ranks' lists are concatenated (any order)
+ * and handed to fc_closure_block_add on every rank.  fc_closure_finish then leaves exactly
+ * the candidates fc_closure_sample(L) gives, on every rank. */
+int fc_closure_begin(fc_ctx* ctx, int64_t attempts, int iteration, int* blocks);
+int fc_closure_block_sample(fc_ctx* ctx, int block, int64_t t_lo, int64_t t_hi, void* dev_out,
+                            int64_t capacity, int64_t* count);
+int fc_closure_block_add(fc_ctx* ctx, int block, const void* dev_in, int64_t count);
+int fc_closure_finish(fc_ctx* ctx, int64_t* n_cand);
 /* Per-candidate count of local replicas co-clustering it into dev_out (int32[n_cand]). */
 int fc_closure_partial(fc_ctx* ctx, void* dev_out);
 /* Add closure edges (louvain weight = reduced count (:186-190); lpm weight 0 (:302-304)),

@@ -100,6 +100,45 @@ class OracleEngine:
         self.cand = (cu[order], cv[order], cf[order])
         return len(cu)
 
+    # sharded closure (distributed._closure_sharded): the rank's sub-range of a block as
+    # (key, first attempt) pairs, the gathered lists re-assembled into the attempt-indexed pair
+    # array, first occurrences kept -- the same candidates as closure_sample by construction
+    def closure_begin(self, attempts, iteration):
+        self._clo = (orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration), int(attempts))
+        self._clo_got = []
+        self._clo_next = 0
+        return max(1, min(orc.CLOSURE_ROUNDS, max(int(attempts), 1)))
+
+    def closure_block_sample(self, block, lo, hi, out):
+        assert block == self._clo_next, "closure blocks go in order"
+        p = self._clo[0][lo:hi].astype(np.int64)
+        t = np.arange(lo, hi, dtype=np.int64)
+        ok = (p[:, 0] >= 0) & (p[:, 0] != p[:, 1])
+        key = (np.minimum(p[:, 0], p[:, 1]) << 32) | np.maximum(p[:, 0], p[:, 1])
+        key, t = key[ok], t[ok]
+        _, first = np.unique(key, return_index=True)   # one entry per pair: its first attempt
+        rows = np.stack([key[first], t[first]], 1).reshape(-1)
+        out.numpy()[:rows.size] = rows
+        return len(first)
+
+    def closure_block_add(self, block, pairs, count):
+        assert block == self._clo_next, "closure blocks go in order"
+        if count:
+            self._clo_got.append(pairs.numpy()[:2 * count].reshape(-1, 2).copy())
+        self._clo_next += 1
+
+    def closure_finish(self):
+        attempts = self._clo[1]
+        pairs = np.full((max(attempts, 1), 2), -1, np.int32)
+        for g in self._clo_got:
+            pairs[g[:, 1], 0] = g[:, 0] >> 32
+            pairs[g[:, 1], 1] = g[:, 0] & 0xffffffff
+        dummy = np.zeros((1, self.g.N), np.int32)
+        cu, cv, _, cf = orc.closure_from_pairs(1, self.kept, pairs[:attempts], dummy, 1)
+        order = np.lexsort((cv, cu))
+        self.cand = (cu[order], cv[order], cf[order])
+        return len(cu)
+
     def closure_partial(self, out):
         cu, cv, _ = self.cand
         out.numpy()[:len(cu)] = (self.lab[:, cu] == self.lab[:, cv]).sum(0)

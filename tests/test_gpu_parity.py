@@ -627,3 +627,76 @@ def test_repair_many_isolates_bit_exact(fcmod):
         for a, b in zip(eng.get_graph(), cpu.get_graph()):
             np.testing.assert_array_equal(a, b)
         eng.close()
+
+
+def _sharded_closure(eng, attempts, world, order_rng):
+    """distributed._closure_sharded's schedule on ONE engine: every block's W sub-ranges drawn
+    one after the other (the ranks), their lists concatenated in a shuffled rank order."""
+    blocks = eng.closure_begin(attempts, 0)
+    for b in range(blocks):
+        t0, t1 = attempts * b // blocks, attempts * (b + 1) // blocks
+        lists = []
+        for r in range(world):
+            lo, hi = t0 + (t1 - t0) * r // world, t0 + (t1 - t0) * (r + 1) // world
+            buf = torch.empty(2 * max(hi - lo, 1), dtype=torch.int64, device="cuda")
+            k = eng.closure_block_sample(b, lo, hi, buf)
+            lists.append(buf[:2 * k].clone())
+        order = order_rng.permutation(world)
+        allp = torch.cat([lists[g] for g in order]) if lists else None
+        eng.closure_block_add(b, allp, int(allp.numel() // 2))
+    return eng.closure_finish()
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_closure_sharded_equals_single(fcmod, world):
+    """The multi-GPU closure (each block's attempts split over W ranks, lists all-gathered,
+    fc_closure_block_add) leaves exactly fc_closure_sample's candidates: graph, weights and
+    ages after closure_apply equal the single-rank device run (itself pinned to the CPU model
+    by test_repair_many_isolates_bit_exact and the full-run tests)."""
+    case, g = _lfr1k_graph()
+    lab = case.cd_batches[0]
+    graphs = []
+    for sharded in (False, True):
+        eng = fcmod.Engine(seed=5)
+        eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+        eng.set_labels(lab)
+        part = dev_i32(eng.m)
+        eng.consensus_partial(0, part)
+        eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)
+        nc = _sharded_closure(eng, g.m, world, np.random.default_rng(world)) if sharded else \
+            eng.closure_sample(g.m, 0)
+        assert nc > 0
+        cnt = dev_i32(nc)
+        eng.closure_partial(cnt)
+        eng.closure_apply(0, case.n_p, case.delta, cnt, 0)
+        graphs.append(eng.get_graph())
+        eng.close()
+    for a, b in zip(*graphs):
+        np.testing.assert_array_equal(a, b)
+    print("W=%d: %d candidates, graph %d edges" % (world, nc, len(graphs[1][0])))
+
+
+def test_closure_block_api_errors(fcmod):
+    """Blocks must go in order, ranges must lie inside their block, outputs must be large
+    enough (FastConsensusError, nothing drawn)."""
+    from fastconsensus_amd import FastConsensusError
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=5)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    eng.set_labels(case.cd_batches[0])
+    part = dev_i32(eng.m)
+    eng.consensus_partial(0, part)
+    eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)
+    buf = torch.empty(2 * g.m, dtype=torch.int64, device="cuda")
+    with pytest.raises(FastConsensusError):
+        eng.closure_block_sample(0, 0, 10, buf)                    # before closure_begin
+    blocks = eng.closure_begin(g.m, 0)
+    assert blocks == 8
+    t1 = g.m // blocks
+    with pytest.raises(FastConsensusError):
+        eng.closure_block_sample(1, t1, t1 + 5, buf)               # block 0 not added yet
+    with pytest.raises(FastConsensusError):
+        eng.closure_block_sample(0, 0, t1 + 1, buf)                # past the block
+    with pytest.raises(FastConsensusError):
+        eng.closure_finish()                                       # blocks missing
+    eng.close()
