@@ -9,10 +9,13 @@ copy of the graph; the only data-path exchanges are
 both travel as uint8 when n_p <= 255 (k_last + 1 and counts are in [0, n_p]): a quarter
 of the int32 bytes on every xGMI ring hop;
 after which threshold, check, repair and the graph rebuild run replicated and
-deterministically -- no graph broadcast.  The triadic closure is split: each of its blocks'
-attempts are divided over the ranks (the counter-based RNG is keyed by the attempt index),
-and the ranks' (pair, first attempt) lists are all-gathered once per block, so every rank
-appends the same candidates (_closure_sharded).  The final
+deterministically -- no graph broadcast.  The triadic closure runs replicated too (same
+counter-based RNG on every rank) unless shard_closure=True: then each closure block's
+attempts are divided over the ranks and their (pair, first attempt) lists all-gathered
+(_closure_sharded, same candidates).  Measured on LFR-1M it does not pay: half the
+attempts yield a candidate, and the per-candidate work (dedup, append, growing the closure
+graph) stays on every rank -- 4.7 ms per rank at W = 8 against 6.0 ms replicated, before
+the ~116 MB all-gathered per iteration (profiles/r03_closure_shard_time.json).  The final
 partitions are all-gathered to rank 0.  The loop mirrors fc_run (capi.cpp) step for step,
 so W ranks produce bit-identical results to one GPU.
 
@@ -82,11 +85,11 @@ def _closure_sharded(engine, attempts, iteration, world, rank, device):
 
 
 def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True, out=None,
-                shard_closure=True):
+                shard_closure=False):
     """Returns (labels [n_p][N] on rank 0 (None elsewhere), stats dict).  `out`: optional
     C-contiguous int32 host array [n_p][N] that rank 0 downloads into (see Engine.run).
-    shard_closure: split the closure's attempts over the ranks (world > 1); False draws all
-    of them on every rank (same result)."""
+    shard_closure: split the closure's attempts over the ranks (world > 1; same result);
+    default False: every rank draws all of them (see the module docstring)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     r0, r1 = shard(n_p, rank, world)
@@ -110,7 +113,7 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
 
 
 def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out=None,
-          shard_closure=True):
+          shard_closure=False):
     mine = r1 - r0
     engine.reset_graph()
     n, _, L = engine.graph_info()
