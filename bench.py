@@ -248,6 +248,9 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="experiment: any engine option (fastconsensus_amd._lib option names), repeatable")
     ap.add_argument("--n-p", type=int, default=0, help="experiment: override the config's n_p")
+    ap.add_argument("--gather-out", action="store_true",
+                    help="N>1: all-gather the labelings to rank 0 and download there (default: one shared-memory "
+                         "host array, each rank writes its rows)")
     ap.add_argument("--resident", action="store_true",
                     help="experiment: time the loop only (graph loaded once before timing)")
     ap.add_argument("--engine-model", action="store_true",
@@ -329,6 +332,19 @@ def main():
     # fresh 256 MB array costs ~20 ms of OS page zeroing on first touch, which is the
     # allocator's cost, not the path's; the PCIe download itself stays inside every step
     host_out = np.zeros((cfg["n_p"], n), np.int32) if rank == 0 else None
+    # N > 1: one shared-memory host array for the node; each rank downloads its own replica
+    # rows over its own PCIe link (no device all-gather, no n_p*n download through rank 0)
+    shared = None
+    if world > 1 and not args.gather_out:
+        from fastconsensus_amd.distributed import SharedOutput, shard as _shard
+        shared = SharedOutput(cfg["n_p"], n)
+        if shared.array is None:
+            log("[rank %d] /dev/shm cannot hold the labelings: all-gather to rank 0 instead" % rank)
+            shared = None
+        else:
+            a0, a1 = _shard(cfg["n_p"], rank, world)
+            shared.array[a0:a1] = 0        # fault this rank's pages in before timing
+            host_out = shared.array
 
     def sync():
         if not model:
@@ -349,7 +365,8 @@ def main():
         if world == 1 and not model:
             _, st = eng.run(algo, cfg["n_p"], cfg["tau"], cfg["delta"], out=host_out)
         else:
-            _, st = run_sharded(eng, algo, cfg["n_p"], cfg["tau"], cfg["delta"], device=dev, out=host_out)
+            _, st = run_sharded(eng, algo, cfg["n_p"], cfg["tau"], cfg["delta"], device=dev, out=host_out,
+                                out_shared=shared is not None)
         sync()
         t2 = time.perf_counter()
         return st, t1 - t, t2 - t1
@@ -477,7 +494,10 @@ def main():
             "step_value_median": float(np.median([p["partition_edges"] / p["ms"] * 1e3 for p in per_step])),
             "step_value_min": float(np.min([p["partition_edges"] / p["ms"] * 1e3 for p in per_step])),
             "loop_ms_per_step": 1e3 * loop_s / args.steps,
-            "dist": {"backend": backend if world > 1 else None, "world_size": world},
+            "dist": {"backend": backend if world > 1 else None, "world_size": world,
+                     "labels_out": (None if world == 1 else
+                                    "shared host array, each rank its rows" if shared is not None else
+                                    "all-gather, rank 0 downloads")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "phase_ms_per_step_rank0": phases,
@@ -486,6 +506,9 @@ def main():
             result["engine"] = "cpu-model (TEST HOOK: oracle-backed model of the engine, not the product)"
             result["value"] = None
         print(json.dumps(result))
+    if shared is not None:
+        host_out = None            # noqa: F841 (the last view of the shared array)
+        shared.close()
 
 
 if __name__ == "__main__":

@@ -22,6 +22,8 @@ so W ranks produce bit-identical results to one GPU.
 The driver only needs an "engine" with the step API of fastconsensus_amd.Engine; buffers
 are torch tensors on the engine's device (RCCL) or on the CPU (gloo, used by the tests).
 """
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -84,12 +86,59 @@ def _closure_sharded(engine, attempts, iteration, world, rank, device):
     return engine.closure_finish()
 
 
+class SharedOutput:
+    """The run's [n_p][n] int32 host labelings in POSIX shared memory, mapped by every rank of
+    the node (collective: all ranks construct it).  Passed as run_sharded(out=..., out_shared=
+    True), each rank downloads ITS replica rows over its own PCIe link straight into the
+    array -- no device all-gather of n_p*n labels and no 256 MB download through rank 0.
+    `array` is None (callers fall back to the gather) when /dev/shm cannot hold it: tmpfs
+    does not reserve pages, and a write past its limit would be a SIGBUS."""
+
+    def __init__(self, n_p, n):
+        from multiprocessing import resource_tracker, shared_memory
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.shm, self.array = None, None
+        size = max(4 * int(n_p) * int(n), 4)
+        name = None
+        if self.rank == 0:
+            try:
+                st = os.statvfs("/dev/shm")
+                if st.f_bavail * st.f_frsize >= size + size // 8 + (64 << 20):
+                    self.shm = shared_memory.SharedMemory(create=True, size=size)
+                    name = self.shm.name
+            except OSError:
+                name = None
+        obj = [name]
+        if dist.is_initialized():
+            dist.broadcast_object_list(obj, src=0)
+        name = obj[0]
+        if name is None:
+            return
+        if self.rank != 0:
+            self.shm = shared_memory.SharedMemory(name=name)
+            resource_tracker.unregister(self.shm._name, "shared_memory")   # rank 0 owns (unlinks) it
+        self.array = np.ndarray((n_p, n), np.int32, buffer=self.shm.buf)
+
+    def close(self):
+        """Collective.  Drop every view of `array` first."""
+        if dist.is_initialized():
+            dist.barrier()
+        self.array = None
+        if self.shm is not None:
+            self.shm.close()
+            if self.rank == 0:
+                self.shm.unlink()
+            self.shm = None
+
+
 def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, gather=True, out=None,
-                shard_closure=False):
+                shard_closure=False, out_shared=False):
     """Returns (labels [n_p][N] on rank 0 (None elsewhere), stats dict).  `out`: optional
     C-contiguous int32 host array [n_p][N] that rank 0 downloads into (see Engine.run).
     shard_closure: split the closure's attempts over the ranks (world > 1; same result);
-    default False: every rank draws all of them (see the module docstring)."""
+    default False: every rank draws all of them (see the module docstring).
+    out_shared: `out` is the same host array on every rank (SharedOutput.array): each rank
+    writes its own rows, rank 0 returns it once all have."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     r0, r1 = shard(n_p, rank, world)
@@ -97,7 +146,7 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     on_gpu = str(device).startswith("cuda")
     if not on_gpu:
         return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out,
-                     shard_closure)
+                     shard_closure, out_shared)
     # engine kernels and torch/RCCL ops on ONE explicit stream: no cross-stream races
     # (torch's default stream is the legacy null stream, which the engine cannot adopt)
     stream = torch.cuda.Stream(device=device)
@@ -106,14 +155,14 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     try:
         with torch.cuda.stream(stream):
             return _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out,
-                         shard_closure)
+                         shard_closure, out_shared)
     finally:
         stream.synchronize()
         engine.set_stream(None)
 
 
 def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank, r0, r1, louv, out=None,
-          shard_closure=False):
+          shard_closure=False, out_shared=False):
     mine = r1 - r0
     engine.reset_graph()
     n, _, L = engine.graph_info()
@@ -166,6 +215,13 @@ def _loop(engine, algo, n_p, tau, delta, device, max_iters, gather, world, rank,
     st["m_final"] = m
     if mine > 0:
         engine.cd(algo, r0, mine, n_p, FINAL_PASS_ITER + it)         # final pass :383-392
+    if gather and world > 1 and out_shared and out is not None:
+        # every rank downloads its rows into the shared host array; the barrier orders the
+        # writes before rank 0 hands the array back
+        if mine > 0:
+            engine.get_labels_into(out[r0:r1], renumber=True)
+        dist.barrier()
+        return (out if rank == 0 else None), st
     if not gather or world == 1:
         if mine > 0 and out is not None and world == 1:
             engine.get_labels_into(out, renumber=True)

@@ -33,9 +33,12 @@ def test_gpus2_launches_two_ranks_bit_identical():
     one = _line(_run(["--gpus", "1"]))
     two = _line(_run(["--gpus", "2"]))
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
-    assert two["dist"] == {"backend": "gloo", "world_size": 2}
+    assert two["dist"] == {"backend": "gloo", "world_size": 2, "labels_out": "shared host array, each rank its rows"}
     assert two["config"]["iterations"] == one["config"]["iterations"]
     assert two["config"]["m_final"] == one["config"]["m_final"]
+    gat = _line(_run(["--gpus", "2", "--gather-out"]))
+    assert gat["dist"]["labels_out"] == "all-gather, rank 0 downloads"
+    assert gat["config"]["m_final"] == one["config"]["m_final"]
     assert two["config"]["parallelism"] == "replica-sharded x2"
     # the test hook never claims a throughput
     assert one["value"] is None and "TEST HOOK" in one["engine"]

@@ -33,24 +33,36 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, algo, n_p, tau, delta, out_path, shard_closure=False):
+def _worker(rank, world, port, algo, n_p, tau, delta, out_path, shard_closure=False, shared_out=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from fastconsensus_amd.distributed import run_sharded
+        from fastconsensus_amd.distributed import SharedOutput, run_sharded
         from tests.cpu_engine import OracleEngine
         N, e = _graph()
         eng = OracleEngine(seed=17, sigma=_sigma(N))
         eng.load_graph(N, e[:, 0], e[:, 1])
-        host = np.full((n_p, N), -9, np.int32) if rank == 0 else None   # rank 0 downloads into it
+        so = None
+        if shared_out:      # every rank writes its rows into one shared host array
+            so = SharedOutput(n_p, N)
+            assert so.array is not None
+            so.array[...] = -9
+            host = so.array
+        else:
+            host = np.full((n_p, N), -9, np.int32) if rank == 0 else None   # rank 0 downloads into it
         labels, st = run_sharded(eng, algo, n_p, tau, delta, device="cpu", max_iters=50, out=host,
-                                 shard_closure=shard_closure)
+                                 shard_closure=shard_closure, out_shared=shared_out)
         if rank == 0:
             assert labels is host
             u, v, w, age = eng.get_graph()
             np.savez(out_path, labels=labels, u=u, v=v, w=w, age=age, iters=st["iterations"],
                      pe=st["partition_edges"])
+        else:
+            assert labels is None
+        if so is not None:
+            labels = host = None
+            so.close()
     finally:
         dist.destroy_process_group()
 
@@ -67,16 +79,18 @@ def _single(algo, n_p, tau, delta):
 
 # n_p=10 louvain runs 9 consensus iterations on this graph (closure + repair every time);
 # shard_closure: each closure block's attempts split over the ranks, lists all-gathered
-@pytest.mark.parametrize("world,algo,n_p,tau,shard_closure",
-                         [(2, 0, 10, 0.2, False), (2, 1, 4, 0.8, False), (3, 0, 12, 0.2, False),
-                          (2, 2, 10, 0.2, False), (2, 3, 6, 0.2, False), (3, 4, 5, 0.6, False),
-                          (2, 0, 10, 0.2, True), (3, 0, 12, 0.2, True), (3, 1, 4, 0.8, True)])
-def test_sharded_equals_single_rank(world, algo, n_p, tau, shard_closure):
+# shared_out: the final labelings land in one shared-memory host array, each rank its rows
+@pytest.mark.parametrize("world,algo,n_p,tau,shard_closure,shared_out",
+                         [(2, 0, 10, 0.2, False, False), (2, 1, 4, 0.8, False, False), (3, 0, 12, 0.2, False, False),
+                          (2, 2, 10, 0.2, False, False), (2, 3, 6, 0.2, False, False), (3, 4, 5, 0.6, False, False),
+                          (2, 0, 10, 0.2, True, False), (3, 0, 12, 0.2, True, False), (3, 1, 4, 0.8, True, False),
+                          (3, 0, 10, 0.2, False, True), (2, 1, 4, 0.8, False, True)])
+def test_sharded_equals_single_rank(world, algo, n_p, tau, shard_closure, shared_out):
     ref_labels, ref_graph, ref_st = _single(algo, n_p, tau, 0.02)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r0.npz")
-        mp.spawn(_worker, args=(world, _free_port(), algo, n_p, tau, 0.02, out, shard_closure), nprocs=world,
-                 join=True)
+        mp.spawn(_worker, args=(world, _free_port(), algo, n_p, tau, 0.02, out, shard_closure, shared_out),
+                 nprocs=world, join=True)
         z = np.load(out)
         np.testing.assert_array_equal(z["labels"], ref_labels)
         for a, b in zip((z["u"], z["v"], z["w"], z["age"]), ref_graph):
