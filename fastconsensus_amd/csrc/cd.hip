@@ -848,21 +848,30 @@ __global__ __launch_bounds__(ATB) void k_apply(CDArgs a, int bucket) {
 // differs from v's (Traag et al.'s fast local moving rule: a neighbour that ended in v's
 // community is not revisited), comparing the labels the sweep left -- deterministic, unlike a
 // mark at move time, which would race with the round's other moves.
+// A wave takes its 64 vertices' movers one at a time and walks each mover's row with all 64
+// lanes (one row = one round of independent gathers), instead of one thread walking a row
+// while the wave's non-movers idle.
 __global__ __launch_bounds__(256) void k_mark_lm(CDArgs a) {
     const int r = blockIdx.y;
     if (!a.active[r] || !a.track[r]) return;     // block-uniform: this sweep was not tracked
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= a.N) return;
     uint8_t* mv = a.mvf + (int64_t)r * a.N;
-    if (!mv[v]) return;
-    mv[v] = 0;
+    const bool moved = v < a.N && mv[v];         // no early exit: every lane walks the rows
+    if (moved) mv[v] = 0;
+    unsigned long long m = __ballot(moved);
+    const int lane = threadIdx.x & 63;
+    const int64_t v0 = v - lane;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     uint8_t* aff = a.aff + (int64_t)r * a.N;
-    const int4 vr = a.vrec[v];
-    const int32_t d = labr[vr.w];
-    const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
-    for (int64_t j = rb; j < re; ++j)
-        if (labr[a.colp[j]] != d) aff[a.col[j]] = 1;
+    while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int4 vr = a.vrec[v0 + b];
+        const int32_t d = labr[vr.w];
+        const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
+        for (int64_t j = rb + lane; j < re; j += 64)
+            if (labr[a.colp[j]] != d) aff[a.col[j]] = 1;
+    }
 }
 
 // End of sweep: python-louvain stops a level when the pass gained < 1e-7 modularity or
