@@ -248,6 +248,8 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="experiment: any engine option (fastconsensus_amd._lib option names), repeatable")
     ap.add_argument("--n-p", type=int, default=0, help="experiment: override the config's n_p")
+    ap.add_argument("--no-pin-out", action="store_true",
+                    help="leave the preallocated output array pageable (default: page-locked at allocation)")
     ap.add_argument("--gather-out", action="store_true",
                     help="N>1: all-gather the labelings to rank 0 and download there (default: one shared-memory "
                          "host array, each rank writes its rows)")
@@ -345,6 +347,16 @@ def main():
             a0, a1 = _shard(cfg["n_p"], rank, world)
             shared.array[a0:a1] = 0        # fault this rank's pages in before timing
             host_out = shared.array
+
+    # the output array is page-locked at allocation (like its first touch: the allocator's cost),
+    # so each step's download is one DMA; --no-pin-out measures the pageable copy
+    pinned = None
+    if not model and not args.no_pin_out and host_out is not None:
+        from fastconsensus_amd.core import PinnedHost
+        from fastconsensus_amd.distributed import shard as _shard2
+        p0, p1 = _shard2(cfg["n_p"], rank, world)
+        pinned = PinnedHost(host_out[p0:p1] if shared is not None else host_out)
+        log("[rank %d] output array pinned: %s" % (rank, pinned.ok))
 
     def sync():
         if not model:
@@ -494,6 +506,7 @@ def main():
             "step_value_median": float(np.median([p["partition_edges"] / p["ms"] * 1e3 for p in per_step])),
             "step_value_min": float(np.min([p["partition_edges"] / p["ms"] * 1e3 for p in per_step])),
             "loop_ms_per_step": 1e3 * loop_s / args.steps,
+            "output_array": ("page-locked at allocation" if pinned is not None and pinned.ok else "pageable"),
             "dist": {"backend": backend if world > 1 else None, "world_size": world,
                      "labels_out": (None if world == 1 else
                                     "shared host array, each rank its rows" if shared is not None else
@@ -506,6 +519,8 @@ def main():
             result["engine"] = "cpu-model (TEST HOOK: oracle-backed model of the engine, not the product)"
             result["value"] = None
         print(json.dumps(result))
+    if pinned is not None:
+        pinned.release()
     if shared is not None:
         host_out = None            # noqa: F841 (the last view of the shared array)
         shared.close()

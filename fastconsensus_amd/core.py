@@ -38,6 +38,25 @@ def algo_id(algorithm):
     return None
 
 
+class PinnedHost:
+    """Page-locks (hipHostRegister) a caller-owned host array that the engine downloads labelings
+    into (Engine.run(out=...), run_sharded(out=...)): the device -> host copy then runs as one
+    direct DMA instead of being staged through the runtime's pinned bounce buffers.  A caller that
+    keeps one output array pins it once, next to allocating it.  `ok` is False (and nothing is
+    pinned) when the runtime refuses.  release() before the array is freed."""
+
+    def __init__(self, array):
+        import torch
+        self._rt = torch._C._cudart
+        self._ptr, self._n = int(array.ctypes.data), int(array.nbytes)
+        self.ok = self._n > 0 and int(self._rt.cudaHostRegister(self._ptr, self._n, 0)) == 0
+
+    def release(self):
+        if self.ok:
+            self._rt.cudaHostUnregister(self._ptr)
+            self.ok = False
+
+
 class Engine:
     """One device-resident consensus engine (one GPU, one host thread)."""
 

@@ -1656,15 +1656,18 @@ void store_order(Ctx& c) {
     // The first sweeps place almost every vertex (LFR-1M: 89 % and 52 % of the vertices move
     // in sweeps 0 and 1, < 6 % from sweep 3 on), so a few sweeps give the storage order; the
     // remaining one-replica sweeps would only pay latency (FC_ORDER_SWEEPS, default 4).
-    const int ms = c.max_sweeps;
+    const int ms = c.max_sweeps, mb = c.buckets;
     c.max_sweeps = std::max(1, std::min(ms, c.order_sweeps));
+    c.buckets = std::max(1, c.order_buckets);
     try {
         cd_run(c, FC_ALGO_LOUVAIN, 0, 1, 1, 0x3fffffff);
     } catch (...) {
         c.max_sweeps = ms;
+        c.buckets = mb;
         throw;
     }
     c.max_sweeps = ms;
+    c.buckets = mb;
     uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, N);
     uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, N);
     int32_t* i1 = (int32_t*)ensure<int64_t>(c.midx, N);

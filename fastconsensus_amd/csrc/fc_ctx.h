@@ -160,6 +160,9 @@ struct Ctx {
     bool order_pass = false;        // store_order()'s CD run (int64 totals, see there)
     int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
     int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 4;   // sweeps of that pass
+    // its buckets per sweep: the pass only permutes label storage (results are identical), and
+    // 4 big launches per sweep beat 32 small ones (LFR-1M load 9.9 -> 8.0 ms, tools/r03_ordb.sh)
+    int order_buckets = getenv("FC_ORDER_BUCKETS") ? atoi(getenv("FC_ORDER_BUCKETS")) : 4;
     DevBuf spos;                    // int32 [N]: storage slot of internal vertex v in every lab row
     int coarsen = 8;                // FC_OPT_COARSEN: 0 off, else the largest g (filtered sweeps in rounds of g buckets)
     double cd_min_dq = 1e-7;        // Louvain sweeps stop below this predicted gain (Leiden's move phase: 0)
