@@ -350,12 +350,11 @@ def main():
 
     # the output array is page-locked at allocation (like its first touch: the allocator's cost),
     # so each step's download is one DMA; --no-pin-out measures the pageable copy
+    # (one GPU only: the shared-memory array of N > 1 stays pageable)
     pinned = None
-    if not model and not args.no_pin_out and host_out is not None:
+    if not model and not args.no_pin_out and host_out is not None and world == 1:
         from fastconsensus_amd.core import PinnedHost
-        from fastconsensus_amd.distributed import shard as _shard2
-        p0, p1 = _shard2(cfg["n_p"], rank, world)
-        pinned = PinnedHost(host_out[p0:p1] if shared is not None else host_out)
+        pinned = PinnedHost(host_out)
         log("[rank %d] output array pinned: %s" % (rank, pinned.ok))
 
     def sync():
