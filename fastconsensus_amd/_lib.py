@@ -18,7 +18,8 @@ FC_ALGO_LEIDEN = 3       # leiden branch (:204-258, final pass :385-388)
 FC_ALGO_INFOMAP = 4      # infomap: the lpm loop (:260-310) around igraph Infomap (:268, :390)
 OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6, "tail_visits": 7,
            "coarsen": 8, "store": 9, "seed": 10, "closure_rounds": 11,
-           "prune_mark": 12, "infomap_trials": 13, "cd_engine": 14}
+           "prune_mark": 12, "infomap_trials": 13, "cd_engine": 14,
+           "rl_min_replicas": 15}
 ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 
 # Every symbol declared in include/fastconsensus_amd.h (checked by tests/test_capi_symbols.py)
@@ -48,6 +49,7 @@ class Stats(ctypes.Structure):
         ("decide_bytes", ctypes.c_int64),
         ("lv_decide_ms", ctypes.c_double), ("lv_decide_launches", ctypes.c_int64), ("lv_decide_bytes", ctypes.c_int64),
         ("lv_heavy_ms", ctypes.c_double), ("lv_heavy_launches", ctypes.c_int64), ("lv_heavy_bytes", ctypes.c_int64),
+        ("rl_decide_ms", ctypes.c_double), ("rl_decide_launches", ctypes.c_int64), ("rl_decide_bytes", ctypes.c_int64),
     ]
 
     def as_dict(self):

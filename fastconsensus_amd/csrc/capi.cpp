@@ -36,10 +36,10 @@ void timer_end(Ctx& c, int slot, int b) {
 }
 void timer_collect(Ctx& c, fc_stats* st) {
     Timer& t = c.timer;
-    double ms[7] = {0, 0, 0, 0, 0, 0, 0};
-    int64_t launches[7] = {0, 0, 0, 0, 0, 0, 0};
+    double ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t launches[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!t.pool.empty()) FC_HIP(hipStreamSynchronize(c.stream));
-    for (int s = 0; s < 7; ++s) {
+    for (int s = 0; s < 8; ++s) {
         for (auto& pr : t.spans[s]) {
             float x = 0.f;
             FC_HIP(hipEventElapsedTime(&x, t.pool[pr.first], t.pool[pr.second]));
@@ -55,6 +55,7 @@ void timer_collect(Ctx& c, fc_stats* st) {
         st->decide_ms = ms[4]; st->decide_launches = launches[4];
         st->lv_decide_ms = ms[5]; st->lv_decide_launches = launches[5];
         st->lv_heavy_ms = ms[6]; st->lv_heavy_launches = launches[6];
+        st->rl_decide_ms = ms[7]; st->rl_decide_launches = launches[7];
     }
     c.prof = fc_stats{};
 }
@@ -68,7 +69,8 @@ static bool known_algo(int algo) {
 static void run_cd(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
     if (algo == FC_ALGO_LEIDEN) leiden_run(c, rbegin, rcount, n_p_total, iteration);
     else if (algo == FC_ALGO_INFOMAP) infomap_run(c, rbegin, rcount, n_p_total, iteration);
-    else if (cd_rl_supported(c, algo)) cd_run_rl(c, algo, rbegin, rcount, n_p_total, iteration);
+    else if (c.cd_engine == 2) cd_run_hybrid(c, algo, rbegin, rcount, n_p_total, iteration);
+    else if (c.cd_engine == 1 && cd_rl_supported(c, algo)) cd_run_rl(c, algo, rbegin, rcount, n_p_total, iteration);
     else cd_run(c, algo, rbegin, rcount, n_p_total, iteration);
 }
 
@@ -139,7 +141,7 @@ void fc_destroy(fc_ctx* ctx) {
     (void)hipStreamSynchronize(c.stream);
     c.g.release();
     c.g0.release();
-    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.rl_lmask, &c.rl_vmask, &c.rl_aff, &c.rl_mvf, &c.rl_vlist, &c.rl_vcount, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
+    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.rl_lmask, &c.rl_vmask, &c.rl_aff, &c.rl_mvf, &c.rl_vlist, &c.rl_vcount, &c.rl_tot, &c.rl_state, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
                       &c.heavy_scratch, &c.wnew, &c.flag, &c.pos, &c.ku, &c.kv, &c.kw, &c.kage, &c.krowptr,
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
@@ -204,7 +206,8 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_CLOSURE_ROUNDS: FC_REQUIRE(value >= 1, FC_EINVAL, "closure_rounds >= 1"); c.closure_rounds = (int)value; break;
         case FC_OPT_PRUNE_MARK: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "prune_mark must be 0, 1 or 2"); c.prune_mark = (int)value; break;
         case FC_OPT_INFOMAP_TRIALS: FC_REQUIRE(value >= 1, FC_EINVAL, "infomap trials >= 1"); c.infomap_trials = (int)value; break;
-        case FC_OPT_CD_ENGINE: FC_REQUIRE(value == 0 || value == 1, FC_EINVAL, "cd_engine must be 0 or 1"); c.cd_engine = (int)value; break;
+        case FC_OPT_CD_ENGINE: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "cd_engine must be 0, 1 or 2"); c.cd_engine = (int)value; break;
+        case FC_OPT_RL_MIN_REPLICAS: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_replicas >= 1"); c.rl_min_replicas = value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }

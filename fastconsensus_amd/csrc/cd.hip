@@ -133,6 +133,8 @@ struct CDArgs {
     unsigned long long* sacc;    // [n_r][4] light-kernel vertices / entries / candidates, summed by k_sweep_end
     double min_dq;               // Louvain stop: a sweep gaining < min_dq (python-louvain __MIN 1e-7; Leiden's
                                  // move phase 0: run until a sweep moves nothing)
+    int shared_full;             // FC_OPT_CD_ENGINE=2: a replica's full sweeps visit the batch's SHARED order
+                                 // (SHARED_RG), its filtered sweeps its own (oracle tw_replica shared = 2)
 };
 
 // Sweep order of replica rg: a random permutation of the vertices, or of chunks of CHUNK
@@ -145,6 +147,13 @@ __device__ __forceinline__ Perm sweep_perm(const CDArgs& a, int rg, int sweep) {
     Perm P = make_perm(a.perm_n, stream_key(a.seed, (uint32_t)rg, a.iter, (uint32_t)sweep, 1));
     if (a.chunk) P.off = stream_key(a.seed, (uint32_t)rg, a.iter, (uint32_t)sweep, 3) & (CHUNK - 1);
     return P;
+}
+// Key of replica r's visit order this sweep: its own, or the shared one while its sweeps are
+// full in the hybrid (the replica-lane engine runs those sweeps when the batch is wide enough;
+// this engine runs them for narrow batches and for replicas still full after the hand-off).
+__device__ __forceinline__ bool rep_full(const CDArgs& a, int r);
+__device__ __forceinline__ int order_rg(const CDArgs& a, int r, bool full) {
+    return (a.shared_full && full) ? (int)SHARED_RG : a.rbase + r;
 }
 // Vertex at sweep position p, or -1 for a padding slot.
 __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, int64_t p) {
@@ -623,7 +632,7 @@ __global__ __launch_bounds__(DTB) __attribute__((amdgpu_waves_per_eu(8))) void k
     const int rg = a.rbase + r;
     int32_t v = -1;
     if (in_range) {
-        if (rr.z & RR_FULL) v = pos_vertex(a, sweep_perm(a, rg, sweep),
+        if (rr.z & RR_FULL) v = pos_vertex(a, sweep_perm(a, order_rg(a, r, true), sweep),
                                            (int64_t)rr.x + di);
         else v = a.list[(int64_t)r * a.PN + rr.x + di];                  // vertex ids
     }
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         const bool full = rep_full(a, r);
         const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
         const bool dpush = a.track[2 * a.n_r + r] != 0, dtrans = a.track[3 * a.n_r + r] != 0;
-        const Perm P = sweep_perm(a, rg, sweep);
+        const Perm P = sweep_perm(a, order_rg(a, r, full), sweep);
         const int32_t stamp = sweep + 1;
         for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
         if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
@@ -1290,7 +1299,8 @@ static int64_t count_heavy(Ctx& c, int64_t thr) {
     return c.hpin[0];
 }
 
-void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration, int shared_full,
+            const CDHandoff* h) {
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
     FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
     const int sl0 = timer_begin(c);
@@ -1326,9 +1336,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     if (g.max_deg > LIGHT_MAX_DEG) n_heavy = count_heavy(c, LIGHT_MAX_DEG);
     int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * (size_t)std::max<int64_t>(n_heavy, 1) + 3);
     uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
-    FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));
     int32_t* track = ensure<int32_t>(c.track, 4 * (size_t)rcount);
-    FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
+    if (!h) {
+        FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));
+        FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
+    }
     int32_t* list = ensure<int32_t>(c.vlist, (size_t)rcount * PN);
     // rrec int4 [B][n_r] | lcnt [B][n_r] | cntfine [n_r][B] | loff [n_r][B+1] | cursor [n_r][B] | gco [n_r] | info [8]
     const size_t plan_ints = 4 * (size_t)B * rcount + (size_t)B * rcount + (size_t)rcount * B +
@@ -1351,7 +1363,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     if (heavy_slots > HEAVY_LDS_SLOTS)   // one slice per heavy-kernel block, or per tail-kernel block (replica)
         hscr = ensure<int32_t>(c.heavy_scratch, (size_t)std::max(HEAVY_GRID, rcount) * 2 * heavy_slots);
 
-    {
+    if (!h) {
         std::vector<int32_t> ones(rcount, (g.M2 > 0) ? 1 : 0);
         FC_HIP(hipMemcpyAsync(active, ones.data(), sizeof(int32_t) * rcount, hipMemcpyHostToDevice, c.stream));
         sync(c);  // `ones` is pageable host memory
@@ -1360,8 +1372,14 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     dim3 ig(nblk(N), rcount);
     const int32_t* spos = c.spos.as<int32_t>();
     const int32_t* sinv = c.sinv.as<int32_t>();
-    if (tot32) k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int32_t*)tot, louv ? 1 : 0);
-    else k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int64_t*)tot, louv ? 1 : 0);
+    if (h) {   // a hybrid batch from its first filtered sweep: the replica-lane engine's state
+        FC_REQUIRE(tot32 || !louv, FC_ESTATE, "hybrid hand-off needs int32 totals");
+        h->fill(c, h->user, lab, (int32_t*)tot, aff, track, active);
+    } else if (tot32) {
+        k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int32_t*)tot, louv ? 1 : 0);
+    } else {
+        k_cd_init<int64_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int64_t*)tot, louv ? 1 : 0);
+    }
     FC_REQUIRE(!louv || (double)g.max_kdeg * (double)g.M2 < 4.0e18, FC_ELIMIT,
                "edge weights too large for exact int64 modularity gains");
 
@@ -1374,6 +1392,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.nlab = nlab; a.rev = g.crev.as<int32_t>(); a.m2 = m2;
     a.red = red; a.sacc = sacc;
     a.min_dq = c.cd_min_dq;
+    a.shared_full = shared_full;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
     a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
     a.hcap = std::max<int64_t>(n_heavy, 1);
@@ -1410,7 +1429,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
     const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
     int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..4] | n_active[0] at [6]
-    int sweep = 0;
+    const int sweep0 = h ? h->sweep0 : 0;
+    int sweep = sweep0;
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
         FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
@@ -1421,7 +1441,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         sync(c);
         const int rounds = hinfo[0];
         const unsigned long long visits = *(unsigned long long*)(hinfo + 2);
-        if (rounds == 0 || (sweep > 0 && hinfo[6] == 0)) break;   // every replica has stopped
+        if (rounds == 0 || (sweep > sweep0 && hinfo[6] == 0)) break;   // every replica has stopped
         // small sweeps (every replica visits <= tail_visits vertices): hand every remaining
         // sweep to the per-replica tail kernel (it takes the flags as its first worklist)
         if (c.tail_visits > 0 && (int64_t)hinfo[4] <= c.tail_visits && B <= TAIL_MAXB) {

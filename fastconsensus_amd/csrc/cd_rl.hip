@@ -45,7 +45,6 @@ constexpr int DM = 64;                  // light rows: degree <= DM
 constexpr int VPWMAX = 8;               // sub-groups per wave (lane groups of >= 8 replicas)
 constexpr int RL_CHUNK = 16;            // = cd.hip CHUNK (chunked visit orders)
 constexpr int32_t DONE = -1;            // merged / own / empty table entry (labels are >= 0)
-constexpr uint32_t SHARED_RG = 0xffffffffu;   // stream key of the shared visit order (oracle TW_SHARED_RG)
 constexpr int NSH = 16;                 // counter shards per replica
 constexpr int RF = 8;                   // fields: 0 dq, 1 unstable, 2 moves, 3 visits, 4 entries, 5 cands, 6 units
 constexpr double DQ_SCALE = 1099511627776.0;   // 2^40 fixed point for predicted dQ (as cd.hip)
@@ -100,6 +99,8 @@ struct RL {
     int32_t* hscratch;           // global tables for rows past the LDS table
     int64_t hslots;
     double min_dq;
+    int hybrid;                  // FC_OPT_CD_ENGINE=2: stop before the first sweep that filters a replica
+                                 // (cd.hip takes the batch over from there: cd_run_hybrid)
 };
 
 __device__ __forceinline__ Perm rl_perm(const RL& a, int sweep) {
@@ -150,7 +151,8 @@ __global__ void k_rl_init(int64_t N, int ldT, const int64_t* kdeg, int32_t* lab,
 }
 // labT [N][ldT] -> lab [n_r][N] in slot order (what labels_to_host and the Leiden code read):
 // 64 slots x 64 replicas per tile through LDS, label rows read and slot rows written as whole
-// 256-byte runs (the inverse of cd.hip k_transpose)
+// 256-byte runs (the inverse of cd.hip k_transpose).  sinv = nullptr: vertex order (the hybrid
+// hands totT [N][ldT] over as cd.hip's tot [n_r][N] this way).
 __global__ __launch_bounds__(256) void k_rl_export(int64_t N, int n_r, int ldT, const int32_t* labT, const int32_t* sinv,
                                                    int32_t* lab) {
     __shared__ int32_t t[64][65];
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256) void k_rl_export(int64_t N, int n_r, int ldT, 
     const int64_t s0 = (int64_t)blockIdx.x * 64;
     const int r0 = blockIdx.y * 64;
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
-    if (ty == 0) sv[tx] = s0 + tx < N ? sinv[s0 + tx] : -1;
+    if (ty == 0) sv[tx] = s0 + tx < N ? (sinv ? sinv[s0 + tx] : (int32_t)(s0 + tx)) : -1;
     __syncthreads();
     for (int ss = ty; ss < 64; ss += 4) {
         const int32_t v = sv[ss];
@@ -193,6 +195,11 @@ __global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int list
         if (a.prune && a.track[a.n_r + r]) atomicOr((unsigned long long*)&s_flt[r >> 6], 1ull << (r & 63));
     }
     __syncthreads();
+    if (a.hybrid) {   // a replica filters this sweep: cd.hip takes over, the flags stay for it (block-uniform)
+        uint64_t any = 0;
+        for (int b = 0; b < a.banks; ++b) any |= s_act[b] & s_flt[b];
+        if (any) return;
+    }
     const Perm P = rl_perm(a, sweep);
     const int64_t v0 = (int64_t)blockIdx.x * LTB * LPER + threadIdx.x;
 #pragma unroll
@@ -1064,13 +1071,14 @@ __global__ __launch_bounds__(RTB) void k_rl_mark_lm(RL a) {
 
 // End of a sweep, per replica (cd.hip k_sweep_end without the push / transition modes):
 // python-louvain stops a level when the pass gained < min_dq or moved nothing; igraph LPA
-// when no visited vertex was unstable.  n_active_out: [0] active after, [2..3] u64 moves,
+// when no visited vertex was unstable.  n_active_out: [0] active after, [1] active replicas whose
+// next sweep is filtered, [2..3] u64 moves,
 // [4..5] u64 replica-sweeps so far, [6..7] u64 visits of this sweep.
 template <bool LOUV>
 __global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
-    __shared__ int cnt, cnt0;
+    __shared__ int cnt, cnt0, nflt;
     __shared__ unsigned long long mv, vis;
-    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; mv = 0; vis = 0; }
+    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; nflt = 0; mv = 0; vis = 0; }
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1090,12 +1098,16 @@ __global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
             if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < a.min_dq;
             else stop = f[1] == 0;
             if (stop) a.active[r] = 0;
-            else atomicAdd(&cnt, 1);
+            else {
+                atomicAdd(&cnt, 1);
+                if (a.prune && a.track[a.n_r + r]) atomicAdd(&nflt, 1);   // filters next sweep
+            }
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         n_active_out[0] = cnt;
+        n_active_out[1] = nflt;
         *(unsigned long long*)(n_active_out + 2) = mv;
         *(unsigned long long*)(n_active_out + 4) += (unsigned long long)cnt0;
         *(unsigned long long*)(n_active_out + 6) = vis;
@@ -1105,6 +1117,27 @@ __global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
 inline unsigned nb(int64_t n, int tb) {
     int64_t b = (n + tb - 1) / tb;
     return (unsigned)(b < 1 ? 1 : b);
+}
+
+// Hybrid hand-off: the affected bits [banks][N] as cd.hip's per-replica flags u8 [n_r][N].
+__global__ __launch_bounds__(256) void k_rl_aff_export(int64_t N, const uint64_t* aff, uint8_t* out) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int r = blockIdx.y;
+    if (v < N) out[(int64_t)r * N + v] = (uint8_t)((aff[(int64_t)(r >> 6) * N + v] >> (r & 63)) & 1ull);
+}
+
+// CDHandoff::fill: the batch's state in cd.hip's layout (labels in slot order, int32 totals by
+// community, affected flags, tracked / filtered flags with pull mode, active flags)
+void rl_handoff_fill(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint8_t* aff, int32_t* track,
+                     int32_t* active) {
+    const RL& a = *(const RL*)user;
+    const dim3 tg(nb(a.N, 64), (a.n_r + 63) / 64);
+    k_rl_export<<<tg, 256, 0, c.stream>>>(a.N, a.n_r, a.ldT, a.lab, c.sinv.as<int32_t>(), lab);
+    if (tot) k_rl_export<<<tg, 256, 0, c.stream>>>(a.N, a.n_r, a.ldT, a.tot, nullptr, tot);
+    k_rl_aff_export<<<dim3(nb(a.N, 256), a.n_r), 256, 0, c.stream>>>(a.N, a.aff, aff);
+    FC_HIP(hipMemcpyAsync(track, a.track, 8 * (size_t)a.n_r, hipMemcpyDeviceToDevice, c.stream));
+    FC_HIP(hipMemsetAsync(track + 2 * a.n_r, 0, 8 * (size_t)a.n_r, c.stream));
+    FC_HIP(hipMemcpyAsync(active, a.active, 4 * (size_t)a.n_r, hipMemcpyDeviceToDevice, c.stream));
 }
 
 }  // namespace
@@ -1120,12 +1153,28 @@ void rl_layout(int n_r, int* LG, int* VPW, int* banks, int* ldT) {
     *ldT = n_r > 64 ? 64 * *banks : lg;
 }
 
-bool cd_rl_supported(const Ctx& c, int algo) {
-    return c.cd_engine == 1 && !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && c.g.M2 <= 0x7fffffffll &&
+// the graph and options the replica-lane kernels handle (int32 totals, 32-bit row offsets)
+static bool cd_rl_fits(const Ctx& c, int algo) {
+    return !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && c.g.M2 <= 0x7fffffffll &&
            c.g.m < (int64_t(1) << 31) && (c.chunk == 0 || c.chunk == RL_CHUNK);
 }
+bool cd_rl_supported(const Ctx& c, int algo) { return c.cd_engine == 1 && cd_rl_fits(c, algo); }
 
-void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+// FC_OPT_CD_ENGINE=2.  Semantics (oracle tw_replica shared = 2): a replica's sweeps visit the
+// batch's shared order while they are full, and its own order from its first filtered sweep.
+// The replica-lane engine runs the full sweeps -- one row walk and one coalesced label read per
+// neighbour for every replica of a wave -- and cd.hip runs the rest, where per-replica lists,
+// coarse rounds and the tail kernel pay.  A batch too narrow for replica lanes runs on cd.hip
+// throughout, with the same semantics (its full sweeps use the shared order too), so results
+// never depend on how replicas are sharded over GPUs.
+void cd_run_hybrid(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
+    if (cd_rl_fits(c, algo) && (int64_t)rcount >= c.rl_min_replicas)
+        cd_run_rl(c, algo, rbegin, rcount, n_p_total, iteration, true);
+    else
+        cd_run(c, algo, rbegin, rcount, n_p_total, iteration, 1);
+}
+
+void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration, bool hybrid) {
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
     FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
     const int sl0 = timer_begin(c);
@@ -1155,7 +1204,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     // sortable keys (label << wbits | weight) need N << wbits < 2^31; else the LDS merge
     const bool pack = ((int64_t)(N - 1) << (a.unitw ? 0 : a.wbits)) < (int64_t(1) << 31);
     a.lab = ensure<int32_t>(c.labT, (size_t)N * ldT);
-    a.tot = louv ? ensure<int32_t>(c.tot, (size_t)N * ldT) : nullptr;
+    a.tot = louv ? ensure<int32_t>(c.rl_tot, (size_t)N * ldT) : nullptr;
     a.dec = ensure<int32_t>(c.dec, (size_t)PN * ldT);
     a.list = (int4*)ensure<int4>(c.vlist, (size_t)PN);
     a.lmask = (uint64_t*)ensure<uint64_t>(c.rl_lmask, (size_t)PN * banks);
@@ -1178,8 +1227,9 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     // Leiden-style marks (cd.hip): consensus graphs, or every graph with prune_mark = 2
     a.lm = ((g.max_w > 1 || c.prune_mark == 2) && c.prune && c.prune_mark >= 1) ? 1 : 0;
     a.min_dq = c.cd_min_dq;
+    a.hybrid = hybrid ? 1 : 0;
     // per-replica state: active i32 [n_r] | track i32 [2 n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active [8]
-    char* rs = (char*)ensure<char>(c.rep_state, (size_t)rcount * (12 + 8 * NSH * RF + 32) + 512);
+    char* rs = (char*)ensure<char>(c.rl_state, (size_t)rcount * (12 + 8 * NSH * RF + 32) + 512);
     a.active = (int32_t*)rs;
     a.track = a.active + rcount;
     a.red = (unsigned long long*)(rs + (((size_t)rcount * 12 + 255) & ~size_t(255)));
@@ -1200,11 +1250,11 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
 
     k_rl_init<<<nb(N * ldT, 256), 256, 0, c.stream>>>(N, ldT, g.kdeg.as<int64_t>(), a.lab, a.tot);
 
-    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // boff [B+1] | n_active copy
+    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // n_active[0..1] copy
     std::vector<int32_t> hb(2 * (nseg + 1));   // boff | voff
     const unsigned lgrid = nb(N, LTB * LPER);
     const size_t lcount_lds = sizeof(unsigned long long) * 2 * banks + 2 * sizeof(int) * nseg;
-    int sweep = 0;
+    int sweep = 0, handoff = -1;
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         const int listed = (c.prune && sweep > 0) ? 1 : 0;
         FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * nseg, c.stream));
@@ -1214,9 +1264,11 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         FC_HIP(hipMemcpyAsync(hb.data(), a.boff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost, c.stream));
         FC_HIP(hipMemcpyAsync(hb.data() + nseg + 1, a.voff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost,
                               c.stream));
-        FC_HIP(hipMemcpyAsync(hinfo, n_active, 4, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hinfo, n_active, 8, hipMemcpyDeviceToHost, c.stream));
         sync(c);
-        if (hb[nseg] == 0 || (sweep > 0 && hinfo[0] == 0)) break;   // every replica has stopped
+        if (sweep > 0 && hinfo[0] == 0) break;                      // every replica has stopped
+        if (hybrid && sweep > 0 && hinfo[1] > 0) { handoff = sweep; break; }   // a replica filters: cd.hip
+        if (hb[nseg] == 0) break;
         k_rl_list_fill<<<lgrid, LTB, 2 * sizeof(int) * nseg, c.stream>>>(a, sweep);
         // visit mode when the replicas of an entry are mostly idle (few visits per listed entry):
         // a wave per entry would run mostly empty lanes
@@ -1274,7 +1326,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     else k_rl_decide_lds<false><<<grid_of(n), RTB, 0, c.stream>>>(a, k, sweep);
                 }
             }
-            timer_end(c, 4, ev);
+            timer_end(c, 7, ev);
             if (hb[(k + 1) * NCLS] > hb[k * NCLS + NCLS - 1]) {
                 if (louv) k_rl_heavy<true><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
                 else k_rl_heavy<false><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
@@ -1300,11 +1352,13 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             t_last = t_now;
         }
     }
-    // labels for the consensus kernels (labT, native) and the slot-order rows everything else reads
-    int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
-    k_rl_export<<<dim3(nb(N, 64), (rcount + 63) / 64), 256, 0, c.stream>>>(N, rcount, ldT, a.lab, c.sinv.as<int32_t>(), lab);
-    c.ldT = ldT;
-    c.labT_valid = true;
+    if (handoff < 0) {
+        // labels for the consensus kernels (labT, native) and the slot-order rows everything else reads
+        int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
+        k_rl_export<<<dim3(nb(N, 64), (rcount + 63) / 64), 256, 0, c.stream>>>(N, rcount, ldT, a.lab, c.sinv.as<int32_t>(), lab);
+        c.ldT = ldT;
+        c.labT_valid = true;
+    }
     // statistics: replica-sweeps, visits, and the decide kernel's algorithmic bytes
     std::vector<unsigned long long> sa(4 * (size_t)rcount + 4);
     FC_HIP(hipMemcpyAsync(sa.data(), a.sacc, sa.size() * 8, hipMemcpyDeviceToHost, c.stream));
@@ -1328,9 +1382,14 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         s->cd_sweeps += (int64_t)rep_sweeps;
         s->cd_vertex_visits += (int64_t)vis;
         s->cd_edge_visits += (int64_t)ent;
-        s->decide_bytes += (int64_t)db;
+        s->rl_decide_bytes += (int64_t)db;
     }
     timer_end(c, 0, sl0);
+    if (handoff >= 0) {
+        if (c.trace) fprintf(stderr, "[fc] rl it=%d hands over to cd.hip at sweep %d\n", iteration, handoff);
+        const CDHandoff h{handoff, rl_handoff_fill, &a};
+        cd_run(c, algo, rbegin, rcount, n_p_total, iteration, 1, &h);
+    }
 }
 
 }  // namespace fc

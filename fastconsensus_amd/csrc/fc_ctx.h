@@ -82,8 +82,8 @@ struct Graph {
 struct Timer {
     bool on = false;
     std::vector<hipEvent_t> pool;
-    // cd, consensus, closure, rebuild, decide, lv decide, lv heavy
-    std::vector<std::pair<int, int>> spans[7];
+    // cd, consensus, closure, rebuild, decide, lv decide, lv heavy, rl decide
+    std::vector<std::pair<int, int>> spans[8];
     size_t next = 0;
 };
 
@@ -115,7 +115,10 @@ struct Ctx {
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
-    int cd_engine = 0;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip, default), 1 replica-lane (cd_rl.hip)
+    int cd_engine = 0;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip, default), 1 replica-lane (cd_rl.hip), 2 hybrid
+    // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many replicas
+    int64_t rl_min_replicas = getenv("FC_RL_MIN_REPLICAS") ? atoll(getenv("FC_RL_MIN_REPLICAS")) : 16;
+    DevBuf rl_tot, rl_state;        // replica-lane totals [N][ldT] and per-replica state (kept apart from cd.hip's)
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable
@@ -184,16 +187,34 @@ struct Ctx {
     int64_t* hpin = nullptr;        // pinned host scratch (64 int64)
 };
 
+struct Ctx;
+// State the replica-lane engine hands to cd_run at the first filtered sweep of a hybrid batch
+// (FC_OPT_CD_ENGINE=2, cd_rl.hip): fill() writes it in cd.hip's layout on c.stream -- labels
+// [n_r][N] in slot order, int32 totals [n_r][N], affected flags u8 [n_r][N], track int32
+// [4][n_r] (tracked, filtered, push, transition) and active [n_r] -- and the sweeps go on from
+// sweep0.
+struct CDHandoff {
+    int sweep0;
+    void (*fill)(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint8_t* aff, int32_t* track, int32_t* active);
+    const void* user;
+};
+
 // graph.cpp
 void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v);
 void graph_build_csr(Ctx& c, Graph& g);
 void graph_merge_next(Ctx& c, int64_t n_added);
 void graph_copy(Ctx& c, Graph& dst, const Graph& src);
 // cd.cpp
-void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
+// shared_full: full sweeps in the batch's shared order (the hybrid's semantics); h: resume a
+// hybrid batch handed over by the replica-lane engine
+void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration, int shared_full = 0,
+            const CDHandoff* h = nullptr);
 // cd_rl.hip: the replica-lane engine (louvain / lpm batches when cd_rl_supported)
 bool cd_rl_supported(const Ctx& c, int algo);
-void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
+void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration, bool hybrid = false);
+// FC_OPT_CD_ENGINE=2: full sweeps in one shared order (on the replica-lane engine when the batch
+// holds >= rl_min_replicas and the graph fits it), filtered sweeps on cd.hip in per-replica orders
+void cd_run_hybrid(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration);
 void store_order(Ctx& c);             // Ctx::spos from a one-replica Louvain run (FC_OPT_STORE)
 void slot_maps(Ctx& c);               // Ctx::sinv / tpos / snpos from spos
 void graph_slots(Ctx& c, Graph& g);   // g.colp = spos[g.col]

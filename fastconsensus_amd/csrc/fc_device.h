@@ -36,6 +36,9 @@ FC_HD uint32_t stream_key(uint64_t seed, uint32_t rg, uint32_t iter, uint32_t sw
     z = mix64(z ^ ((uint64_t)iter << 32 | sweep) ^ ((uint64_t)salt << 56));
     return (uint32_t)(z ^ (z >> 32));
 }
+// Stream key of the visit order every replica of a batch shares (FC_OPT_CD_ENGINE 1 and 2:
+// cd_rl.hip, and cd.hip's full sweeps in the hybrid; oracle TW_SHARED_RG).
+constexpr uint32_t SHARED_RG = 0xffffffffu;
 
 // Random bijection on [0, n): balanced 4-round Feistel network on 2*hb bits with cycle
 // walking.  Sweep order of a replica = perm(0), perm(1), ...; bucket k of a sweep is the

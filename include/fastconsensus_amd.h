@@ -82,6 +82,11 @@ typedef struct fc_stats {
     double lv_heavy_ms;
     int64_t lv_heavy_launches;
     int64_t lv_heavy_bytes;
+    /* replica-lane decide kernels (cd_rl.hip k_rl_decide*: the full sweeps of the hybrid,
+     * FC_OPT_CD_ENGINE=2, and every sweep at 1); decide_* above covers cd.hip's k_decide_light */
+    double rl_decide_ms;
+    int64_t rl_decide_launches;
+    int64_t rl_decide_bytes;
 } fc_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------- */
@@ -147,8 +152,14 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 a batch visits the vertices in ONE shared random order per sweep
                                 (ties broken per replica), labels node-major, one wave deciding a
                                 vertex for up to 64 replicas; no coarse rounds or tail kernel.
-                                Both are bit-exact against oracle/fc_oracle.c orc_engine_cd
-                                (shared = 0 / 1).                                                */
+                                2: the hybrid -- a replica's sweeps visit the batch's shared order
+                                while they are full and its own order from its first filtered
+                                (pruned) sweep on; the replica-lane engine runs the full sweeps of a
+                                batch of >= FC_OPT_RL_MIN_REPLICAS replicas, cd.hip everything else.
+                                All three are bit-exact against oracle/fc_oracle.c orc_engine_cd
+                                (shared = 0 / 1 / 2).                                            */
+#define FC_OPT_RL_MIN_REPLICAS 15 /* hybrid: the smallest batch whose full sweeps run on the
+                                replica-lane engine (default 16).  Speed only: same results.     */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

@@ -889,14 +889,15 @@ static int tw_coarse(i64 N, i64 V, int B, int gmax) {
     return g;
 }
 
-/* shared: the replica-lane engine (cd_rl.hip) -- every replica visits the vertices in the SAME
+/* shared: 1 the replica-lane engine (cd_rl.hip) -- every replica visits the vertices in the SAME
  * per-(iteration, sweep) order (its stream key uses TW_SHARED_RG in place of the replica
- * index); tie keys stay per replica.  0: the classic engine's per-replica orders. */
+ * index); tie keys stay per replica.  0: the classic engine's per-replica orders.  2: the
+ * hybrid (FC_OPT_CD_ENGINE=2) -- the shared order while the replica's sweeps visit every
+ * vertex, its own order from its first filtered (pruned) sweep on. */
 #define TW_SHARED_RG 0xffffffffu
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
                       u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
                       int coarsen, int lm, int shared, i32* lab) {
-    const uint32_t prg = shared ? TW_SHARED_RG : rg;   /* key of the visit order */
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
@@ -917,6 +918,8 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     int active = M2 > 0, sweep = 0;
     int track_now = 0, prune_now = 0;   /* adaptive pruning state (engine: k_sweep_end) */
     for (; sweep < max_sweeps && active; ++sweep) {
+        const int filtered = prune && sweep > 0 && prune_now;
+        const uint32_t prg = (shared == 1 || (shared == 2 && !filtered)) ? TW_SHARED_RG : rg;   /* order key */
         const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, prg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
         const uint32_t off = tw_chunk_off(chunk, seed, prg, iter, (uint32_t)sweep);

@@ -158,8 +158,17 @@ def _lfr1k_graph():
 # tail: FC_OPT_TAIL_VISITS -- 0 keeps every sweep on the multi-kernel path; a huge value
 # hands every sweep after the first two to the per-replica tail kernel (classic engine)
 TAILS = [0, 1 << 40]
-# FC_OPT_CD_ENGINE: 0 classic (default, cd.hip), 1 replica-lane (cd_rl.hip; twin shared=1, coarsen=0)
-ENGINES = [0, 1]
+# FC_OPT_CD_ENGINE: 0 classic (cd.hip), 1 replica-lane (cd_rl.hip; twin shared=1, coarsen=0),
+# 2 hybrid (twin shared=2): test engine 2 runs the full sweeps on the replica-lane engine
+# (rl_min_replicas=1), test engine 3 the same semantics on cd.hip alone (a batch too narrow)
+ENGINES = [0, 1, 2, 3]
+SHARED = {0: 0, 1: 1, 2: 2, 3: 2}
+
+
+def _set_engine(eng, engine):
+    eng.set_option("cd_engine", min(engine, 2))
+    if engine >= 2:
+        eng.set_option("rl_min_replicas", 1 if engine == 2 else 1 << 30)
 
 
 def _engine(eng, engine, tail=0, coarsen=0):
@@ -170,10 +179,10 @@ def _engine(eng, engine, tail=0, coarsen=0):
             pytest.skip("replica-lane engine: no tail kernel / coarse rounds")
         eng.set_option("cd_engine", 1)
         return {"shared": 1, "coarsen": 0}
-    eng.set_option("cd_engine", 0)
+    _set_engine(eng, engine)
     eng.set_option("tail_visits", tail)
     eng.set_option("coarsen", coarsen)
-    return {"shared": 0, "coarsen": coarsen}
+    return {"shared": SHARED[engine], "coarsen": coarsen}
 
 
 @pytest.mark.parametrize("engine", ENGINES)
@@ -488,8 +497,8 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     case, _ = _lfr1k_graph()
     e = case.edges_file
     eng = fcmod.Engine(seed=17)
-    eng.set_option("cd_engine", engine)
-    if engine == 0:
+    _set_engine(eng, engine)
+    if engine != 1:
         eng.set_option("tail_visits", tail)
     elif tail:
         pytest.skip("replica-lane engine: no tail kernel")
@@ -501,7 +510,8 @@ def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, re
     sigma = eng.node_map()
     if not relabel:
         assert np.array_equal(sigma, np.arange(case.N))
-    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune, sigma=sigma, shared=engine, coarsen=0 if engine else 8)
+    cpu = OracleEngine(seed=17, chunk=chunk, prune=prune, sigma=sigma, shared=SHARED[engine],
+                       coarsen=0 if engine == 1 else 8)
     cpu.load_graph(case.N, e[:, 0], e[:, 1])
     exp_labels, exp_st = run_sharded(cpu, algo, n_p, tau, 0.02, device="cpu", max_iters=50)
     labels, st = eng.run(algo, n_p, tau, 0.02)
