@@ -101,10 +101,11 @@ def test_c2_lpa_vs_restatement_and_reference_run(fcmod):
 
 def test_c2_lpa_detectability_edge_vs_reference_run(fcmod):
     """LFR n=1000 mu=0.55 (LPA's detectability edge): a replica either finds the communities
-    or floods to one.  The reference run's first LPA batch (lfr1k_mu055_lpm_np20) has 8 of 20
-    structured replicas.  Device (64 replicas) vs restatement (64): structured fraction within
-    0.25 of each other (about 3 binomial standard errors) and NMI of the structured replicas
-    >= restatement - 0.03 and >= reference run - 0.05."""
+    or floods to one.  The reference run's first LPA batch, pooled over seeds 21..40
+    (lfr1k_mu055_lpm_firstbatch.json, no seed selection), has 100 of 400 structured replicas.
+    Device (64 replicas) vs restatement (64): structured fraction within 0.25 of each other
+    (about 3 binomial standard errors) and NMI of the structured replicas >= restatement - 0.03
+    and >= the reference runs' - 0.05."""
     case = golden_io.load("lfr1k_mu055_lpm_np20")
     planted = np.load(golden_io.GOLDEN + "/lfr1k_mu055_synth_planted.npy")[case.z["nodes"]]
     g = orc.EdgeGraph.from_lines(case.N, case.edges_file)
@@ -117,7 +118,12 @@ def test_c2_lpa_detectability_edge_vs_reference_run(fcmod):
         return len(ok) / len(L), (float(np.mean([nmi(planted, x) for x in ok])) if ok else 0.0)
     fd, nd = split(dev)
     fr, nr = split(ref)
-    fu, nu = split(runl)
+    import json
+    with open(golden_io.GOLDEN + "/lfr1k_mu055_lpm_firstbatch.json") as f:
+        pool = json.load(f)
+    fu = pool["structured_fraction"]
+    nu = float(np.mean([x for per_seed in pool["structured_nmi"] for x in per_seed]))
+    assert split(runl)[0] * 20 == pool["structured"][-1]     # the fixture is the seed-21 run
     print("C2 lpa (mu=0.55) structured fraction / NMI: gpu %.3f / %.4f | restatement %.3f / %.4f | "
           "reference run %.3f / %.4f" % (fd, nd, fr, nr, fu, nu))
     assert fu > 0 and fd > 0
@@ -327,8 +333,18 @@ def test_device_closure_sampler_is_the_measured_one(fcmod, name):
         L = graphs[0].m
         nc = eng.closure_sample(L, 0)
         pairs = orc.closure_sample_pairs(kept, L, seed, 0)
-        cu, cv, _, _ = orc.closure_from_pairs(case.algo, kept, pairs, case.cd_batches[0], case.n_p)
+        cu, cv, cw, cfirst = orc.closure_from_pairs(case.algo, kept, pairs, case.cd_batches[0], case.n_p)
         assert nc == len(cu)
+        # the candidates themselves: keys, first attempts (the edge age the adjacency model
+        # reads, (iteration + 1) << 40 | attempt) and co-membership weights (0 for lpm)
+        cnt = torch.zeros(max(nc, 1), dtype=torch.int32, device="cuda")
+        eng.closure_partial(cnt)
+        eng.closure_apply(case.algo, case.n_p, case.delta, cnt, 0)
+        gu, gv, gw, gage = eng.get_graph()
+        new = (gage >> 39) == 2                   # closure edges of iteration 0 (repair edges: 3)
+        got = sorted(zip(gu[new].tolist(), gv[new].tolist(), gw[new].tolist(), (gage[new] & ((1 << 39) - 1)).tolist()))
+        exp = sorted(zip(cu.tolist(), cv.tolist(), cw.tolist(), cfirst.tolist()))
+        assert got == exp
 
 
 # ------------------------------------------------------------------------------ CLI end to end

@@ -135,7 +135,33 @@ def test_consensus_second_iteration_weights(fcmod):
     eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)
     ku, kv, kw, _ = eng.get_nextgraph()
     np.testing.assert_array_equal(kw, traces[1]["kept"].w)
-    assert (traces[1]["consensus_w"] > case.n_p).any() or True
+    # the w + (n_p - 1 - k_last) branch (fast_consensus.py:153-159) with w' > n_p: on the same
+    # iteration-1 graph, partition 0 random and every later partition one community, so an edge
+    # of prior weight w not in {0, n_p} that partition 0 splits gets w + n_p - 1 > n_p
+    g1 = graphs[1]
+    assert ((g1.w != 0) & (g1.w != case.n_p) & (g1.w > 1)).any()
+    lab2 = np.zeros((case.n_p, case.N), np.int32)
+    lab2[0] = np.random.default_rng(5).integers(0, 4, case.N)
+    eng.reset_graph()
+    eng.set_labels(case.cd_batches[0])
+    part = dev_i32(eng.m)
+    eng.consensus_partial(0, part)
+    eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)
+    eng.closure_set_pairs(case.pair_batches[0], 0)
+    eng.closure_partial(cnt)
+    eng.closure_apply(0, case.n_p, case.delta, cnt, 0)
+    eng.set_labels(lab2)
+    part = dev_i32(eng.m)
+    eng.consensus_partial(0, part)
+    conv, kept, unc = eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)
+    w_ref = orc.consensus(0, g1, lab2, case.n_p)
+    keep = orc.threshold(w_ref, case.tau, case.n_p)
+    ku, kv, kw, _ = eng.get_nextgraph()
+    np.testing.assert_array_equal(ku, g1.u[keep])
+    np.testing.assert_array_equal(kv, g1.v[keep])
+    np.testing.assert_array_equal(kw, w_ref[keep])
+    assert (kw > case.n_p).any(), "no edge took the w + (n_p - 1 - k_last) > n_p branch"
+    assert unc == orc.check(w_ref[keep], case.n_p, case.delta)[1]
     eng.close()
 
 
