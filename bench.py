@@ -176,10 +176,10 @@ def cpu_baseline(n, u, v, cfg, seed):
                          math.ceil(n_p / reps), full_s)}
 
 
-def load_traffic(config):
-    """HBM bytes per decide launch from profiles/pmc_<config>.json, only when that profile was
-    taken on a library built from the same sources as the one being timed (csrc_hash);
-    returns (bytes or None, note)."""
+def load_traffic(config, kernel="k_decide_light"):
+    """HBM bytes per launch of the decide kernel `kernel` (k_decide_light, or the k_rl_decide
+    family) from profiles/pmc_<config>.json, only when that profile was taken on a library built
+    from the same sources as the one being timed (csrc_hash); returns (bytes or None, note)."""
     from fastconsensus_amd.build import built_hash
     p = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
     if not os.path.exists(p):
@@ -190,7 +190,8 @@ def load_traffic(config):
     if not lib or prof != lib:
         return None, "PMC profile %s is from csrc %s, the timed library from %s: traffic not attached" % (
             os.path.basename(p), prof, lib)
-    return d.get("decide_hbm_bytes_per_launch"), "traffic from %s (csrc %s)" % (os.path.basename(p), prof)
+    key = "rl_decide_hbm_bytes_per_launch" if kernel == "k_rl_decide" else "decide_hbm_bytes_per_launch"
+    return d.get(key), "traffic of %s from %s (csrc %s)" % (kernel, os.path.basename(p), prof)
 
 
 def load_lv_traffic(config, kernel):
@@ -427,29 +428,35 @@ def main():
 
     roof, phases = None, None
     if tim is not None:
-        # roofline of the dominant kernel (light local-moving decide), measured with HIP
-        # events on the engine's stream over the timed region; bytes = the algorithmic model
-        launches = max(1, tim["decide_launches"])
-        avg_s = tim["decide_ms"] / launches / 1e3
-        bytes_per_launch = tim["decide_bytes"] / launches
-        achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        # roofline of the dominant kernel, measured with HIP events on the engine's stream over
+        # the timed region; bytes = the algorithmic model.  Two decide kernels share the CD
+        # batches of the hybrid engine (the default): the replica-lane k_rl_decide family (full
+        # sweeps) and cd.hip's k_decide_light (filtered sweeps); the one with more time is
+        # reported, both are listed under "kernels"
+        kern = {}
+        for key, name in (("decide", "k_decide_light"), ("rl_decide", "k_rl_decide")):
+            n_l = tim["%s_launches" % key]
+            if n_l:
+                a_s = tim["%s_ms" % key] / n_l / 1e3
+                b_l = tim["%s_bytes" % key] / n_l
+                ach = b_l / a_s / 1e9 if a_s > 0 else 0.0
+                kern[name] = {"launches": n_l, "avg_us": a_s * 1e6, "algorithmic_bytes_per_launch": b_l,
+                              "achieved": ach, "frac": ach / HBM_PEAK_GBS, "ms_per_step": tim["%s_ms" % key] / args.steps}
+        dom = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else "k_decide_light"
+        kd = kern.get(dom, {"launches": 0, "avg_us": 0.0, "algorithmic_bytes_per_launch": 0.0, "achieved": 0.0})
+        avg_s = kd["avg_us"] / 1e6
         if args.n_p <= 0:
-            traffic, traffic_note = load_traffic(args.config)
+            traffic, traffic_note = load_traffic(args.config, dom)
         else:
             traffic, traffic_note = None, "the PMC summary is for the config's n_p"
-        cd_engine = 0                          # FC_OPT_CD_ENGINE default (classic)
-        for kv in args.opt:
-            if kv.split("=", 1)[0] == "cd_engine":
-                cd_engine = int(kv.split("=", 1)[1])
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
-                "kernel": "%s<%s>" % ("k_rl_decide" if cd_engine == 1 and cfg["algo"] in ("louvain", "lpm")
-                                      else "k_decide_light", "true" if algo != 1 else "false"),
+        roof = {"bound": "hbm", "achieved": kd["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": kd["achieved"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
+                "kernel": "%s<%s>" % (dom, "true" if algo != 1 else "false"),
                 "note": (None if cfg["algo"] in ("louvain", "lpm") else
                          "the %s CD runs its own kernels (leiden.hip); this roofline covers the Louvain-engine "
                          "decide launches only" % cfg["algo"]),
-                "launches": tim["decide_launches"], "avg_us": avg_s * 1e6,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "launches": kd["launches"], "avg_us": kd["avg_us"],
+                "algorithmic_bytes_per_launch": kd["algorithmic_bytes_per_launch"], "kernels": kern,
                 # line traffic (PMC, L2 misses x 128 B) per second of decide time, against the
                 # measured ceiling of random 4-B gathers that miss L2 (tools/micro/gather.hip:
                 # ~56 G requests/s x 128 B, whether or not the Infinity Cache holds the line)
@@ -479,7 +486,7 @@ def main():
                         "launches": lv[dom]["launches"], "avg_us": lv[dom]["avg_us"],
                         "algorithmic_bytes_per_launch": lv[dom]["algorithmic_bytes_per_launch"], "kernels": lv}
         phases = {k: tim[k] / args.steps for k in ("cd_ms", "consensus_ms", "closure_ms", "rebuild_ms", "decide_ms",
-                                                    "lv_decide_ms", "lv_heavy_ms")}
+                                                    "rl_decide_ms", "lv_decide_ms", "lv_heavy_ms")}
 
     if rank == 0:
         cpu = None

@@ -1288,14 +1288,14 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         for (int k = 0; k < B; ++k) {
             const int64_t nb_all = hb[(k + 1) * NCLS] - hb[k * NCLS];
             if (nb_all <= 0) continue;
-            const int ev = timer_begin(c);
+            // each decide launch timed on its own (span 7: one span per launch, as rocprofv3 counts them)
             if (pack && vmode) {
                 for (int cls = 0; cls < NCLS - 1; ++cls) {
                     const int seg = k * NCLS + cls;
                     const int64_t n = hb[nseg + 1 + seg + 1] - hb[nseg + 1 + seg];
                     if (n <= 0) continue;
                     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 63) / 64, 8192));
-#define RL_LAUNCH(L, KK, U) k_rl_decide_v<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep)
+#define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide_v<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep); timer_end(c, 7, ev); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, true);
@@ -1310,7 +1310,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     const int64_t n = hb[seg + 1] - hb[seg];
                     if (n <= 0) continue;
                     const unsigned grid = grid_of(n);
-#define RL_LAUNCH(L, KK, U) k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep)
+#define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep); timer_end(c, 7, ev); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, true);
@@ -1322,11 +1322,12 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             } else {
                 const int64_t n = hb[k * NCLS + NCLS - 1] - hb[k * NCLS];
                 if (n > 0) {
+                    const int ev = timer_begin(c);
                     if (louv) k_rl_decide_lds<true><<<grid_of(n), RTB, 0, c.stream>>>(a, k, sweep);
                     else k_rl_decide_lds<false><<<grid_of(n), RTB, 0, c.stream>>>(a, k, sweep);
+                    timer_end(c, 7, ev);
                 }
             }
-            timer_end(c, 7, ev);
             if (hb[(k + 1) * NCLS] > hb[k * NCLS + NCLS - 1]) {
                 if (louv) k_rl_heavy<true><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
                 else k_rl_heavy<false><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);

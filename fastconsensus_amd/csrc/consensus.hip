@@ -163,6 +163,7 @@ __global__ void k_krowptr(int64_t n, const int64_t* rowptr, const int64_t* p2, i
 
 void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept_out,
                      int64_t* unconv_out) {
+    c.clo_next = -1;   // a sharded closure sequence (fc_closure_begin ...) read the previous kept graph
     const int sl = timer_begin(c);
     Graph& g = c.g;
     const int64_t m = g.m, cap = m + 1;
@@ -472,6 +473,7 @@ static void clo_append(Ctx& c, const Clo& b, int64_t n, int64_t t0, int r) {
 }
 
 void closure_sample(Ctx& c, int64_t attempts, int iteration) {
+    c.clo_next = -1;   // it resets the candidate table a sharded sequence was filling
     const int sl = timer_begin(c);
     const Clo b = clo_bufs(c, attempts);
     clo_reset(c, b);
@@ -580,6 +582,7 @@ int64_t closure_finish(Ctx& c) {
 }
 
 void closure_from_pairs(Ctx& c, int64_t npairs, const int32_t* pairs, int iteration) {
+    c.clo_next = -1;
     const int64_t cap = npairs > 0 ? npairs : 1;
     int32_t* dp = ensure<int32_t>(c.ckey, 2 * cap);
     if (npairs > 0) FC_HIP(hipMemcpyAsync(dp, pairs, sizeof(int32_t) * 2 * npairs, hipMemcpyHostToDevice, c.stream));

@@ -154,6 +154,7 @@ __global__ void k_scatter_unique(int64_t m, const uint64_t* key, const int64_t* 
 // device: validation, internal numbering, canonical keys, dedupe (stable radix sort keeps
 // the first occurrence = networkx adjacency age), CSR, label storage order.
 void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v) {
+    c.clo_next = -1;   // a sharded closure sequence is sized for the old graph
     FC_REQUIRE(n >= 1 && n < (int64_t(1) << 31), FC_EINVAL, "node count out of range");
     FC_REQUIRE(m >= 0 && m < (int64_t(1) << 31), FC_EINVAL, "edge count out of range");
     auto t_last = std::chrono::steady_clock::now();
@@ -273,6 +274,7 @@ void graph_to_host(Ctx& c, int64_t m, const int32_t* u, const int32_t* v, const 
 
 // graph = G.copy() (fast_consensus.py:131): device-to-device, the input stays resident.
 void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
+    c.clo_next = -1;
     const int64_t m = src.m > 0 ? src.m : 1, n = c.N;
     auto cp = [&](DevBuf& d, const DevBuf& s, size_t bytes) {
         d.ensure(bytes + 16);

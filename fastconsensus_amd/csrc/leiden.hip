@@ -1057,6 +1057,12 @@ enum {
 static_assert(B_END <= (int)(sizeof(((Ctx*)nullptr)->lv) / sizeof(DevBuf)), "Ctx::lv too small");
 
 // device max of ubo[i+1]-ubo[i] (int64) or of len[i] (int32): one atomic per block
+// Rows of [0, n) longer than thr entries (offsets ubo): what a level's heavy lists must hold.
+__global__ void k_count_long(int64_t n, const int64_t* ubo, int64_t thr, unsigned long long* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long b = __ballot(i < n && ubo[i + 1] - ubo[i] > thr);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+}
 __global__ void k_max_row(int64_t n, const int64_t* ubo, const int32_t* len, unsigned long long* out) {
     __shared__ unsigned long long sm[LTB / 64];
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1209,9 +1215,21 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         a.blist = I32(B_BLIST, nblk * LTB);
         a.btgt = I32(B_BTGT, nblk * LTB);
         a.bcnt = I32(B_BCNT, nblk);
-        a.hcap = nU;
-        a.heavy = I32(B_HEAVY, NTIER * nU);
-        a.htgt = I32(B_HTGT, NTIER * nU);
+        // each length tier's list holds at most the level's rows past the smallest heavy
+        // threshold (64 entries, k_lv_decide<.., 512, 4>), not nU each
+        {
+            unsigned long long* dcnt = (unsigned long long*)(c.hpin + 48);
+            unsigned long long* dd = (unsigned long long*)ensure<int64_t>(c.counters, 4);
+            FC_HIP(hipMemsetAsync(dd, 0, 8, c.stream));
+            const int64_t nrows = impl ? N : nU;
+            if (max_deg > 64)
+                k_count_long<<<nb(nrows), LTB, 0, c.stream>>>(nrows, impl ? g.rowptr.as<int64_t>() : cur.rowptr, 64, dd);
+            FC_HIP(hipMemcpyAsync(dcnt, dd, 8, hipMemcpyDeviceToHost, c.stream));
+            sync(c);
+            a.hcap = std::max<int64_t>(1, (int64_t)*dcnt * (impl ? n_r : 1));
+        }
+        a.heavy = I32(B_HEAVY, NTIER * a.hcap);
+        a.htgt = I32(B_HTGT, NTIER * a.hcap);
         int64_t hs = 64;   // global tables only for rows beyond the block's LDS table
         if (max_deg > HLIGHT)
             while (hs < 2 * (int64_t)max_deg) hs <<= 1;
@@ -1398,18 +1416,22 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         int64_t* hx = (int64_t*)c.hpin + 40;
         unsigned long long* dmax = (unsigned long long*)(misc + 2 * (int64_t)n_r + 2 + ((2 * n_r) & 1));
         FC_HIP(hipMemsetAsync(dmax, 0, 16, c.stream));
+        unsigned long long* dlong = (unsigned long long*)ensure<int64_t>(c.counters, 4);
+        FC_HIP(hipMemsetAsync(dlong, 0, 8, c.stream));
         k_max_row<<<nb(nUn), LTB, 0, c.stream>>>(nUn, ubo, nullptr, dmax);
+        k_count_long<<<nb(nUn), LTB, 0, c.stream>>>(nUn, ubo, LIGHT, dlong);   // rows k_ag_rows lists as heavy
         FC_HIP(hipMemcpyAsync(hx, ubo + nUn, 8, hipMemcpyDeviceToHost, c.stream));
         FC_HIP(hipMemcpyAsync(hx + 1, dmax, 8, hipMemcpyDeviceToHost, c.stream));
+        FC_HIP(hipMemcpyAsync(hx + 3, dlong, 8, hipMemcpyDeviceToHost, c.stream));
         sync(c);
-        const int64_t ubtot = hx[0], ubmax = hx[1];
+        const int64_t ubtot = hx[0], ubmax = hx[1], nlong = hx[3];
         int32_t* tcol = I32(B_TCOL, ubtot + 1);
         int32_t* tw = I32(B_TW, ubtot + 1);
         int32_t* olen = I32(B_OLEN, nUn + 1);
-        int32_t* agh = I32(B_AGH, NTIER * (nUn + 1));
+        const int64_t ahc = std::max<int64_t>(1, nlong);   // per-tier capacity: the heavy rows
+        int32_t* agh = I32(B_AGH, NTIER * ahc);
         FC_HIP(hipMemsetAsync(hcnt, 0, 4 * NTIER, c.stream));
         const unsigned agb = nb(nUn, LTB / 64);
-        const int64_t ahc = nUn + 1;
         if (impl) k_ag_rows<true><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc);
         else k_ag_rows<false><<<agb, LTB, 0, c.stream>>>(a, nUn, nid, moff, mlist, ubo, tcol, tw, olen, agh, hcnt, ahc);
         if (ubmax > LIGHT) {

@@ -91,8 +91,9 @@ class SharedOutput:
     the node (collective: all ranks construct it).  Passed as run_sharded(out=..., out_shared=
     True), each rank downloads ITS replica rows over its own PCIe link straight into the
     array -- no device all-gather of n_p*n labels and no 256 MB download through rank 0.
-    `array` is None (callers fall back to the gather) when /dev/shm cannot hold it: tmpfs
-    does not reserve pages, and a write past its limit would be a SIGBUS."""
+    `array` is None on every rank (callers fall back to the gather) when /dev/shm cannot hold
+    it -- tmpfs does not reserve pages, and a write past its limit would be a SIGBUS -- or when
+    the ranks are not all on one node (a rank elsewhere could not map it)."""
 
     def __init__(self, n_p, n):
         from multiprocessing import resource_tracker, shared_memory
@@ -100,7 +101,13 @@ class SharedOutput:
         self.shm, self.array = None, None
         size = max(4 * int(n_p) * int(n), 4)
         name = None
-        if self.rank == 0:
+        one_node = True
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            import socket
+            hosts = [None] * dist.get_world_size()
+            dist.all_gather_object(hosts, socket.gethostname())
+            one_node = len(set(hosts)) == 1
+        if self.rank == 0 and one_node:
             try:
                 st = os.statvfs("/dev/shm")
                 if st.f_bavail * st.f_frsize >= size + size // 8 + (64 << 20):
@@ -141,6 +148,10 @@ def run_sharded(engine, algo, n_p, tau, delta, device="cuda", max_iters=1000, ga
     writes its own rows, rank 0 returns it once all have."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    if out_shared and world > 1 and out is None:
+        # every rank must pass the shared array: a rank without it would take the all-gather
+        # path while the others wait in the shared path's barrier
+        raise ValueError("run_sharded(out_shared=True) needs the SharedOutput array on every rank")
     r0, r1 = shard(n_p, rank, world)
     louv = algo in (LOUVAIN, LOUVAIN_NC)    # louvain loop: check #1, closure counts, repair
     on_gpu = str(device).startswith("cuda")

@@ -735,4 +735,12 @@ def test_closure_block_api_errors(fcmod):
         eng.closure_block_sample(0, 0, t1 + 1, buf)                # past the block
     with pytest.raises(FastConsensusError):
         eng.closure_finish()                                       # blocks missing
+    # a begun sequence goes stale when the one-rank sampler, a consensus update or a graph
+    # reset runs in between (they reset the table and the graph the blocks read)
+    for stale in (lambda: eng.closure_sample(g.m, 0), lambda: eng.reset_graph(),
+                  lambda: eng.consensus_apply(0, case.n_p, case.tau, case.delta, part)):
+        eng.closure_begin(g.m, 0)
+        stale()
+        with pytest.raises(FastConsensusError):
+            eng.closure_block_sample(0, 0, 10, buf)
     eng.close()

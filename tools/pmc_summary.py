@@ -35,6 +35,8 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
             if "k_decide_light" in kern:   # per instance: <true, int> is the consensus runs' Louvain kernel
                 targs = kern.split("<", 1)[1].split(">")[0].replace(" ", "")
                 short = "k_decide_light<%s>" % {"true,int": "louvain", "false,int": "lpa"}.get(targs, targs)
+            elif re.search(r"k_rl_decide<", kern):   # the replica-lane decide family (every K / weight instance)
+                short = "k_rl_decide<%s>" % ("louvain" if "k_rl_decide<true" in kern.replace(" ", "") else "lpa")
             elif "k_lv_" in kern:       # Leiden / Infomap kernels: one entry per kernel (all instances)
                 # (anonymous-namespace names: "void fc::(anonymous namespace)::k_lv_decide<...>(...)")
                 short = re.search(r"(k_lv_\w+)", kern).group(1)
@@ -58,6 +60,15 @@ def main(prof_dir, config, out_dir="profiles", tag="r01"):
         hit, miss = d.get("TCC_HIT_sum", (None,))[0], d.get("TCC_MISS_sum", (None,))[0]
         if hit is not None and miss:
             summary["decide_l2_hit_rate"] = hit / (hit + miss)
+    rl = [k for k in per if k == ("k_rl_decide<lpa>" if lpa else "k_rl_decide<louvain>")]
+    if rl:
+        d = per[rl[0]]
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            summary["rl_decide_hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"][0] + d["WRITE_SIZE"][0]) * 1024.0
+            summary["rl_decide_hbm_bytes_per_launch_uncorrected"] = (d["FETCH_SIZE"][0] + d["WRITE_SIZE"][0]) * 1024.0
+        hit, miss = d.get("TCC_HIT_sum", (None,))[0], d.get("TCC_MISS_sum", (None,))[0]
+        if hit is not None and miss:
+            summary["rl_decide_l2_hit_rate"] = hit / (hit + miss)
     # Leiden / Infomap: per-launch HBM bytes of their own kernels (bench attaches the dominant one)
     for kern in ("k_lv_decide", "k_lv_heavy"):
         d = per.get(kern)
