@@ -141,7 +141,7 @@ void fc_destroy(fc_ctx* ctx) {
     (void)hipStreamSynchronize(c.stream);
     c.g.release();
     c.g0.release();
-    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.rl_lmask, &c.rl_vmask, &c.rl_aff, &c.rl_mvf, &c.rl_vlist, &c.rl_vcount, &c.rl_tot, &c.rl_state, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
+    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.rl_lmask, &c.rl_vmask, &c.rl_aff, &c.rl_mvf, &c.rl_vlist, &c.rl_vcount, &c.rl_tot, &c.rl_state, &c.rl_colw, &c.rl_slow, &c.rl_slow_cnt, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
                       &c.heavy_scratch, &c.wnew, &c.flag, &c.pos, &c.ku, &c.kv, &c.kw, &c.kage, &c.krowptr,
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,

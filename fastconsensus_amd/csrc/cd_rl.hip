@@ -26,7 +26,7 @@
 // equal labels are merged per lane by a triangular scan (duplicates marked), the candidates of
 // maximal weight compacted in place, and only their Sigma gathered (score = w*2M - k_v*Sigma
 // <= w*2M: a lighter candidate can only win if k_v*Sigma >= 2M, handled exactly by a rare
-// per-lane fallback).  Longer rows: one workgroup per unit (k_rl_heavy).
+// per-lane fallback).  Longer rows: one workgroup per unit (k_rl_exact).
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
@@ -48,13 +48,14 @@ constexpr int32_t DONE = -1;            // merged / own / empty table entry (lab
 constexpr int NSH = 16;                 // counter shards per replica
 constexpr int RF = 8;                   // fields: 0 dq, 1 unstable, 2 moves, 3 visits, 4 entries, 5 cands, 6 units
 constexpr double DQ_SCALE = 1099511627776.0;   // 2^40 fixed point for predicted dQ (as cd.hip)
-constexpr int HSLOTS = 4096;            // heavy-row LDS table
+constexpr int HWSLOTS = 1024;           // heavy rows: LDS table slots per wave (rows <= 512 entries)
 constexpr int HTB = 256;
-constexpr int HEAVY_GRID = 256;
+constexpr int HEAVY_GRID = 2048;       // k_rl_exact blocks at most (HTB / 64 visits each)
+constexpr int SLOW_GRID = 256;         // k_rl_exact blocks for the slow visits (their count stays on the device)
 constexpr int LTB = 256;                // list kernels
 constexpr int LPER = 8;                 // vertices per thread in the list kernels
 // Degree classes of a bucket's entries (the list is bucket-major, class-minor): rows of <= 16,
-// <= 32, <= DM entries are decided by sorting networks of that width, longer ones by k_rl_heavy.
+// <= 32, <= DM entries are decided by sorting networks of that width, longer ones by k_rl_exact.
 constexpr int NCLS = 4;
 __host__ __device__ __forceinline__ int rl_class(int d) { return d <= 16 ? 0 : d <= 32 ? 1 : d <= DM ? 2 : 3; }
 
@@ -75,9 +76,15 @@ struct RL {
     int64_t M2;
     int unitw;
     int wbits;                   // bits of the largest edge weight (key packing)
+    const int32_t* colw;         // weighted graphs with weights < 256: (col << wbits) | weight per entry
     int32_t* lab;                // labT [N][ldT]
     int32_t* tot;                // totT [N][ldT] (louvain)
     int32_t* dec;                // [PN][ldT]: target community or -1, per list entry and replica
+    // visits whose best max-weight candidate does not settle the decision (a lighter community
+    // may still score higher: k_v * Sigma >= 2M), decided exactly by k_rl_exact: (entry << 14) |
+    // local replica; slow_cnt is reset by the bucket's k_rl_apply
+    int64_t* slow;
+    int32_t* slow_cnt;
     int4* list;                  // [PN] the sweep's entries, bucket-major: vertex, row start, degree, k_v
                                  // (the vertex record travels with the entry: no dependent vrec read)
     uint64_t* lmask;             // [PN][banks] visiting replicas of each entry
@@ -320,7 +327,7 @@ __device__ __forceinline__ int64_t rl_items(const RL& a, int64_t n) {
 
 // ------------------------------------------------------------------ decide (light rows)
 // Per unit the lanes' header: the entry's vertex, the lane's replica bit, the row.  Rows
-// longer than DM are listed for k_rl_heavy (one entry per unit, by the sub-group's lane 0).
+// longer than DM are listed for k_rl_exact (one entry per unit, by the sub-group's lane 0).
 struct Hdr {
     int32_t v;
     uint64_t msk;
@@ -383,36 +390,16 @@ __device__ __forceinline__ void bitonic_sort(int32_t (&x)[K]) {
 // Pass B: the runs of weight vm are the candidates; their Sigma is gathered (16 positions per
 // batch, batches without a candidate skipped wave-wide) and the best score wins (score =
 // vm*2M - k_v*Sigma, ties by the replica's hash, then the smaller id).  A lighter run scores
-// <= (vm - 1)*2M: only when that still reaches the best are the lighter runs evaluated (rare).
-// A lighter neighbour community may still reach the best score (k_v * Sigma_min >= 2M, rare):
-// the lane re-evaluates every community of weight < vm from its row in global memory (O(d^2)
-// reads, cached), so the sorted keys need not stay live for it.
-__device__ __forceinline__ void rl_slow(const RL& a, const Hdr& h, int32_t own, int vm, uint32_t tvh,
-                                                  long long& best_s, uint32_t& best_h, int32_t& best_c,
-                                                  unsigned long long& c_cand, bool slow) {
-    if (!slow) return;
-    const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
-    const long long kv = h.kvi;
-    for (int j1 = 0; j1 < h.d; ++j1) {
-        const int32_t c1 = ld_off(a.lab, (uint32_t)a.col[h.rb + j1] * ldT + rr);
-        if (c1 == own) continue;
-        bool dup = false;
-        for (int j2 = 0; j2 < j1 && !dup; ++j2) dup = ld_off(a.lab, (uint32_t)a.col[h.rb + j2] * ldT + rr) == c1;
-        if (dup) continue;
-        long long val = 0;
-        for (int j2 = j1; j2 < h.d; ++j2)
-            if (ld_off(a.lab, (uint32_t)a.col[h.rb + j2] * ldT + rr) == c1) val += a.unitw ? 1 : a.cw[h.rb + j2];
-        if (val >= vm || val * a.M2 < best_s) continue;         // weight vm: evaluated already
-        const long long sc = val * a.M2 - kv * (long long)ld_off(a.tot, (uint32_t)c1 * ldT + rr);
-        const uint32_t hh = hash32(tvh ^ (uint32_t)c1);
-        ++c_cand;
-        if (rl_better(sc, hh, c1, best_s, best_h, best_c)) { best_s = sc; best_h = hh; best_c = c1; }
-    }
-}
-
-template <bool LOUV, int K, bool UNITW>
+// <= (vm - 1)*2M: only when that still reaches the best are the lighter runs evaluated.
+// WM: the row's weights -- WM_UNIT none (every weight 1), WM_W8 read with the neighbour id from
+// colw and kept 4 per register while the label gathers are in flight (weights < 256), WM_WIDE a
+// separate cw row (one register per entry)
+constexpr int WM_WIDE = 0, WM_UNIT = 1, WM_W8 = 2;
+template <bool LOUV, int K, int WM>
 __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
-                                             unsigned long long& c_unst, unsigned long long& c_cand) {
+                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
+    constexpr bool UNITW = WM == WM_UNIT;
+    slow_out = false;
     const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
     const int wb = UNITW ? 0 : a.wbits;
     const int32_t wm = (1 << wb) - 1;
@@ -429,7 +416,7 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
     int32_t x[K];
 #pragma unroll
     for (int j = 0; j < K; ++j)                                 // idle / padding lanes read col[rb] (a hit)
-        x[j] = ld_off(a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
+        x[j] = ld_off(WM == WM_W8 ? a.colw : a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
     int32_t tot_own = 0;
     if (LOUV) {
         const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
@@ -452,6 +439,26 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             }
             kown = ko;
         }
+    } else if constexpr (WM == WM_W8) {
+        uint32_t wpk[(K + 3) / 4];                              // 4 weights per register
+#pragma unroll
+        for (int i = 0; i < (K + 3) / 4; ++i) wpk[i] = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) wpk[j >> 2] |= (uint32_t)(x[j] & wm) << (8 * (j & 3));
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)(x[j] >> wb) * ldT + rr : home);
+            x[j] = j < dsw ? lj : -1;
+        }
+        int ko = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t wj = (int32_t)((wpk[j >> 2] >> (8 * (j & 3))) & 0xffu);
+            const bool mine = LOUV && x[j] == own && x[j] >= 0;
+            ko += mine ? wj : 0;
+            x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wj);
+        }
+        kown = ko;
     } else {
         int32_t wv[K];
 #pragma unroll
@@ -506,7 +513,7 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
         }
     }
     const int ncand = __popc(cm_lo) + __popc(cm_hi);
-    if (wk) c_cand += (unsigned long long)ncand;
+    if (wk) c_cand += (uint32_t)ncand;
     const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + h.rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)h.v);
     int32_t dcs = -1;
     if (LOUV) {
@@ -542,9 +549,12 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             best_c = (int32_t)(hash32_inv(best_h) ^ tvh);
             best_s = (long long)vm * a.M2 - kv * (long long)(uint32_t)(bkey >> 32);
         }
-        const bool slow = ncand != 0 && (long long)(vm - 1) * a.M2 >= best_s;
-        if (__ballot(slow)) rl_slow(a, h, own, vm, tvh, best_s, best_h, best_c, c_cand, slow);   // wave-uniform, rare
-        if (wk && ncand != 0) {
+        // a lighter run (weight <= vm - 1) scores <= weight * 2M: it can still reach the best
+        // only when k_v * Sigma_best >= 2M -- rare on large graphs, common on small weighted
+        // consensus graphs (2M small against k_v * Sigma).  Such a visit is handed to
+        // k_rl_exact (a wave and an LDS table per visit) instead of being finished here.
+        slow_out = wk && ncand != 0 && (long long)(vm - 1) * a.M2 >= best_s;
+        if (wk && ncand != 0 && !slow_out) {
             const long long G = best_s - kown * a.M2 + kv * ((long long)tot_own - kv);
             if (G > 0) {
                 const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
@@ -573,13 +583,33 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
 
 // Light rows with sortable keys (label and weight fit 31 bits): no LDS, one sorting network
 // per lane, K chosen per wave from its longest row.
-template <bool LOUV, int K, bool UNITW>
-__global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int seg, int sweep) {
+// Append the wave's slow visits to the exact kernel's list (one atomic per wave).
+__device__ __forceinline__ void rl_push_slow(const RL& a, bool slow, int64_t e, int rr) {
+    const uint64_t m = __ballot(slow);
+    if (!m) return;                                             // wave-uniform
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(a.slow_cnt, __popcll(m));
+    base = __shfl(base, 0);
+    if (slow) a.slow[base + __popcll(m & ((1ull << lane) - 1))] = (e << 14) | (int64_t)rr;
+}
+
+// Occupancy bounds per key width (waves per SIMD; 1 = the compiler's choice): A/B switches
+#ifndef FC_RLW16
+#define FC_RLW16 1
+#endif
+#ifndef FC_RLW32
+#define FC_RLW32 1
+#endif
+template <bool LOUV, int K, int WM>
+__global__ __launch_bounds__(RTB) __attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 32 ? FC_RLW32 : 1)))
+void k_rl_decide(RL a, int seg, int sweep) {
     const int lane = threadIdx.x & 63;
     const int64_t e0 = a.boff[seg], e1 = a.boff[seg + 1];
     const int64_t items = rl_items(a, e1 - e0);
     const int LG = a.LG;
-    unsigned long long c_dq = 0, c_unst = 0, c_vis = 0, c_ent = 0, c_cand = 0, c_units = 0;
+    unsigned long long c_dq = 0;                                // 32-bit counts: one block's items
+    uint32_t c_unst = 0, c_vis = 0, c_ent = 0, c_cand = 0, c_units = 0;
     int last_r = -1;
     auto flush = [&](int r) {
         if (r < 0) return;
@@ -589,13 +619,14 @@ __global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int seg, int sweep) {
         }
         if (lane < LG && r < a.n_r) {
             if (c_dq) atomicAdd(rl_red(a, r, 0), c_dq);
-            if (c_unst) atomicAdd(rl_red(a, r, 1), c_unst);
-            if (c_vis) atomicAdd(rl_red(a, r, 3), c_vis);
-            if (c_ent) atomicAdd(rl_red(a, r, 4), c_ent);
-            if (c_cand) atomicAdd(rl_red(a, r, 5), c_cand);
-            if (c_units) atomicAdd(rl_red(a, r, 6), c_units);
+            if (c_unst) atomicAdd(rl_red(a, r, 1), (unsigned long long)c_unst);
+            if (c_vis) atomicAdd(rl_red(a, r, 3), (unsigned long long)c_vis);
+            if (c_ent) atomicAdd(rl_red(a, r, 4), (unsigned long long)c_ent);
+            if (c_cand) atomicAdd(rl_red(a, r, 5), (unsigned long long)c_cand);
+            if (c_units) atomicAdd(rl_red(a, r, 6), (unsigned long long)c_units);
         }
-        c_dq = c_unst = c_vis = c_ent = c_cand = c_units = 0;
+        c_dq = 0;
+        c_unst = c_vis = c_ent = c_cand = c_units = 0;
     };
     Rec nxt = rl_fetch(a, rl_unit(a, e0, e1, blockIdx.x));
     for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
@@ -605,8 +636,10 @@ __global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int seg, int sweep) {
         const Rec cur = nxt;
         nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
         const Hdr h = rl_header(a, u, cur);
-        const int32_t dcs = rl_sorted<LOUV, K, UNITW>(a, h, sweep, c_dq, c_unst, c_cand);
-        if (h.work) { c_vis += 1; c_ent += (unsigned long long)h.d; }
+        bool slow;
+        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
+        rl_push_slow(a, slow, u.e, h.rr);
+        if (h.work) { c_vis += 1; c_ent += (uint32_t)h.d; }
         if (u.valid && u.rl == 0 && h.msk) c_units += 1;
         if (u.valid && h.rr < a.n_r) a.dec[u.e * a.ldT + h.rr] = h.work ? dcs : -1;
     }
@@ -616,7 +649,7 @@ __global__ __launch_bounds__(RTB) void k_rl_decide(RL a, int seg, int sweep) {
 // Visit mode: lane = one (entry, replica) visit -- rows are per lane (no sharing), for the
 // sparse sweeps where most replicas of an entry are idle and a wave per entry would run mostly
 // empty lanes.  Same decision code; counters go straight to the per-replica shards.
-template <bool LOUV, int K, bool UNITW>
+template <bool LOUV, int K, int WM>
 __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
     const int64_t v0 = a.voff[seg], v1 = a.voff[seg + 1];
     for (int64_t base = (int64_t)blockIdx.x * 64; base < v1 - v0; base += (int64_t)gridDim.x * 64) {
@@ -637,17 +670,20 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
         h.heavy = false;
         h.work = valid && h.d > 0;
         h.ds = valid ? h.d : 0;
-        unsigned long long c_dq = 0, c_unst = 0, c_cand = 0;
-        const int32_t dcs = rl_sorted<LOUV, K, UNITW>(a, h, sweep, c_dq, c_unst, c_cand);
+        unsigned long long c_dq = 0;
+        uint32_t c_unst = 0, c_cand = 0;
+        bool slow;
+        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
+        rl_push_slow(a, slow, e, h.rr);
         if (valid) {
             a.dec[e * a.ldT + h.rr] = h.work ? dcs : -1;
             if (c_dq) atomicAdd(rl_red(a, h.rr, 0), c_dq);
-            if (c_unst) atomicAdd(rl_red(a, h.rr, 1), c_unst);
+            if (c_unst) atomicAdd(rl_red(a, h.rr, 1), (unsigned long long)c_unst);
             if (h.work) {
                 atomicAdd(rl_red(a, h.rr, 3), 1ull);
                 atomicAdd(rl_red(a, h.rr, 4), (unsigned long long)h.d);
             }
-            if (c_cand) atomicAdd(rl_red(a, h.rr, 5), c_cand);
+            if (c_cand) atomicAdd(rl_red(a, h.rr, 5), (unsigned long long)c_cand);
         }
     }
 }
@@ -868,105 +904,117 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_lds(RL a, int k, int sweep) {
     flush(last_r);
 }
 
-// ------------------------------------------------------------------ decide (heavy rows)
+// ------------------------------------------------------------------ decide (exact, by table)
+// Visits the sorting networks do not finish: the heavy class's rows (degree > DM) for every
+// visiting replica, and the slow visits k_rl_decide listed.  One WAVE per visit, four per block:
+// a wave's LDS table (HWSLOTS slots, rows <= HWSLOTS / 2; longer rows a global table of the
+// wave's own) is cleared, filled and scanned by its 64 lanes with no block barrier (a wave's LDS
+// operations execute in order), and the best candidate over EVERY neighbour community is a wave
+// reduction.  (One block per vertex deciding its replicas one after the other paid four block
+// barriers per replica; the slow visits used to re-read their row O(d^2) times per lane.)
 template <bool LOUV>
-__global__ __launch_bounds__(HTB) void k_rl_heavy(RL a, int k, int sweep) {
-    __shared__ int32_t key[HSLOTS], val[HSLOTS];
-    __shared__ long long s_s[HTB], s_k[HTB];
-    __shared__ uint32_t s_h[HTB];
-    __shared__ int32_t s_c[HTB];
+__global__ __launch_bounds__(HTB) void k_rl_exact(RL a, int k, int sweep) {
+    __shared__ int32_t key[HTB / 64][HWSLOTS], val[HTB / 64][HWSLOTS];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t h0 = a.boff[k * NCLS + NCLS - 1], h1 = a.boff[k * NCLS + NCLS];   // the heavy class
-    const int64_t cnt = (h1 - h0) * a.banks;
-    for (int64_t item = blockIdx.x; item < cnt; item += gridDim.x) {
-        const int64_t e = h0 + item / a.banks;
-        const int bank = (int)(item % a.banks);
+    const int64_t ch = (h1 - h0) * a.n_r;
+    const int64_t cnt = ch + (LOUV ? *a.slow_cnt : 0);
+    const int64_t gw = (int64_t)blockIdx.x * (HTB / 64) + wv, nw = (int64_t)gridDim.x * (HTB / 64);
+    for (int64_t item = gw; item < cnt; item += nw) {      // wave-uniform
+        int64_t e;
+        int rr;
+        const bool heavy = item < ch;
+        if (heavy) {
+            e = h0 + item / a.n_r;
+            rr = (int)(item % a.n_r);
+            const uint64_t msk = a.lmask[e * a.banks + (rr >> 6)];
+            if (!((msk >> (rr & 63)) & 1ull)) continue;
+        } else {                                            // k_rl_decide counted the visit itself
+            const int64_t p = a.slow[item - ch];
+            e = p >> 14;
+            rr = (int)(p & 16383);
+        }
         const int32_t v = a.list[e].x;
-        const uint64_t msk = a.lmask[e * a.banks + bank];
         const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
-        uint32_t slots = 1;
+        uint32_t slots = 64;
         while (slots < 2 * (uint32_t)d) slots <<= 1;
-        int32_t* keys = key;
-        int32_t* vals = val;
-        if (slots > HSLOTS) {
+        int32_t* keys = key[wv];
+        int32_t* vals = val[wv];
+        if (slots > HWSLOTS) {
             slots = (uint32_t)a.hslots;
-            keys = a.hscratch + (int64_t)blockIdx.x * 2 * a.hslots;
+            keys = a.hscratch + gw * 2 * a.hslots;
             vals = keys + slots;
         }
+        for (uint32_t q = lane; q < slots; q += 64) { keys[q] = -1; vals[q] = 0; }
+        wsync();
+        for (int64_t j = rb + lane; j < rb + d; j += 64) {
+            const int32_t c = a.lab[(int64_t)a.col[j] * a.ldT + rr];
+            const int32_t w = a.unitw ? 1 : a.cw[j];
+            uint32_t h = hash32((uint32_t)c) & (slots - 1);
+            while (true) {
+                const int32_t prev = atomicCAS(&keys[h], -1, c);
+                if (prev == -1 || prev == c) { atomicAdd(&vals[h], w); break; }
+                h = (h + 1) & (slots - 1);
+            }
+        }
+        wsync();
+        const int32_t own = a.lab[(int64_t)v * a.ldT + rr];
         const long long kv = a.kdeg[v];
-        for (int rl = 0; rl < 64; ++rl) {                      // block-uniform
-            const int rr = bank * 64 + rl;
-            if (rr >= a.n_r || !((msk >> rl) & 1ull)) continue;
-            for (uint32_t s = threadIdx.x; s < slots; s += HTB) { keys[s] = -1; vals[s] = 0; }
-            __syncthreads();
-            for (int64_t j = rb + threadIdx.x; j < rb + d; j += HTB) {
-                const int32_t c = a.lab[(int64_t)a.col[j] * a.ldT + rr];
-                const int32_t w = a.unitw ? 1 : a.cw[j];
-                uint32_t h = hash32((uint32_t)c) & (slots - 1);
-                while (true) {
-                    const int32_t prev = atomicCAS(&keys[h], -1, c);
-                    if (prev == -1 || prev == c) { atomicAdd(&vals[h], w); break; }
-                    h = (h + 1) & (slots - 1);
-                }
+        const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)v);
+        long long best_s = LLONG_MIN, kown = 0;
+        uint32_t best_h = 0;
+        int32_t best_c = INT_MAX;
+        int ncand = 0;
+        for (uint32_t q = lane; q < slots; q += 64) {
+            const int32_t c = keys[q];
+            if (c < 0) continue;
+            const long long w = vals[q];
+            if (c == own) kown = w;
+            long long sc;
+            if (LOUV) {
+                if (c == own) continue;
+                sc = w * a.M2 - kv * (long long)a.tot[(int64_t)c * a.ldT + rr];
+            } else {
+                sc = w;
             }
-            __syncthreads();
-            const int32_t own = a.lab[(int64_t)v * a.ldT + rr];
-            const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)v);
-            long long best_s = LLONG_MIN, kown = 0;
-            uint32_t best_h = 0;
-            int32_t best_c = INT_MAX;
-            int ncand = 0;
-            for (uint32_t s = threadIdx.x; s < slots; s += HTB) {
-                const int32_t c = keys[s];
-                if (c < 0) continue;
-                const long long w = vals[s];
-                if (c == own) kown = w;
-                long long sc;
+            ++ncand;
+            const uint32_t h = hash32(tvh ^ (uint32_t)c);
+            if (best_c == INT_MAX || rl_better(sc, h, c, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = c; }
+        }
+        wsync();                                              // the table is reused by the next visit
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const long long s2 = __shfl_xor(best_s, off);
+            const uint32_t hh2 = __shfl_xor(best_h, off);
+            const int32_t c2 = __shfl_xor(best_c, off);
+            if (c2 != INT_MAX && (best_c == INT_MAX || rl_better(s2, hh2, c2, best_s, best_h, best_c))) {
+                best_s = s2; best_h = hh2; best_c = c2;
+            }
+            kown += __shfl_xor(kown, off);
+            ncand += __shfl_xor(ncand, off);
+        }
+        if (lane == 0) {
+            int32_t dcs = -1;
+            if (best_c != INT_MAX) {
                 if (LOUV) {
-                    if (c == own) continue;
-                    sc = w * a.M2 - kv * (long long)a.tot[(int64_t)c * a.ldT + rr];
+                    const long long tot_own = a.tot[(int64_t)own * a.ldT + rr];
+                    const long long G = best_s - kown * a.M2 + kv * (tot_own - kv);
+                    if (G > 0) {
+                        const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
+                        atomicAdd(rl_red(a, rr, 0), (unsigned long long)llrint(dqd * DQ_SCALE));
+                        dcs = best_c;
+                    }
                 } else {
-                    sc = w;
+                    if (kown != best_s) atomicAdd(rl_red(a, rr, 1), 1ull);
+                    dcs = best_c != own ? best_c : -1;
                 }
-                ++ncand;
-                const uint32_t h = hash32(tvh ^ (uint32_t)c);
-                if (best_c == INT_MAX || rl_better(sc, h, c, best_s, best_h, best_c)) { best_s = sc; best_h = h; best_c = c; }
             }
-            s_s[threadIdx.x] = best_s; s_h[threadIdx.x] = best_h; s_c[threadIdx.x] = best_c; s_k[threadIdx.x] = kown;
+            a.dec[e * a.ldT + rr] = dcs;
             if (ncand) atomicAdd(rl_red(a, rr, 5), (unsigned long long)ncand);
-            __syncthreads();
-            for (int off = HTB / 2; off > 0; off >>= 1) {
-                if ((int)threadIdx.x < off) {
-                    const int t2 = threadIdx.x + off;
-                    if (s_c[t2] != INT_MAX && (s_c[threadIdx.x] == INT_MAX ||
-                                               rl_better(s_s[t2], s_h[t2], s_c[t2], s_s[threadIdx.x], s_h[threadIdx.x],
-                                                         s_c[threadIdx.x]))) {
-                        s_s[threadIdx.x] = s_s[t2]; s_h[threadIdx.x] = s_h[t2]; s_c[threadIdx.x] = s_c[t2];
-                    }
-                    s_k[threadIdx.x] += s_k[t2];
-                }
-                __syncthreads();
-            }
-            if (threadIdx.x == 0) {
-                int32_t dcs = -1;
-                if (s_c[0] != INT_MAX) {
-                    if (LOUV) {
-                        const long long tot_own = a.tot[(int64_t)own * a.ldT + rr];
-                        const long long G = s_s[0] - s_k[0] * a.M2 + kv * (tot_own - kv);
-                        if (G > 0) {
-                            const double dqd = (double)G * 2.0 / ((double)a.M2 * (double)a.M2);
-                            atomicAdd(rl_red(a, rr, 0), (unsigned long long)llrint(dqd * DQ_SCALE));
-                            dcs = s_c[0];
-                        }
-                    } else {
-                        if (s_k[0] != s_s[0]) atomicAdd(rl_red(a, rr, 1), 1ull);
-                        dcs = s_c[0] != own ? s_c[0] : -1;
-                    }
-                }
-                a.dec[e * a.ldT + rr] = dcs;
+            if (heavy) {
                 atomicAdd(rl_red(a, rr, 3), 1ull);
                 atomicAdd(rl_red(a, rr, 4), (unsigned long long)d);
             }
-            __syncthreads();
         }
     }
 }
@@ -978,6 +1026,8 @@ __global__ __launch_bounds__(HTB) void k_rl_heavy(RL a, int k, int sweep) {
 template <bool LOUV>
 __global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
     const int lane = threadIdx.x & 63;
+    // k_rl_exact consumed the bucket's slow list: empty it for the next bucket
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.slow_cnt = 0;
     const int64_t e0 = a.boff[k * NCLS], e1 = a.boff[k * NCLS + NCLS];
     const int64_t items = rl_items(a, e1 - e0);
     const int LG = a.LG;
@@ -1119,6 +1169,12 @@ inline unsigned nb(int64_t n, int tb) {
     return (unsigned)(b < 1 ? 1 : b);
 }
 
+// (col << wb) | weight per adjacency entry (WM_W8: one load brings both)
+__global__ __launch_bounds__(256) void k_rl_colw(int64_t n, const int32_t* col, const int32_t* cw, int wb, int32_t* out) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n) out[j] = (col[j] << wb) | cw[j];
+}
+
 // Hybrid hand-off: the affected bits [banks][N] as cd.hip's per-replica flags u8 [n_r][N].
 __global__ __launch_bounds__(256) void k_rl_aff_export(int64_t N, const uint64_t* aff, uint8_t* out) {
     const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1203,9 +1259,19 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     while (a.wbits < 31 && ((int64_t)g.max_w >> a.wbits) != 0) ++a.wbits;
     // sortable keys (label << wbits | weight) need N << wbits < 2^31; else the LDS merge
     const bool pack = ((int64_t)(N - 1) << (a.unitw ? 0 : a.wbits)) < (int64_t(1) << 31);
+    a.colw = nullptr;
+    if (pack && louv && !a.unitw && a.wbits <= 8 && g.m > 0) {
+        int32_t* cwp = ensure<int32_t>(c.rl_colw, 2 * (size_t)g.m);
+        k_rl_colw<<<nb(2 * g.m, 256), 256, 0, c.stream>>>(2 * g.m, g.col.as<int32_t>(), g.cw.as<int32_t>(), a.wbits, cwp);
+        a.colw = cwp;
+    }
     a.lab = ensure<int32_t>(c.labT, (size_t)N * ldT);
     a.tot = louv ? ensure<int32_t>(c.rl_tot, (size_t)N * ldT) : nullptr;
     a.dec = ensure<int32_t>(c.dec, (size_t)PN * ldT);
+    // slow visits of one bucket: at most its entries (<= S) times the local replicas
+    a.slow = ensure<int64_t>(c.rl_slow, (size_t)S * ldT + 1);
+    a.slow_cnt = ensure<int32_t>(c.rl_slow_cnt, 4);
+    FC_HIP(hipMemsetAsync(a.slow_cnt, 0, 4, c.stream));
     a.list = (int4*)ensure<int4>(c.vlist, (size_t)PN);
     a.lmask = (uint64_t*)ensure<uint64_t>(c.rl_lmask, (size_t)PN * banks);
     a.vmask = (uint64_t*)ensure<uint64_t>(c.rl_vmask, (size_t)N * banks);
@@ -1246,7 +1312,12 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     a.hslots = 1;
     while (a.hslots < 2 * (int64_t)g.max_deg) a.hslots <<= 1;
     a.hscratch = nullptr;
-    if (a.hslots > HSLOTS) a.hscratch = ensure<int32_t>(c.heavy_scratch, (size_t)HEAVY_GRID * 2 * a.hslots);
+    // global tables (rows past HWSLOTS / 2): one per wave of at most hblocks blocks, <= 1 GiB in all
+    int64_t hblocks = HEAVY_GRID;
+    if (a.hslots > HWSLOTS) {
+        hblocks = std::max<int64_t>(1, std::min<int64_t>(HEAVY_GRID, (int64_t(1) << 30) / ((HTB / 64) * 2 * a.hslots * 4)));
+        a.hscratch = ensure<int32_t>(c.heavy_scratch, (size_t)hblocks * (HTB / 64) * 2 * a.hslots);
+    }
 
     k_rl_init<<<nb(N * ldT, 256), 256, 0, c.stream>>>(N, ldT, g.kdeg.as<int64_t>(), a.lab, a.tot);
 
@@ -1298,9 +1369,10 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
 #define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide_v<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep); timer_end(c, 7, ev); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
-                    if (louv && a.unitw) RL_LAUNCH_K(true, true);
-                    else if (louv) RL_LAUNCH_K(true, false);
-                    else RL_LAUNCH_K(false, true);
+                    if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
+                    else if (louv && a.colw) RL_LAUNCH_K(true, WM_W8);
+                    else if (louv) RL_LAUNCH_K(true, WM_WIDE);
+                    else RL_LAUNCH_K(false, WM_UNIT);
 #undef RL_LAUNCH_K
 #undef RL_LAUNCH
                 }
@@ -1313,9 +1385,10 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
 #define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep); timer_end(c, 7, ev); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
-                    if (louv && a.unitw) RL_LAUNCH_K(true, true);
-                    else if (louv) RL_LAUNCH_K(true, false);
-                    else RL_LAUNCH_K(false, true);
+                    if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
+                    else if (louv && a.colw) RL_LAUNCH_K(true, WM_W8);
+                    else if (louv) RL_LAUNCH_K(true, WM_WIDE);
+                    else RL_LAUNCH_K(false, WM_UNIT);
 #undef RL_LAUNCH_K
 #undef RL_LAUNCH
                 }
@@ -1328,9 +1401,17 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     timer_end(c, 7, ev);
                 }
             }
-            if (hb[(k + 1) * NCLS] > hb[k * NCLS + NCLS - 1]) {
-                if (louv) k_rl_heavy<true><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
-                else k_rl_heavy<false><<<HEAVY_GRID, HTB, 0, c.stream>>>(a, k, sweep);
+            // exact decisions: the heavy rows (one wave per (entry, replica) visit, HTB / 64 per
+            // block) and, louvain, the slow visits the decide launches listed (count on the device:
+            // a floor of SLOW_GRID blocks, idle ones return at once)
+            {
+                const int64_t hv = (int64_t)(hb[(k + 1) * NCLS] - hb[k * NCLS + NCLS - 1]) * rcount;
+                const int64_t want = (hv + HTB / 64 - 1) / (HTB / 64) + (louv && pack ? SLOW_GRID : 0);
+                const unsigned hgrid = (unsigned)std::min<int64_t>(hblocks, want);
+                if (hgrid > 0) {
+                    if (louv) k_rl_exact<true><<<hgrid, HTB, 0, c.stream>>>(a, k, sweep);
+                    else k_rl_exact<false><<<hgrid, HTB, 0, c.stream>>>(a, k, sweep);
+                }
             }
             if (louv) k_rl_apply<true><<<grid_of(nb_all), RTB, 0, c.stream>>>(a, k);
             else k_rl_apply<false><<<grid_of(nb_all), RTB, 0, c.stream>>>(a, k);

@@ -119,6 +119,8 @@ struct Ctx {
     // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many replicas
     int64_t rl_min_replicas = getenv("FC_RL_MIN_REPLICAS") ? atoll(getenv("FC_RL_MIN_REPLICAS")) : 16;
     DevBuf rl_tot, rl_state;        // replica-lane totals [N][ldT] and per-replica state (kept apart from cd.hip's)
+    DevBuf rl_colw;                 // replica-lane: (col << wbits) | weight per adjacency entry (weights < 256)
+    DevBuf rl_slow, rl_slow_cnt;    // replica-lane: one bucket's visits left to the exact kernel
     int ldT = 0;
     bool labT_valid = false;
     DevBuf rep_state;               // per replica: active flag, dq accum, moves, unstable

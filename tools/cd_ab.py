@@ -58,6 +58,7 @@ def child(lib, config, algo, reps):
         out["decide_ms"] = min(t["decide_ms"] for t in cds)
         out["decide_launches"] = cds[0]["decide_launches"]
         out["decide_us_avg"] = 1e3 * out["decide_ms"] / max(1, out["decide_launches"])
+        out["rl_decide_ms"] = min(t["rl_decide_ms"] for t in cds)
         out["visits"] = cds[0]["cd_vertex_visits"]
         out["sweeps"] = cds[0]["cd_sweeps"]
         host = np.zeros((n_p, n), np.int32)
@@ -77,6 +78,7 @@ def child(lib, config, algo, reps):
             cds.append(eng.collect_timing())
         out["w_cd_ms"] = min(t["cd_ms"] for t in cds)
         out["w_decide_ms"] = min(t["decide_ms"] for t in cds)
+        out["w_rl_decide_ms"] = min(t["rl_decide_ms"] for t in cds)
         out["w_labels_sha"] = hashlib.sha1(eng.get_labels(n_p).tobytes()).hexdigest()[:16]
     print(json.dumps(out), flush=True)
 
