@@ -319,7 +319,7 @@ def main():
         from fastconsensus_amd.distributed import shard
         r0, r1 = shard(cfg["n_p"], rank, world)
         eng.set_option("store", store_order_pays(r1 - r0, ALGORITHMS[cfg["algo"]],
-                                                int(dict(kv.split("=", 1) for kv in args.opt).get("cd_engine", 0))))
+                                                int(dict(kv.split("=", 1) for kv in args.opt).get("cd_engine", 2))))
         if args.buckets:
             eng.set_params(buckets=args.buckets)
         for name in ("chunk", "prune", "relabel", "store", "coarsen"):

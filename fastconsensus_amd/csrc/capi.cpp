@@ -208,6 +208,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_INFOMAP_TRIALS: FC_REQUIRE(value >= 1, FC_EINVAL, "infomap trials >= 1"); c.infomap_trials = (int)value; break;
         case FC_OPT_CD_ENGINE: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "cd_engine must be 0, 1 or 2"); c.cd_engine = (int)value; break;
         case FC_OPT_RL_MIN_REPLICAS: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_replicas >= 1"); c.rl_min_replicas = value; break;
+        case FC_OPT_RL_MIN_VERTICES: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_vertices >= 1"); c.rl_min_vertices = value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }

@@ -1224,7 +1224,7 @@ bool cd_rl_supported(const Ctx& c, int algo) { return c.cd_engine == 1 && cd_rl_
 // throughout, with the same semantics (its full sweeps use the shared order too), so results
 // never depend on how replicas are sharded over GPUs.
 void cd_run_hybrid(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
-    if (cd_rl_fits(c, algo) && (int64_t)rcount >= c.rl_min_replicas)
+    if (cd_rl_fits(c, algo) && (int64_t)rcount >= c.rl_min_replicas && c.N >= c.rl_min_vertices)
         cd_run_rl(c, algo, rbegin, rcount, n_p_total, iteration, true);
     else
         cd_run(c, algo, rbegin, rcount, n_p_total, iteration, 1);

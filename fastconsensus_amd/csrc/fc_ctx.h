@@ -115,9 +115,12 @@ struct Ctx {
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
-    int cd_engine = 0;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip, default), 1 replica-lane (cd_rl.hip), 2 hybrid
+    int cd_engine = 2;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip), 1 replica-lane (cd_rl.hip), 2 hybrid (default)
     // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many replicas
     int64_t rl_min_replicas = getenv("FC_RL_MIN_REPLICAS") ? atoll(getenv("FC_RL_MIN_REPLICAS")) : 16;
+    // ... and the graph this many vertices (a bucket of a smaller graph is too few waves for the
+    // replica-lane kernels: LFR-100k louvain 45.9 vs 31.2 ms, LFR-1M 175.8 vs 211 ms)
+    int64_t rl_min_vertices = getenv("FC_RL_MIN_VERTICES") ? atoll(getenv("FC_RL_MIN_VERTICES")) : 262144;
     DevBuf rl_tot, rl_state;        // replica-lane totals [N][ldT] and per-replica state (kept apart from cd.hip's)
     DevBuf rl_colw;                 // replica-lane: (col << wbits) | weight per adjacency entry (weights < 256)
     DevBuf rl_slow, rl_slow_cnt;    // replica-lane: one bucket's visits left to the exact kernel

@@ -160,6 +160,8 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 (shared = 0 / 1 / 2).                                            */
 #define FC_OPT_RL_MIN_REPLICAS 15 /* hybrid: the smallest batch whose full sweeps run on the
                                 replica-lane engine (default 16).  Speed only: same results.     */
+#define FC_OPT_RL_MIN_VERTICES 16 /* hybrid: ... and the smallest graph (default 262144 vertices;
+                                below it cd.hip runs the full sweeps too).  Speed only.          */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

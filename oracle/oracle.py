@@ -282,10 +282,12 @@ def infomap_full(g, seed, trials=10):
 
 
 def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8,
-              prune_mark=1, shared=0):
+              prune_mark=1, shared=2):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels).  Defaults = the
-    default (classic) engine, cd.hip (fc_ctx.h).  The replica-lane engine (FC_OPT_CD_ENGINE=1,
-    cd_rl.hip) is shared=1 (one visit order shared by every replica), coarsen=0."""
+    default engine (fc_ctx.h): the hybrid, FC_OPT_CD_ENGINE=2, shared=2 (a replica's full sweeps
+    in the batch's shared order, its filtered sweeps in its own).  The classic engine (cd.hip
+    alone, FC_OPT_CD_ENGINE=0) is shared=0; the replica-lane engine (FC_OPT_CD_ENGINE=1, cd_rl.hip)
+    is shared=1 (one visit order shared by every replica in every sweep), coarsen=0."""
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)

@@ -12,10 +12,11 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1, shared=0):
+    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1, shared=2):
         """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity.  Defaults:
-        the default (classic) CD engine; shared=1, coarsen=0 model the replica-lane engine
-        (FC_OPT_CD_ENGINE=1, cd_rl.hip: shared visit order, no coarse rounds)."""
+        the default (hybrid) CD engine, FC_OPT_CD_ENGINE=2; shared=0 models the classic engine,
+        shared=1, coarsen=0 the replica-lane engine (FC_OPT_CD_ENGINE=1, cd_rl.hip: one shared
+        visit order in every sweep, no coarse rounds)."""
         self.seed = int(seed)
         self.buckets = buckets
         self.chunk = chunk

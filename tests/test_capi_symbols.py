@@ -66,10 +66,9 @@ def test_cpu_twin_defaults_match_engine_defaults():
     from tests.cpu_engine import OracleEngine
     src = open(os.path.join(ROOT, "fastconsensus_amd", "csrc", "fc_ctx.h")).read()
     eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen", "prune_mark")}
-    # the default CD engine is the classic one (per-replica visit orders); the replica-lane
-    # engine is opt-in (FC_OPT_CD_ENGINE=1)
-    assert int(re.search(r"\bcd_engine = (\d+)", src).group(1)) == 0
-    eng["shared"] = 0
+    # the default CD engine is the hybrid (FC_OPT_CD_ENGINE=2): the twin's shared=2
+    assert int(re.search(r"\bcd_engine = (\d+)", src).group(1)) == 2
+    eng["shared"] = 2
     twin = inspect.signature(orc.engine_cd).parameters
     model = inspect.signature(OracleEngine.__init__).parameters
     for k, v in eng.items():

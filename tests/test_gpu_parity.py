@@ -195,6 +195,7 @@ def _set_engine(eng, engine):
     eng.set_option("cd_engine", min(engine, 2))
     if engine >= 2:
         eng.set_option("rl_min_replicas", 1 if engine == 2 else 1 << 30)
+        eng.set_option("rl_min_vertices", 1)
 
 
 def _engine(eng, engine, tail=0, coarsen=0):
