@@ -1211,7 +1211,9 @@ void rl_layout(int n_r, int* LG, int* VPW, int* banks, int* ldT) {
 
 // the graph and options the replica-lane kernels handle (int32 totals, 32-bit row offsets)
 static bool cd_rl_fits(const Ctx& c, int algo) {
-    return !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && c.g.M2 <= 0x7fffffffll &&
+    // int32 community totals (louvain only: LPA ignores the weights, so a heavily weighted
+    // consensus graph -- 2M past 2^31 at SBM-4M, n_p = 128 -- still fits its label propagation)
+    return !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && (!is_louvain(algo) || c.g.M2 <= 0x7fffffffll) &&
            c.g.m < (int64_t(1) << 31) && (c.chunk == 0 || c.chunk == RL_CHUNK);
 }
 bool cd_rl_supported(const Ctx& c, int algo) { return c.cd_engine == 1 && cd_rl_fits(c, algo); }
