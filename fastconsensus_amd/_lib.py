@@ -19,7 +19,7 @@ FC_ALGO_INFOMAP = 4      # infomap: the lpm loop (:260-310) around igraph Infoma
 OPTIONS = {"buckets": 1, "max_sweeps": 2, "max_iters": 3, "chunk": 4, "prune": 5, "relabel": 6, "tail_visits": 7,
            "coarsen": 8, "store": 9, "seed": 10, "closure_rounds": 11,
            "prune_mark": 12, "infomap_trials": 13, "cd_engine": 14,
-           "rl_min_replicas": 15, "rl_min_vertices": 16}
+           "rl_min_replicas": 15, "rl_min_vertices": 16, "dense_div": 17}
 ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 
 # Every symbol declared in include/fastconsensus_amd.h (checked by tests/test_capi_symbols.py)

@@ -141,7 +141,7 @@ void fc_destroy(fc_ctx* ctx) {
     (void)hipStreamSynchronize(c.stream);
     c.g.release();
     c.g0.release();
-    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.rl_lmask, &c.rl_vmask, &c.rl_aff, &c.rl_mvf, &c.rl_vlist, &c.rl_vcount, &c.rl_tot, &c.rl_state, &c.rl_colw, &c.rl_slow, &c.rl_slow_cnt, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
+    DevBuf* bufs[] = {&c.lab, &c.nlab, &c.rl_lmask, &c.rl_vmask, &c.rl_aff, &c.rl_mvf, &c.rl_vlist, &c.rl_vcount, &c.rl_tot, &c.rl_state, &c.rl_colw, &c.rl_slow, &c.rl_slow_cnt, &c.aff_cnt, &c.aff, &c.vlist, &c.vcnt, &c.track, &c.tot, &c.dec, &c.labT, &c.rep_state, &c.heavy_list, &c.heavy_cnt,
                       &c.heavy_scratch, &c.wnew, &c.flag, &c.pos, &c.ku, &c.kv, &c.kw, &c.kage, &c.krowptr,
                       &c.kcol, &c.counters, &c.ckey, &c.cval, &c.ckey2, &c.cval2, &c.cu, &c.cv, &c.cw2,
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
@@ -209,6 +209,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_CD_ENGINE: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "cd_engine must be 0, 1 or 2"); c.cd_engine = (int)value; break;
         case FC_OPT_RL_MIN_REPLICAS: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_replicas >= 1"); c.rl_min_replicas = value; break;
         case FC_OPT_RL_MIN_VERTICES: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_vertices >= 1"); c.rl_min_vertices = value; break;
+        case FC_OPT_DENSE_DIV: FC_REQUIRE(value >= 0 && value <= 64, FC_EINVAL, "dense_div must be 0..64"); c.dense_div = (int)value; break;
         case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }

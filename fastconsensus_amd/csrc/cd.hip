@@ -135,6 +135,9 @@ struct CDArgs {
                                  // move phase 0: run until a sweep moves nothing)
     int shared_full;             // FC_OPT_CD_ENGINE=2: a replica's full sweeps visit the batch's SHARED order
                                  // (SHARED_RG), its filtered sweeps its own (oracle tw_replica shared = 2)
+    const int32_t* vcnt;         // hybrid: [n_r] affected flags at this sweep's start (the filtered list's
+                                 // size); a list of >= N/dense_div ("dense") keeps the shared order and 1-bucket rounds
+    int dense_div;
 };
 
 // Sweep order of replica rg: a random permutation of the vertices, or of chunks of CHUNK
@@ -152,8 +155,12 @@ __device__ __forceinline__ Perm sweep_perm(const CDArgs& a, int rg, int sweep) {
 // full in the hybrid (the replica-lane engine runs those sweeps when the batch is wide enough;
 // this engine runs them for narrow batches and for replicas still full after the hand-off).
 __device__ __forceinline__ bool rep_full(const CDArgs& a, int r);
-__device__ __forceinline__ int order_rg(const CDArgs& a, int r, bool full) {
-    return (a.shared_full && full) ? (int)SHARED_RG : a.rbase + r;
+__device__ __forceinline__ int order_rg(const CDArgs& a, int r, bool shared) {
+    return (a.shared_full && shared) ? (int)SHARED_RG : a.rbase + r;
+}
+// hybrid: replica r's filtered sweep still visits >= N/dense_div vertices -- the shared order, no coarse rounds
+__device__ __forceinline__ bool rep_dense(const CDArgs& a, int r) {
+    return a.shared_full && a.vcnt && !rep_full(a, r) && (int64_t)a.dense_div * a.vcnt[r] >= a.N;
 }
 // Vertex at sweep position p, or -1 for a padding slot.
 __device__ __forceinline__ int32_t pos_vertex(const CDArgs& a, const Perm& P, int64_t p) {
@@ -989,16 +996,18 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
         const bool full = rep_full(a, r);
         const bool push = a.track[2 * a.n_r + r] != 0 || a.track[3 * a.n_r + r] != 0, trk = a.track[r] != 0;
         const bool dpush = a.track[2 * a.n_r + r] != 0, dtrans = a.track[3 * a.n_r + r] != 0;
-        const Perm P = sweep_perm(a, order_rg(a, r, full), sweep);
+        const int n = s_n;                    // this sweep's list (when filtered)
+        const bool dense = a.shared_full && a.dense_div && !full && (int64_t)a.dense_div * n >= a.N;   // rep_dense, from the list
+        const Perm P = sweep_perm(a, order_rg(a, r, full || dense), sweep);
         const int32_t stamp = sweep + 1;
+        __syncthreads();                      // every thread has read s_n
         for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = 0;
         if (threadIdx.x < 6) s_acc[threadIdx.x] = 0;
         if (threadIdx.x == 0) { s_nnext = 0; s_stop = 0; s_nheavy = 0; s_nmv = 0; }
         __syncthreads();
-        const int n = s_n;
         const int32_t* blp = bl;
         if (!full && first) {                 // rounds as k_list_plan laid them out: round j = buckets [j*g, (j+1)*g)
-            const int g0 = a.coarsen ? coarse_factor(a.N, (int64_t)n, B, a.coarsen) : 1;
+            const int g0 = (a.coarsen && !dense) ? coarse_factor(a.N, (int64_t)n, B, a.coarsen) : 1;
             for (int k = threadIdx.x; k <= B; k += NTH) s_off[k] = lo0[(k + g0 - 1) / g0];
             blp = a.list + (int64_t)r * a.PN;
             __syncthreads();
@@ -1020,7 +1029,7 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
             __syncthreads();
         }
         // rounds: one bucket each, or g consecutive buckets of a filtered sweep (k_list_plan)
-        const int g = (!full && a.coarsen) ? coarse_factor(a.N, (int64_t)n, B, a.coarsen) : 1;
+        const int g = (!full && !dense && a.coarsen) ? coarse_factor(a.N, (int64_t)n, B, a.coarsen) : 1;
         for (int k = 0; k < B; k += g) {
             const int k1 = min(B, k + g);
             const int64_t nk = full ? min(a.S, a.PN - (int64_t)k * a.S) : (int64_t)(s_off[k1] - s_off[k]);
@@ -1154,13 +1163,25 @@ __device__ __forceinline__ uint32_t vertex_bucket(const CDArgs& a, const Perm& P
     const uint32_t pos = vertex_pos(a, P, v);
     return pos / (uint32_t)a.S;
 }
+// Hybrid: each filtered replica's affected flags (its list size this sweep, rep_dense).
+__global__ __launch_bounds__(256) void k_aff_count(CDArgs a, int32_t* vcnt) {
+    const int r = blockIdx.y;
+    if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
+    const uint8_t* aff = a.aff + (int64_t)r * a.N;
+    int c = 0;
+    for (int64_t v = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x; v < a.N && v < (int64_t)(blockIdx.x + 1) * TB * LB_PER;
+         v += TB)
+        c += aff[v] != 0;
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(vcnt + r, c);
+}
 __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t* cntfine) {
     extern __shared__ int s_lb[];
     const int r = blockIdx.y, B = a.B;
     if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
     for (int k = threadIdx.x; k < B; k += TB) s_lb[k] = 0;
     __syncthreads();
-    const Perm P = sweep_perm(a, a.rbase + r, sweep);
+    const Perm P = sweep_perm(a, order_rg(a, r, rep_dense(a, r)), sweep);
     const uint8_t* aff = a.aff + (int64_t)r * a.N;
     const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
 #pragma unroll
@@ -1209,7 +1230,7 @@ __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int
         const int32_t* cf = cntfine + (int64_t)r * B;
         int64_t V = 0;
         for (int k = 0; k < B; ++k) V += cf[k];
-        const int g = a.coarsen ? coarse_factor(a.N, V, B, a.coarsen) : 1;
+        const int g = (a.coarsen && !rep_dense(a, r)) ? coarse_factor(a.N, V, B, a.coarsen) : 1;
         const int rounds = (B + g - 1) / g;
         int32_t acc = 0;
         for (int k = 0; k < B; ++k) {
@@ -1241,7 +1262,7 @@ __global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const in
     for (int k = threadIdx.x; k < B; k += TB) s_cnt[k] = 0;
     __syncthreads();
     const int g = gco[r];
-    const Perm P = sweep_perm(a, a.rbase + r, sweep);
+    const Perm P = sweep_perm(a, order_rg(a, r, rep_dense(a, r)), sweep);
     uint8_t* aff = a.aff + (int64_t)r * a.N;
     int bk[LB_PER], loc[LB_PER];
     const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
@@ -1393,6 +1414,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.red = red; a.sacc = sacc;
     a.min_dq = c.cd_min_dq;
     a.shared_full = shared_full;
+    // hybrid: per-replica list sizes of the filtered sweeps (dense lists keep the shared order)
+    int32_t* vcnt = (shared_full && c.prune && c.dense_div) ? ensure<int32_t>(c.aff_cnt, (size_t)rcount) : nullptr;
+    a.vcnt = vcnt;
+    a.dense_div = c.dense_div;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
     a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
     a.hcap = std::max<int64_t>(n_heavy, 1);
@@ -1434,6 +1459,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
         FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
+        if (vcnt && sweep > 0) {
+            FC_HIP(hipMemsetAsync(vcnt, 0, sizeof(int32_t) * (size_t)rcount, c.stream));
+            k_aff_count<<<dim3(lb_grid, rcount), TB, 0, c.stream>>>(a, vcnt);
+        }
         k_list_count<<<dim3(lb_grid, rcount), TB, sizeof(int) * B, c.stream>>>(a, sweep, cntfine);
         k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, rrec, info);
         FC_HIP(hipMemcpyAsync(hinfo, info, 20, hipMemcpyDeviceToHost, c.stream));

@@ -106,9 +106,15 @@ struct RL {
     int32_t* hscratch;           // global tables for rows past the LDS table
     int64_t hslots;
     double min_dq;
-    int hybrid;                  // FC_OPT_CD_ENGINE=2: stop before the first sweep that filters a replica
-                                 // (cd.hip takes the batch over from there: cd_run_hybrid)
+    int hybrid;                  // FC_OPT_CD_ENGINE=2: stop before the first sweep in which a replica's
+                                 // filtered list is sparse (< N/4; cd.hip takes over: cd_run_hybrid)
+    const int32_t* acnt;         // hybrid: [n_r] affected bits per replica at the sweep's start
+    int dense_div;               // hybrid: a filtered list of >= N/dense_div stays here (0: none does)
 };
+// hybrid: replica r runs a filtered sweep whose list holds < N/dense_div vertices (its own order on cd.hip)
+__device__ __forceinline__ bool rl_sparse(const RL& a, int r) {
+    return a.hybrid && a.active[r] && a.prune && a.track[a.n_r + r] && (int64_t)a.dense_div * a.acnt[r] < a.N;
+}
 
 __device__ __forceinline__ Perm rl_perm(const RL& a, int sweep) {
     Perm P = make_perm(a.perm_n, stream_key(a.seed, SHARED_RG, a.iter, (uint32_t)sweep, 1));
@@ -202,9 +208,9 @@ __global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int list
         if (a.prune && a.track[a.n_r + r]) atomicOr((unsigned long long*)&s_flt[r >> 6], 1ull << (r & 63));
     }
     __syncthreads();
-    if (a.hybrid) {   // a replica filters this sweep: cd.hip takes over, the flags stay for it (block-uniform)
-        uint64_t any = 0;
-        for (int b = 0; b < a.banks; ++b) any |= s_act[b] & s_flt[b];
+    if (a.hybrid && listed) {   // a sparse filtered list: cd.hip takes over, the flags stay for it (block-uniform)
+        bool any = false;
+        for (int r = 0; r < a.n_r && !any; ++r) any = rl_sparse(a, r);
         if (any) return;
     }
     const Perm P = rl_perm(a, sweep);
@@ -1121,14 +1127,14 @@ __global__ __launch_bounds__(RTB) void k_rl_mark_lm(RL a) {
 
 // End of a sweep, per replica (cd.hip k_sweep_end without the push / transition modes):
 // python-louvain stops a level when the pass gained < min_dq or moved nothing; igraph LPA
-// when no visited vertex was unstable.  n_active_out: [0] active after, [1] active replicas whose
-// next sweep is filtered, [2..3] u64 moves,
+// when no visited vertex was unstable.  n_active_out: [0] active after, [1] (k_rl_hand) replicas
+// whose filtered list is sparse this sweep, [2..3] u64 moves,
 // [4..5] u64 replica-sweeps so far, [6..7] u64 visits of this sweep.
 template <bool LOUV>
 __global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
-    __shared__ int cnt, cnt0, nflt;
+    __shared__ int cnt, cnt0;
     __shared__ unsigned long long mv, vis;
-    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; nflt = 0; mv = 0; vis = 0; }
+    if (threadIdx.x == 0) { cnt = 0; cnt0 = 0; mv = 0; vis = 0; }
     __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         unsigned long long f[RF] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1148,16 +1154,12 @@ __global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
             if (LOUV) stop = f[2] == 0 || ((double)f[0] / DQ_SCALE) < a.min_dq;
             else stop = f[1] == 0;
             if (stop) a.active[r] = 0;
-            else {
-                atomicAdd(&cnt, 1);
-                if (a.prune && a.track[a.n_r + r]) atomicAdd(&nflt, 1);   // filters next sweep
-            }
+            else atomicAdd(&cnt, 1);
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         n_active_out[0] = cnt;
-        n_active_out[1] = nflt;
         *(unsigned long long*)(n_active_out + 2) = mv;
         *(unsigned long long*)(n_active_out + 4) += (unsigned long long)cnt0;
         *(unsigned long long*)(n_active_out + 6) = vis;
@@ -1167,6 +1169,42 @@ __global__ void k_rl_sweep_end(RL a, int32_t* n_active_out) {
 inline unsigned nb(int64_t n, int tb) {
     int64_t b = (n + tb - 1) / tb;
     return (unsigned)(b < 1 ? 1 : b);
+}
+
+// Hybrid: affected bits per replica at a listed sweep's start (a wave turns its 64 words per bank
+// into 64 per-replica counts with one ballot per bit).  Dynamic LDS: banks * 64 ints.
+__global__ __launch_bounds__(LTB) void k_rl_aff_count(RL a, int32_t* cnt) {
+    extern __shared__ int s_c[];
+    for (int k = threadIdx.x; k < a.banks * 64; k += LTB) s_c[k] = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    for (int64_t v0 = (int64_t)blockIdx.x * LTB * LPER; v0 < min(a.N, (int64_t)(blockIdx.x + 1) * LTB * LPER); v0 += LTB) {
+        const int64_t v = v0 + threadIdx.x;
+        for (int b = 0; b < a.banks; ++b) {
+            const uint64_t w = v < a.N ? a.aff[(int64_t)b * a.N + v] : 0;
+            if (__ballot(w != 0) == 0) continue;                // wave-uniform
+            int mine = 0;
+#pragma unroll 8
+            for (int q = 0; q < 64; ++q) {
+                const int c = __popcll(__ballot((w >> q) & 1ull));
+                mine = lane == q ? c : mine;
+            }
+            if (mine) atomicAdd(&s_c[b * 64 + lane], mine);
+        }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < a.n_r; r += LTB)
+        if (s_c[r]) atomicAdd(cnt + r, s_c[r]);
+}
+// Hybrid: the replicas whose filtered list is sparse this sweep (any: hand over to cd.hip).
+__global__ void k_rl_hand(RL a, int32_t* n_active_out) {
+    __shared__ int n;
+    if (threadIdx.x == 0) n = 0;
+    __syncthreads();
+    for (int r = threadIdx.x; r < a.n_r; r += blockDim.x)
+        if (rl_sparse(a, r)) atomicAdd(&n, 1);
+    __syncthreads();
+    if (threadIdx.x == 0) n_active_out[1] = n;
 }
 
 // (col << wb) | weight per adjacency entry (WM_W8: one load brings both)
@@ -1296,6 +1334,9 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     a.lm = ((g.max_w > 1 || c.prune_mark == 2) && c.prune && c.prune_mark >= 1) ? 1 : 0;
     a.min_dq = c.cd_min_dq;
     a.hybrid = hybrid ? 1 : 0;
+    int32_t* acnt = hybrid ? ensure<int32_t>(c.aff_cnt, (size_t)rcount) : nullptr;
+    a.acnt = acnt;
+    a.dense_div = c.dense_div;
     // per-replica state: active i32 [n_r] | track i32 [2 n_r] | red u64 [n_r][NSH][RF] | sacc u64 [n_r][4] | n_active [8]
     char* rs = (char*)ensure<char>(c.rl_state, (size_t)rcount * (12 + 8 * NSH * RF + 32) + 512);
     a.active = (int32_t*)rs;
@@ -1332,6 +1373,11 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         const int listed = (c.prune && sweep > 0) ? 1 : 0;
         FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * nseg, c.stream));
         FC_HIP(hipMemsetAsync(vcnt, 0, sizeof(int32_t) * nseg, c.stream));
+        if (hybrid && listed) {   // per-replica list sizes: a sparse one hands the batch to cd.hip
+            FC_HIP(hipMemsetAsync(acnt, 0, sizeof(int32_t) * (size_t)rcount, c.stream));
+            if (a.dense_div) k_rl_aff_count<<<lgrid, LTB, sizeof(int) * 64 * banks, c.stream>>>(a, acnt);
+            k_rl_hand<<<1, 256, 0, c.stream>>>(a, n_active);
+        }
         k_rl_list_count<<<lgrid, LTB, lcount_lds, c.stream>>>(a, sweep, listed, bcnt, vcnt);
         k_rl_list_plan<<<1, 64, 0, c.stream>>>(nseg, bcnt, a.boff, a.cursor, vcnt, a.voff, a.vcursor);
         FC_HIP(hipMemcpyAsync(hb.data(), a.boff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost, c.stream));
@@ -1340,7 +1386,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         FC_HIP(hipMemcpyAsync(hinfo, n_active, 8, hipMemcpyDeviceToHost, c.stream));
         sync(c);
         if (sweep > 0 && hinfo[0] == 0) break;                      // every replica has stopped
-        if (hybrid && sweep > 0 && hinfo[1] > 0) { handoff = sweep; break; }   // a replica filters: cd.hip
+        if (hybrid && listed && hinfo[1] > 0) { handoff = sweep; break; }   // a sparse filtered list: cd.hip
         if (hb[nseg] == 0) break;
         k_rl_list_fill<<<lgrid, LTB, 2 * sizeof(int) * nseg, c.stream>>>(a, sweep);
         // visit mode when the replicas of an entry are mostly idle (few visits per listed entry):

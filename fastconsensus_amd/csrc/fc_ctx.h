@@ -110,6 +110,7 @@ struct Ctx {
     DevBuf nlab;                    // int32 [n_r][2m]: label of each adjacency entry's neighbour
     DevBuf aff, vlist, vcnt, track; // pruning: affected flags, per-sweep visit lists, list lengths, modes
     DevBuf mvf;                     // movers of a tracked sweep (prune_mark = 1 on weighted Louvain graphs)
+    DevBuf aff_cnt;                 // hybrid: per-replica affected-flag counts at a sweep's start
     // replica-lane engine (cd_rl.hip): per-entry replica masks, list-build scratch, affected /
     // mover bits [banks][N]; labels and totals node-major in labT / tot ([N][ldT])
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
@@ -121,6 +122,10 @@ struct Ctx {
     // ... and the graph this many vertices (a bucket of a smaller graph is too few waves for the
     // replica-lane kernels: LFR-100k louvain 45.9 vs 31.2 ms, LFR-1M 175.8 vs 211 ms)
     int64_t rl_min_vertices = getenv("FC_RL_MIN_VERTICES") ? atoll(getenv("FC_RL_MIN_VERTICES")) : 262144;
+    // hybrid semantics: a filtered sweep visiting >= N/dense_div vertices keeps the shared order
+    // (without coarse rounds); 0 = never (FC_OPT_DENSE_DIV).  Measured no gain: LFR-1M 175.9 /
+    // 177.7 / 176.7 ms at 0 / 2 / 4, SBM-4M 712 / 759 / 722 ms (profiles/r04_dense_ab.txt)
+    int dense_div = 0;
     DevBuf rl_tot, rl_state;        // replica-lane totals [N][ldT] and per-replica state (kept apart from cd.hip's)
     DevBuf rl_colw;                 // replica-lane: (col << wbits) | weight per adjacency entry (weights < 256)
     DevBuf rl_slow, rl_slow_cnt;    // replica-lane: one bucket's visits left to the exact kernel

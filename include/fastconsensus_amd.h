@@ -162,6 +162,9 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 replica-lane engine (default 16).  Speed only: same results.     */
 #define FC_OPT_RL_MIN_VERTICES 16 /* hybrid: ... and the smallest graph (default 262144 vertices;
                                 below it cd.hip runs the full sweeps too).  Speed only.          */
+#define FC_OPT_DENSE_DIV 17  /* hybrid semantics: a filtered sweep that still visits >= n/dense_div
+                                vertices keeps the shared order (single-bucket rounds); default 0
+                                = the shared order for full sweeps only (twin: dense_div)        */
 int fc_set_option(fc_ctx* ctx, int option, int64_t value);
 
 /* ---- graph (replaces nx.read_edgelist + G.copy() + weight reset, :131-136, :434) ---- */

@@ -892,12 +892,13 @@ static int tw_coarse(i64 N, i64 V, int B, int gmax) {
 /* shared: 1 the replica-lane engine (cd_rl.hip) -- every replica visits the vertices in the SAME
  * per-(iteration, sweep) order (its stream key uses TW_SHARED_RG in place of the replica
  * index); tie keys stay per replica.  0: the classic engine's per-replica orders.  2: the
- * hybrid (FC_OPT_CD_ENGINE=2) -- the shared order while the replica's sweeps visit every
- * vertex, its own order from its first filtered (pruned) sweep on. */
+ * hybrid (FC_OPT_CD_ENGINE=2) -- the shared order while the replica's sweep visits every vertex
+ * or at least N/dense_div of them (a dense filtered sweep, run without coarse rounds), its own
+ * order (and coarse rounds) once its filtered list is sparser. */
 #define TW_SHARED_RG 0xffffffffu
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
                       u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
-                      int coarsen, int lm, int shared, i32* lab) {
+                      int coarsen, int lm, int shared, int dense_div, i32* lab) {
     const int louv = algo == 0;
     i64* tot = (i64*)malloc(sizeof(i64) * (size_t)N);
     i32* csz = (i32*)malloc(sizeof(i32) * (size_t)N);
@@ -919,7 +920,15 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     int track_now = 0, prune_now = 0;   /* adaptive pruning state (engine: k_sweep_end) */
     for (; sweep < max_sweeps && active; ++sweep) {
         const int filtered = prune && sweep > 0 && prune_now;
-        const uint32_t prg = (shared == 1 || (shared == 2 && !filtered)) ? TW_SHARED_RG : rg;   /* order key */
+        /* hybrid: a filtered sweep that still visits >= N/dense_div vertices ("dense") keeps the
+         * shared order, in single-bucket rounds (no coarsening); dense_div = 0: never */
+        int dense = 0;
+        if (shared == 2 && filtered && dense_div > 0) {
+            i64 V = 0;
+            for (i64 v = 0; v < N; ++v) V += aff[v] != 0;
+            dense = (i64)dense_div * V >= N;
+        }
+        const uint32_t prg = (shared == 1 || (shared == 2 && (!filtered || dense))) ? TW_SHARED_RG : rg;
         const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, prg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
         const uint32_t off = tw_chunk_off(chunk, seed, prg, iter, (uint32_t)sweep);
@@ -943,7 +952,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
             loff[B] = n;
         }
         /* rounds: one bucket each, or g consecutive buckets of a filtered sweep */
-        const int g = (listed && prune_now && coarsen) ? tw_coarse(N, loff[B], B, coarsen) : 1;
+        const int g = (listed && prune_now && coarsen && !dense) ? tw_coarse(N, loff[B], B, coarsen) : 1;
         for (int k = 0; k < B; k += g) {
             const int k1 = k + g < B ? k + g : B;
             i64 blen = PN - (i64)k * S;
@@ -1029,7 +1038,7 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
  * lab: [n_r][N] raw community ids (not renumbered), sweeps: [n_r]. */
 void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, int n_r, int rbase,
                    int iteration, u64 seed, int buckets, int max_sweeps, int chunk, int prune, int coarsen,
-                   int prune_mark, int shared, i32* lab, int* sweeps) {
+                   int prune_mark, int shared, int dense_div, i32* lab, int* sweeps) {
     i64* kdeg = (i64*)malloc(sizeof(i64) * (size_t)(N ? N : 1));
     i64 M2 = 0;
     i32 max_w = 0;
@@ -1045,7 +1054,7 @@ void orc_engine_cd(int algo, i64 N, const i64* rowptr, const i32* col, const i32
 #pragma omp parallel for schedule(dynamic, 1)
     for (int r = 0; r < n_r; ++r) {
         int sw = tw_replica(algo, N, rowptr, col, cw, kdeg, M2, seed, (uint32_t)(rbase + r), (uint32_t)iteration,
-                            buckets, max_sweeps, chunk, prune, coarsen, lm, shared, lab + (i64)r * N);
+                            buckets, max_sweeps, chunk, prune, coarsen, lm, shared, dense_div, lab + (i64)r * N);
         if (sweeps) sweeps[r] = sw;
     }
     free(kdeg);

@@ -75,7 +75,7 @@ def lib():
         L.orc_modularity.restype = dbl
         L.orc_engine_cd.argtypes = [ctypes.c_int, i64, _i64p, _i32p, _i32p, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
         L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
         L.orc_infomap_full.argtypes = [i64, _i64p, _i32p, u64, ctypes.c_int, _i32p, ctypes.POINTER(dbl)]
@@ -281,8 +281,11 @@ def infomap_full(g, seed, trials=10):
     return lab, L, core.value
 
 
+DENSE_DIV = 0   # the engine's default (fc_ctx.h dense_div, FC_OPT_DENSE_DIV)
+
+
 def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8,
-              prune_mark=1, shared=2):
+              prune_mark=1, shared=2, dense_div=DENSE_DIV):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels).  Defaults = the
     default engine (fc_ctx.h): the hybrid, FC_OPT_CD_ENGINE=2, shared=2 (a replica's full sweeps
     in the batch's shared order, its filtered sweeps in its own).  The classic engine (cd.hip
@@ -292,7 +295,7 @@ def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, 
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)
     lib().orc_engine_cd(_cd_algo(algo), g.N, rowptr, col, cw, n_r, rbase, iteration, int(seed) & (2**64 - 1), buckets,
-                        max_sweeps, chunk, prune, coarsen, prune_mark, shared, lab, sw)
+                        max_sweeps, chunk, prune, coarsen, prune_mark, shared, dense_div, lab, sw)
     return lab, sw
 
 

@@ -12,7 +12,8 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1, shared=2):
+    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1, shared=2,
+                 dense_div=orc.DENSE_DIV):
         """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity.  Defaults:
         the default (hybrid) CD engine, FC_OPT_CD_ENGINE=2; shared=0 models the classic engine,
         shared=1, coarsen=0 the replica-lane engine (FC_OPT_CD_ENGINE=1, cd_rl.hip: one shared
@@ -24,6 +25,7 @@ class OracleEngine:
         self.coarsen = coarsen
         self.prune_mark = prune_mark
         self.shared = shared
+        self.dense_div = dense_div
         self.sigma = None if sigma is None else np.asarray(sigma, np.int32)
         self.lab = None
 
@@ -65,7 +67,7 @@ class OracleEngine:
         else:
             self.lab, _ = orc.engine_cd(algo, self.g, count, r0, iteration, self.seed, buckets=self.buckets,
                                         chunk=self.chunk, prune=self.prune, coarsen=self.coarsen,
-                                        prune_mark=self.prune_mark, shared=self.shared)
+                                        prune_mark=self.prune_mark, shared=self.shared, dense_div=self.dense_div)
         self.r0 = r0
 
     def consensus_partial(self, algo, out):

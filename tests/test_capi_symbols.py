@@ -65,7 +65,7 @@ def test_cpu_twin_defaults_match_engine_defaults():
     from oracle import oracle as orc
     from tests.cpu_engine import OracleEngine
     src = open(os.path.join(ROOT, "fastconsensus_amd", "csrc", "fc_ctx.h")).read()
-    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen", "prune_mark")}
+    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen", "prune_mark", "dense_div")}
     # the default CD engine is the hybrid (FC_OPT_CD_ENGINE=2): the twin's shared=2
     assert int(re.search(r"\bcd_engine = (\d+)", src).group(1)) == 2
     eng["shared"] = 2

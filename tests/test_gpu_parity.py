@@ -239,6 +239,37 @@ def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen,
     eng.close()
 
 
+@pytest.mark.parametrize("engine", [2, 3])
+@pytest.mark.parametrize("dense_div", [0, 2, 4, 16])
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cd_hybrid_dense_lists_bit_exact_vs_twin(fcmod, algo, dense_div, engine):
+    """FC_OPT_DENSE_DIV: a filtered sweep whose list still holds >= N/dense_div vertices keeps the
+    shared order in single-bucket rounds (0: only full sweeps do) -- on the replica-lane kernels
+    (engine 2) and on cd.hip alone (3), the input graph and a weighted consensus graph."""
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=57)
+    kw = _engine(eng, engine, 0, 8)
+    eng.set_option("dense_div", dense_div)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    eng.cd(algo, 0, 12, 12, 5)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, 12, 0, 5, 57, dense_div=dense_div, **kw)
+    np.testing.assert_array_equal(eng.get_labels(12), exp)
+    eng.close()
+    case, eng = _weighted_consensus_engine(fcmod, 59)
+    kw = _engine(eng, engine, 0, 8)
+    eng.set_option("dense_div", dense_div)
+    u, v, w, _ = eng.get_graph()
+    sigma = eng.node_map()
+    a_, b_ = sigma[u], sigma[v]
+    lo, hi = np.minimum(a_, b_), np.maximum(a_, b_)
+    o = np.lexsort((hi, lo))
+    g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
+    eng.cd(algo, 0, 12, 12, 6)
+    exp, _ = orc.engine_cd(algo, g_int, 12, 0, 6, 59, dense_div=dense_div, **kw)
+    np.testing.assert_array_equal(eng.get_labels(12), exp[:, sigma])
+    eng.close()
+
+
 @pytest.mark.parametrize("algo", [0, 1])
 @pytest.mark.parametrize("n_r", [1, 13, 33, 64, 70, 130])
 def test_cd_replica_lanes_bit_exact_vs_twin(fcmod, algo, n_r):
