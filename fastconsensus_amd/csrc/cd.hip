@@ -291,6 +291,7 @@ struct WaveShared {
     long long kv[WNT];
     int32_t vm[WNT], own[WNT], kown[WNT];
     uint32_t tvh[WNT];
+    int32_t hope[WNT];           // Louvain: some candidate may gain (else no Sigma is gathered)
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -479,6 +480,15 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         if (ko > ws.k2[lane]) ws.k2[lane] = ko;   // every other lane's max landed before the barrier
     }
     if (!LOUV && lane < WNT && ws.k2[lane]) ws.vm[lane] = (int32_t)(ws.k2[lane] >> 32);   // read by this lane only
+    if (LOUV) {
+        // no candidate can gain when even weight vm at Sigma = 0 cannot: (vm - k_own)*2M +
+        // k_v*(Sigma_own - k_v) <= 0 (score_c <= vm*2M for every c) -- then the vertex stays and
+        // no Sigma is gathered (most vertices of a settled sweep)
+        if (lane < WNT)
+            ws.hope[lane] = (work && ws.vm[lane] != INT_MIN &&
+                             ((long long)ws.vm[lane] - ws.kown[lane]) * a.M2 + kv * ((long long)tot_own - kv) > 0) ? 1 : 0;
+        wave_sync();
+    }
     PST(5);
     int ncand = 0;
     auto score = [&](int32_t val, long long tt, long long kvt) -> long long {
@@ -511,7 +521,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             if (it >= nl) break;
             if (rec[it] < 0) continue;
             const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
-            if (ws.val[sl] == ws.vm[t]) tg[it] = totr[ws.key[sl]];
+            if (ws.val[sl] == ws.vm[t] && ws.hope[t]) tg[it] = totr[ws.key[sl]];
         }
         if constexpr (PK) {
 #pragma unroll
@@ -545,6 +555,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
             if (it >= nl) break;
             if (rec[it] < 0 || tg[it] >= 0) continue;
             const int t = rec[it] >> 8;
+            if (!ws.hope[t]) continue;
             const long long b1 = PK ? ws.b1[t] : score(ws.vm[t], ws.tmin[t], ws.kv[t]);
             need |= (long long)ws.val[t * HCAP + (rec[it] & 255)] * a.M2 >= b1;
         }
@@ -555,6 +566,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
                 if (it >= nl) break;
                 if (rec[it] < 0 || tg[it] >= 0) continue;
                 const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+                if (!ws.hope[t]) continue;
                 const int32_t val = ws.val[sl];
                 if ((long long)val * a.M2 < score(ws.vm[t], ws.tmin[t], ws.kv[t])) continue;
                 tg[it] = totr[ws.key[sl]];
@@ -590,7 +602,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     Visit out;
     out.dcs = -1; out.dq = 0; out.unst = 0; out.ncand = ncand; out.d = d; out.work = work; out.heavy = heavy;
     out.own = own; out.kvw = (int32_t)kv;
-    if (work && ws.vm[lane] != INT_MIN) {        // some candidate besides the own community (Louvain)
+    if (work && ws.vm[lane] != INT_MIN && (!LOUV || ws.hope[lane])) {   // a candidate that may gain (Louvain)
         const long long best_s = best_of(lane);
         {
             const int32_t best_c = !LOUV ? (int32_t)(hash32_inv((uint32_t)ws.k2[lane]) ^ ws.tvh[lane])

@@ -504,9 +504,14 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
         }
         if (!LOUV) kown = kl;
     }
+    // Louvain: no candidate can gain when even weight vm at Sigma = 0 cannot, i.e. when
+    // (vm - k_own)*2M + k_v*(Sigma_own - k_v) <= 0 (score_c <= vm*2M for every c): then no
+    // Sigma is gathered and the vertex stays (in settled sweeps most vertices)
+    bool hope = true;
+    if (LOUV) hope = wk && ((long long)vm - kown) * a.M2 + (long long)h.kvi * ((long long)tot_own - h.kvi) > 0;
     // pass B: candidate runs (the runs of weight vm), as bits of cm
     uint32_t cm_lo = 0, cm_hi = 0;
-    {
+    if (hope) {
         int acc = 0;
 #pragma unroll
         for (int q = 0; q < K; ++q) {
