@@ -486,6 +486,15 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
         }
         kown = ko;
     }
+    // Louvain, settled vertex: every foreign community weighs at most k_v - k_own, so no move can
+    // gain when (k_v - 2 k_own)*2M + k_v*(Sigma_own - k_v) <= 0.  When that holds on every lane
+    // (the vertex is settled in all the wave's replicas -- most of a consensus graph), the sort
+    // and the passes are skipped.
+    if (LOUV) {
+        const long long kvl = h.kvi;
+        const bool settled = !wk || (kvl - 2 * kown) * a.M2 + kvl * ((long long)tot_own - kvl) <= 0;
+        if (__ballot(!settled) == 0) return -1;                 // wave-uniform
+    }
     bitonic_sort<K>(x);
     // run ends and summed weights: e = bit q set when the run of equal labels ends at q
     // pass A: the largest weight vm
