@@ -124,11 +124,6 @@ template <int MODE> __device__ __forceinline__ int lv_entry_bytes(bool weighted)
     return 4 + (weighted ? 4 : 0) + (MODE == MODE_REFINE ? 8 : 4);
 }
 template <int MODE> __device__ __forceinline__ constexpr int lv_cand_bytes() { return MODE == MODE_INFO ? 16 : 8; }
-// wave sum of a per-lane byte count, one atomic per wave into the block's shard
-__device__ __forceinline__ void lv_count(unsigned long long* dst, unsigned long long v) {
-    for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst + (blockIdx.x & (MSH - 1)), v);
-}
 
 __device__ __forceinline__ double plogp2(double p) { return p > 0.0 ? p * log2(p) : 0.0; }
 // The map-equation change split into the part of the source module A (computed once per
@@ -255,7 +250,7 @@ __device__ __forceinline__ int tins(int32_t* keys, int32_t* vals, uint32_t nslot
 template <int MODE, int UNR>
 __device__ __forceinline__ void row_insert(const LvArgs& a, int64_t base, int64_t j0, int64_t re, int ST, int32_t own,
                                            int32_t pc, int32_t* keys, int32_t* vals, uint32_t ts, long long& wl,
-                                           uint32_t& c_ent, int32_t* lst, int* s_n) {
+                                           int32_t* lst, int* s_n) {
     for (int64_t j = j0; j < re; j += (int64_t)ST * UNR) {
         int64_t y[UNR];
         int32_t wy[UNR], cy[UNR];
@@ -275,7 +270,6 @@ __device__ __forceinline__ void row_insert(const LvArgs& a, int64_t base, int64_
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
             if (y[u] < 0) continue;
-            ++c_ent;
             if (cy[u] < 0) continue;
             // entries in the own community are summed in registers, not inserted: on aggregated
             // levels they are a large share of a row, all on one LDS address
@@ -360,11 +354,15 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     constexpr int GL = 64 / G, TSG = TS / G;
     __shared__ int32_t skey[LTB / 64][TS], sval[LTB / 64][TS];
     __shared__ int s_cnt;
+    __shared__ uint32_t s_bytes;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_cnt = 0;
+    if (threadIdx.x == 0) { s_cnt = 0; s_bytes = 0; }
     __syncthreads();
-    // this lane's share of the algorithmic bytes: scanned / decided vertices, movers, entries, candidates
-    uint32_t c_scan = 0, c_vtx = 0, c_mov = 0, c_ent = 0, c_cand = 0;
+    // this lane's share of the algorithmic bytes (scanned / decided vertices, movers, entries,
+    // candidates), ONE accumulator: five counters cost the Infomap instance an occupancy step
+    // (88 -> 100 VGPRs, 5 -> 4 waves per SIMD: LFR-100k infomap 5.31 -> 5.82 s)
+    uint32_t c_b = 0;
+    const uint32_t eb = (uint32_t)lv_entry_bytes<MODE>(a.w != nullptr);
     int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
     if (IMPL && a.bmap) {
         const int64_t loc = (int64_t)(blockIdx.x % a.bpr) * LTB + threadIdx.x;
@@ -372,7 +370,8 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     }
     bool elig = false;
     if (x0 < a.nU) {
-        c_scan = 1;   // the eligibility scan: replica id (explicit levels), queue flag / refined size
+        // the eligibility scan: replica id (explicit levels), queue flag / refined size
+        c_b = (IMPL ? 0 : 4) + (MODE == MODE_MOVE ? 1 : MODE == MODE_REFINE ? 8 : 0);
         const int32_t r = rep_of<IMPL>(a, x0);
         if (!a.done[r] && in_bucket(a, r, x0, bucket)) {
             if (MODE == MODE_MOVE) {
@@ -429,8 +428,9 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         const int32_t own = valid ? (MODE == MODE_REFINE ? a.R[x] : a.P[x]) : -1;
         const int32_t pc = valid ? a.P[x] : -1;
         long long wl = 0;   // Infomap: weight to the own module
-        c_vtx += (valid && gl == 0) ? 1u : 0u;
-        row_insert<MODE, 1>(a, base, rb + gl, re, GL, own, pc, keys, vals, ts, wl, c_ent, nullptr, nullptr);
+        // the vertex's record and its row's entries, counted once by the group's first lane
+        c_b += (valid && gl == 0) ? (uint32_t)lv_vertex_bytes<MODE>() + (uint32_t)(re - rb) * eb : 0u;
+        row_insert<MODE, 1>(a, base, rb + gl, re, GL, own, pc, keys, vals, ts, wl, nullptr, nullptr);
         wsync();
         const long long kvx = valid ? kv_of<IMPL>(a, x) : 0;
         const int32_t rx = valid ? rep_of<IMPL>(a, x) : 0;
@@ -453,11 +453,11 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             wown = wl;
             wave_scan<GL>(a, keys, vals, ts, own, kvx, rx, x, bs, bh, bc, wown, ncand);
         }
-        c_cand += valid ? (uint32_t)ncand : 0u;
+        c_b += valid ? (uint32_t)ncand * (uint32_t)lv_cand_bytes<MODE>() : 0u;
         if (valid && gl == 0) {
             const int32_t t = MODE == MODE_INFO ? bc : lv_final<MODE>(a, x, own, kvx, wown, bs, bc);
             if (t >= 0) {
-                ++c_mov;
+                c_b += (uint32_t)lv_mover_bytes<MODE>();
                 const int p = atomicAdd(&s_cnt, 1);
                 const int64_t q = (int64_t)blockIdx.x * LTB + p;
                 a.blist[q] = (int32_t)x;
@@ -468,12 +468,14 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
         }
         wsync();
     }
-    lv_count(a.lvb, (unsigned long long)c_scan * ((IMPL ? 0 : 4) + (MODE == MODE_MOVE ? 1 : MODE == MODE_REFINE ? 8 : 0)) +
-                        (unsigned long long)c_vtx * lv_vertex_bytes<MODE>() + (unsigned long long)c_mov * lv_mover_bytes<MODE>() +
-                        (unsigned long long)c_ent * lv_entry_bytes<MODE>(a.w != nullptr) +
-                        (unsigned long long)c_cand * lv_cand_bytes<MODE>());
+    // the block's bytes through one LDS word (a 64-bit wave reduction here cost the Infomap
+    // instance 10 VGPRs: 90 -> 100, one occupancy step)
+    if (c_b) atomicAdd(&s_bytes, c_b);
     __syncthreads();
-    if (threadIdx.x == 0) a.bcnt[blockIdx.x] = s_cnt;
+    if (threadIdx.x == 0) {
+        a.bcnt[blockIdx.x] = s_cnt;
+        if (s_bytes) atomicAdd(a.lvb + (blockIdx.x & (MSH - 1)), (unsigned long long)s_bytes);
+    }
 }
 
 // Block reduction of (score, tie, community) candidates; thread 0 ends with the best.
@@ -542,7 +544,8 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
     const int n = a.heavy_cnt[tier];
     const int32_t* hlist = a.heavy + tier * a.hcap;
     int32_t* htgt = a.htgt + tier * a.hcap;
-    uint32_t c_vtx = 0, c_ent = 0, c_cand = 0;   // this thread's share of the algorithmic bytes
+    uint32_t c_b = 0;   // this thread's share of the algorithmic bytes
+    const uint32_t eb = (uint32_t)lv_entry_bytes<MODE>(a.w != nullptr);
     int32_t* gkey = a.hkey + (int64_t)blockIdx.x * a.hslots;
     int32_t* gval = a.hval + (int64_t)blockIdx.x * a.hslots;
     int32_t* lst = a.hlst + (int64_t)blockIdx.x * a.hslots;
@@ -562,8 +565,9 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
         const int32_t own = MODE == MODE_REFINE ? a.R[x] : a.P[x];
         const int32_t pc = a.P[x];
         long long wl = 0;
-        c_vtx += threadIdx.x == 0 ? 1u : 0u;
-        row_insert<MODE, UNR>(a, base, rb + threadIdx.x, re, LTB, own, pc, keys, vals, ts, wl, c_ent, lds ? nullptr : lst,
+        c_b += threadIdx.x == 0 ? (uint32_t)(lv_vertex_bytes<MODE>() + 4 /* heavy list */ + 4 /* htgt */) +
+                                      (uint32_t)(re - rb) * eb : 0u;
+        row_insert<MODE, UNR>(a, base, rb + threadIdx.x, re, LTB, own, pc, keys, vals, ts, wl, lds ? nullptr : lst,
                          &s_n);
         if (MODE == MODE_INFO && wl) atomicAdd((unsigned long long*)&s_wown, (unsigned long long)wl);
         __syncthreads();
@@ -609,7 +613,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
 #pragma unroll
             for (int u = 0; u < UNR; ++u) {
                 if (k[u] < 0) continue;
-                ++c_cand;
+                c_b += (uint32_t)lv_cand_bytes<MODE>();
                 const uint32_t h = tie_of(a, r, x, k[u]);
                 if (MODE == MODE_INFO) {
                     const double d = info_b(a.inv, IA, qr, tk2[u], tk[u], kvx, svx, val[u]);
@@ -637,9 +641,12 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
         }
         __syncthreads();
     }
-    lv_count(a.lvb + MSH, (unsigned long long)c_vtx * (lv_vertex_bytes<MODE>() + 4 /* heavy list */ + 4 /* htgt */) +
-                            (unsigned long long)c_ent * lv_entry_bytes<MODE>(a.w != nullptr) +
-                            (unsigned long long)c_cand * lv_cand_bytes<MODE>());
+    __shared__ uint32_t s_bytes;                      // the block's bytes through one LDS word (k_lv_decide)
+    if (threadIdx.x == 0) s_bytes = 0;
+    __syncthreads();
+    if (c_b) atomicAdd(&s_bytes, c_b);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_bytes) atomicAdd(a.lvb + MSH + (blockIdx.x & (MSH - 1)), (unsigned long long)s_bytes);
 }
 
 // Apply one bucket's moves, one wave per mover: blocks [0, nblk) take the decide blocks'
