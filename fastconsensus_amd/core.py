@@ -307,7 +307,10 @@ class IdGraph:
     order whose per-node first occurrences reproduce networkx adjacency order."""
 
     def __init__(self, labels, u, v):
-        self.labels = np.asarray(labels)
+        lab = np.asarray(labels)
+        if lab.ndim != 1:      # tuple nodes (grid graphs ...): one object per node, not a 2-D array
+            lab = np.fromiter(labels, dtype=object, count=len(labels))
+        self.labels = lab
         self.u = np.ascontiguousarray(u, dtype=np.int32)
         self.v = np.ascontiguousarray(v, dtype=np.int32)
 
@@ -411,14 +414,18 @@ def labels_to_output(algorithm, node_labels, labels):
             vl[vid] = lab
             out.append(Cover(vl))
         return out
+    na = np.asarray(node_labels)
     for lab in labels:
         if algorithm == "louvain":
             out.append(dict(zip(nodes, lab.tolist())))
         else:
-            groups = {}
-            for node, c in zip(nodes, lab.tolist()):
-                groups.setdefault(c, []).append(node)
-            out.append({frozenset(g) for g in groups.values()})
+            # the communities as runs of one stable sort by label (C speed; a frozenset per run)
+            lab = np.asarray(lab)
+            order = np.argsort(lab, kind="stable")
+            sl = lab[order]
+            b = [0] + (np.flatnonzero(sl[1:] != sl[:-1]) + 1).tolist() + [len(sl)]
+            srt = na[order].tolist()
+            out.append({frozenset(srt[b[i]:b[i + 1]]) for i in range(len(b) - 1)} if len(sl) else set())
     return out
 
 

@@ -101,7 +101,7 @@ def test_networkx_input_order_is_adjacency_order():
     assert pairs.index((1, 2)) < pairs.index((1, 3))
 
 
-@pytest.mark.parametrize("labels", ["ints", "shuffled", "strings", "sparse_ints"])
+@pytest.mark.parametrize("labels", ["ints", "shuffled", "strings", "sparse_ints", "tuples"])
 def test_networkx_conversion_matches_literal_walk(labels):
     """The vectorised IdGraph.from_networkx equals the literal walk (every node in G.nodes()
     order, its later neighbours in G.adj order) for integer, shuffled, string and sparse labels."""
@@ -120,12 +120,36 @@ def test_networkx_conversion_matches_literal_walk(labels):
         G = nx.relabel_nodes(G, {i: "v%d" % (i * 7 % 600) for i in G.nodes()})
     elif labels == "sparse_ints":
         G = nx.relabel_nodes(G, {i: i * 100003 for i in G.nodes()})
+    elif labels == "tuples":                       # grid-style nodes: one object each, not a 2-D array
+        G = nx.relabel_nodes(G, {i: (i // 30, i % 30) for i in G.nodes()})
     nodes = list(G.nodes())
     idx = {x: i for i, x in enumerate(nodes)}
     exp = [(idx[x], idx[z]) for x in nodes for z in G.adj[x] if idx[z] > idx[x]]
     g = IdGraph.from_networkx(G)
     assert list(g.labels) == nodes
     assert list(zip(g.u.tolist(), g.v.tolist())) == exp
+
+
+@pytest.mark.parametrize("kind", ["ints", "strings", "tuples"])
+def test_partition_output_matches_literal_grouping(kind):
+    """labels_to_output (lpm / infomap: a set of frozensets per labeling, fast_consensus.py:383-392)
+    equals the literal per-node grouping, for integer, string and tuple nodes and ragged labels."""
+    from fastconsensus_amd.core import IdGraph, labels_to_output
+    rng = np.random.default_rng(7)
+    n = 500
+    nodes = {"ints": list(range(n)), "strings": ["v%d" % (i * 7 % n) for i in range(n)],
+             "tuples": [(i // 25, i % 25) for i in range(n)]}[kind]
+    g = IdGraph(nodes, np.zeros(0, np.int32), np.zeros(0, np.int32))
+    labels = np.stack([rng.integers(0, k, n) for k in (1, 7, 200, n)]).astype(np.int32)
+    out = labels_to_output("lpm", g.labels, labels)
+    for lab, got in zip(labels, out):
+        groups = {}
+        for x, c in zip(nodes, lab.tolist()):
+            groups.setdefault(c, []).append(x)
+        assert got == {frozenset(v) for v in groups.values()}
+    d = labels_to_output("louvain", g.labels, labels[:1])[0]
+    assert list(d.keys()) == nodes and list(d.values()) == labels[0].tolist()
+    assert labels_to_output("lpm", g.labels, labels[:0]) == []
 
 
 def test_unknown_and_out_of_scope_algorithms():

@@ -2,7 +2,7 @@
 """A/B of CD-kernel variants on one graph (GPU box).  Each variant is a library path (variant
 builds from tools/build_variant.sh; `base` = the in-tree library) run in its own process:
 
-    python tools/cd_ab.py [--config lfr1m] [--algo 0] [--reps 3] base name1 name2 ...
+    python tools/cd_ab.py [--config lfr1m] [--algo 0] [--reps 3] [--np N] base name1 name2 ...
 
 Per variant: one CD batch of n_p replicas on the input graph (fc_cd, iteration 0) timed with
 the engine's HIP events (cd_ms, decide_ms, launches), a whole fc_run, and a hash of the
@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib, config, algo, reps):
+def child(lib, config, algo, reps, np_over=0):
     os.environ["FC_LIB_PATH"] = lib
     sys.path.insert(0, ROOT)
     import time
@@ -28,6 +28,8 @@ def child(lib, config, algo, reps):
     import fastconsensus_amd as fc
     cfg = dict(bench.CONFIGS[config])
     n, u, v, _ = bench.make_graph(cfg, 42)
+    if np_over:
+        cfg["n_p"] = np_over
     n_p = cfg["n_p"]
     out = {"lib": lib}
     with fc.Engine(seed=42) as eng:
@@ -86,9 +88,9 @@ def child(lib, config, algo, reps):
 def main():
     args = sys.argv[1:]
     if args and args[0] == "--child":
-        child(args[1], args[2], int(args[3]), int(args[4]))
+        child(args[1], args[2], int(args[3]), int(args[4]), int(args[5]))
         return
-    config, algo, reps = "lfr1m", 0, 3
+    config, algo, reps, np_over = "lfr1m", 0, 3, 0
     while args and args[0].startswith("--"):
         k, val = args[0], args[1]
         args = args[2:]
@@ -98,6 +100,8 @@ def main():
             algo = int(val)
         elif k == "--reps":
             reps = int(val)
+        elif k == "--np":
+            np_over = int(val)
     for spec in args or ["base"]:
         # name[@ENV=VAL,ENV=VAL]: a variant library and engine environment switches
         name, _, envs = spec.partition("@")
@@ -108,7 +112,7 @@ def main():
         lib = os.path.join(ROOT, "fastconsensus_amd", "lib",
                            "libfastconsensus_amd.so" if name == "base" else name + "/libfastconsensus_amd.so")
         print("variant", spec, flush=True)
-        rc = subprocess.call([sys.executable, __file__, "--child", lib, config, str(algo), str(reps)], env=env)
+        rc = subprocess.call([sys.executable, __file__, "--child", lib, config, str(algo), str(reps), str(np_over)], env=env)
         if rc != 0:
             print("variant %s failed rc=%d" % (name, rc), flush=True)
             sys.exit(rc)
