@@ -1468,6 +1468,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..4] | n_active[0] at [6]
     const int sweep0 = h ? h->sweep0 : 0;
     int sweep = sweep0;
+    if (c.trace && !h) { sync(c); trace_dt_us(true); }   // a hand-off's first sweep includes the conversion
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
         FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
@@ -1511,14 +1512,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         else k_sweep_end<false><<<1, TB, 0, c.stream>>>(a, n_active);
         if (c.trace) {
             sync(c);
-            static auto t_last = std::chrono::steady_clock::now();
-            const auto t_now = std::chrono::steady_clock::now();
             int32_t st4[4];   // n_active[0] active, [2..3] moves of this sweep (all replicas)
             FC_HIP(hipMemcpy(st4, n_active, sizeof(st4), hipMemcpyDeviceToHost));
             fprintf(stderr, "[fc] cd it=%d sweep=%d rounds=%d visits=%llu moves=%llu active=%d dt_us=%.0f\n", iteration,
-                    sweep, rounds, visits, *(unsigned long long*)(st4 + 2), st4[0],
-                    1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
-            t_last = t_now;
+                    sweep, rounds, visits, *(unsigned long long*)(st4 + 2), st4[0], trace_dt_us());
         }
     }
     // replica-sweeps and light-kernel traffic counters for the roofline model

@@ -3,12 +3,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <chrono>
 #include <string>
 #include <vector>
 
 #include "../../include/fastconsensus_amd.h"
 
 namespace fc {
+
+// FC_TRACE: microseconds since the previous trace mark -- one clock shared by every engine
+// (cd.hip, cd_rl.hip, leiden.hip), so a line's dt is the work since the line before it;
+// reset = true marks a batch start (returns 0)
+inline double trace_dt_us(bool reset = false) {
+    static std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+    const auto now = std::chrono::steady_clock::now();
+    const double dt = 1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(now - last).count();
+    last = now;
+    return reset ? 0.0 : dt;
+}
 
 void set_error(const std::string& msg);
 

@@ -1538,12 +1538,9 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         a.B = B;
         if (c.trace) {
             sync(c);
-            static auto t_last = std::chrono::steady_clock::now();
-            const auto t_now = std::chrono::steady_clock::now();
             fprintf(stderr, "[fc] leiden level %d: %lld union vertices, %lld entries, max degree %d, %d move sweeps, "
                     "%.1f ms since the previous level\n", level + 1, (long long)nU, (long long)cur.E, max_deg, sw + 1,
-                    1e-3 * (double)std::chrono::duration_cast<std::chrono::microseconds>(t_now - t_last).count());
-            t_last = t_now;
+                    1e-3 * trace_dt_us());
         }
     }
     if (c.trace) fprintf(stderr, "[fc] %s it=%d: %d levels, %lld level sweeps\n", name, iteration, level + 1,
