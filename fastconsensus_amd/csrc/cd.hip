@@ -1498,6 +1498,10 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                 k_cd_tail<true, int32_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep, c.max_sweeps, tbuf, tmark, tail_acc, n_active);
             else
                 k_cd_tail<true, int64_t, TAIL_TB><<<rcount, TAIL_TB, 0, c.stream>>>(a, sweep, c.max_sweeps, tbuf, tmark, tail_acc, n_active);
+            if (c.trace) {
+                sync(c);
+                fprintf(stderr, "[fc] cd it=%d tail kernel dt_us=%.0f\n", iteration, trace_dt_us());
+            }
             break;
         }
         k_list_fill<<<dim3(lb_grid, rcount), TB, 2 * sizeof(int) * B, c.stream>>>(a, sweep, gco, cursor, list);

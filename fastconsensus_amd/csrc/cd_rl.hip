@@ -371,22 +371,24 @@ __device__ __forceinline__ Hdr rl_header(const RL& a, const Unit& u, const Rec& 
     return h;
 }
 
-// Bitonic sort of K keys held in registers (compile-time indices: 2 VALU per compare-exchange).
+// Ascending sort of K keys held in registers: Batcher's odd-even merge sort (K = 2^k; 63 / 191 /
+// 543 compare-exchanges at K = 16 / 32 / 64 against a bitonic network's 80 / 240 / 672; every
+// index is a compile-time constant, 2 VALU per compare-exchange).
 template <int K>
-__device__ __forceinline__ void bitonic_sort(int32_t (&x)[K]) {
+__device__ __forceinline__ void oem_sort(int32_t (&x)[K]) {
 #pragma unroll
-    for (int k = 2; k <= K; k <<= 1)
+    for (int p = 1; p < K; p <<= 1)
 #pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
+        for (int k = p; k >= 1; k >>= 1)
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const int32_t p = x[i], q = x[l];
-                    if ((i & k) == 0) { x[i] = min(p, q); x[l] = max(p, q); }
-                    else { x[i] = max(p, q); x[l] = min(p, q); }
-                }
-            }
+            for (int j = k % p; j + k < K; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; ++i)
+                    if ((i + j) / (2 * p) == (i + j + k) / (2 * p) && i + j + k < K) {
+                        const int32_t a = x[i + j], b = x[i + j + k];
+                        x[i + j] = min(a, b);
+                        x[i + j + k] = max(a, b);
+                    }
 }
 
 // One lane's decision from its row (K >= the wave's longest light row).  Keys are
@@ -495,7 +497,7 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
         const bool settled = !wk || (kvl - 2 * kown) * a.M2 + kvl * ((long long)tot_own - kvl) <= 0;
         if (__ballot(!settled) == 0) return -1;                 // wave-uniform
     }
-    bitonic_sort<K>(x);
+    oem_sort<K>(x);
     // run ends and summed weights: e = bit q set when the run of equal labels ends at q
     // pass A: the largest weight vm
     int vm = INT_MIN;
@@ -1383,6 +1385,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     const unsigned lgrid = nb(N, LTB * LPER);
     const size_t lcount_lds = sizeof(unsigned long long) * 2 * banks + 2 * sizeof(int) * nseg;
     int sweep = 0, handoff = -1;
+    if (c.trace) { sync(c); trace_dt_us(true); }
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         const int listed = (c.prune && sweep > 0) ? 1 : 0;
         FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * nseg, c.stream));
@@ -1486,14 +1489,11 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         else k_rl_sweep_end<false><<<1, 256, 0, c.stream>>>(a, n_active);
         if (c.trace) {
             sync(c);
-            static auto t_last = std::chrono::steady_clock::now();
-            const auto t_now = std::chrono::steady_clock::now();
             int32_t st8[8];
             FC_HIP(hipMemcpy(st8, n_active, sizeof(st8), hipMemcpyDeviceToHost));
             fprintf(stderr, "[fc] rl it=%d sweep=%d entries=%d visits=%llu moves=%llu active=%d dt_us=%.0f\n", iteration,
                     sweep, hb[nseg], *(unsigned long long*)(st8 + 6), *(unsigned long long*)(st8 + 2), st8[0],
-                    1e-3 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_now - t_last).count());
-            t_last = t_now;
+                    trace_dt_us());
         }
     }
     if (handoff < 0) {

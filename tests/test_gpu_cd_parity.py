@@ -138,10 +138,26 @@ def refsem(name):
         return json.load(f)
 
 
-def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds):
+# The CD engines held to the reference loop's distribution: the default (hybrid semantics; at
+# C2/C3 sizes on cd.hip alone), the hybrid with its replica-lane kernels forced at these sizes,
+# the classic engine (per-replica orders throughout) and the replica-lane engine alone (one
+# shared order in every sweep).  They differ from each other (different visit orders), each is
+# bit-exact against its twin elsewhere; here each must match the reference's distribution.
+ENGINE_OPTS = {"hybrid": {}, "hybrid_rl": {"rl_min_vertices": 1, "rl_min_replicas": 1},
+               "classic": {"cd_engine": 0}, "replica_lane": {"cd_engine": 1}}
+
+
+@pytest.fixture(params=sorted(ENGINE_OPTS))
+def engine_opts(request):
+    return ENGINE_OPTS[request.param]
+
+
+def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds, opts=None):
     out = []
     for seed in seeds:
         with fcmod.Engine(seed=seed) as eng:
+            for k, v in (opts or {}).items():
+                eng.set_option(k, v)
             eng.load_graph(N, e[:, 0], e[:, 1])
             labels, st = eng.run(algo, n_p, tau, delta)
         assert st["iterations"] >= 1 and not st["hit_iter_cap"]
@@ -149,7 +165,7 @@ def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds):
     return np.array(out)
 
 
-def test_c2_louvain_consensus_nmi_vs_reference(fcmod):
+def test_c2_louvain_consensus_nmi_vs_reference(fcmod, engine_opts):
     """The whole louvain consensus against the reference's own output.  The consensus NMI
     varies from run to run (0.78-0.95 on LFR-1k), so the device's mean over 32 seeds is held
     to the REFERENCE LOOP's mean over 30 seeds (its unmodified code with the restated CD,
@@ -159,7 +175,7 @@ def test_c2_louvain_consensus_nmi_vs_reference(fcmod):
     case = golden_io.load("lfr1k_louvain_np20")
     _, g, planted = lfr1k()
     ref = refsem("lfr1k_louvain_np20")
-    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(100, 132))
+    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(100, 132), engine_opts)
     one = float(np.mean([nmi(planted, l) for l in case.z["final_labels"]]))
     print("C2 louvain consensus NMI: device mean %.4f sd %.4f min %.4f | reference loop mean %.4f sd %.4f min %.4f "
           "| reference run's recorded output %.4f" % (got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"],
@@ -167,7 +183,7 @@ def test_c2_louvain_consensus_nmi_vs_reference(fcmod):
     assert got.mean() >= ref["nmi_mean"] - 0.025
 
 
-def test_c2_lpm_consensus_nmi_vs_reference(fcmod):
+def test_c2_lpm_consensus_nmi_vs_reference(fcmod, engine_opts):
     """lpm consensus on a graph where LPA sits at its detectability edge (native LFR n=1000
     mu=0.55: the reference loop either recovers the communities, NMI ~0.95, or collapses to one,
     NMI 0 -- 14 of 30 seeds recover).  Device over 24 seeds: recovery rate >= reference - 0.3
@@ -177,7 +193,7 @@ def test_c2_lpm_consensus_nmi_vs_reference(fcmod):
     ref = refsem("lfr1k_mu055_lpm_np20")
     e = np.loadtxt(golden_io.GOLDEN + "/lfr1k_mu055_synth.txt", dtype=np.int32).reshape(-1, 2)
     planted = np.load(golden_io.GOLDEN + "/lfr1k_mu055_synth_planted.npy")
-    got = device_runs(fcmod, 1, len(planted), e, 20, 0.8, 0.02, planted, range(200, 224))
+    got = device_runs(fcmod, 1, len(planted), e, 20, 0.8, 0.02, planted, range(200, 224), engine_opts)
     r_ok = np.array(ref["nmi"]) > 0.5
     d_ok = got > 0.5
     case = golden_io.load("lfr1k_lpm_np20")
@@ -248,7 +264,7 @@ def test_c3_consensus_update_bit_exact_and_run(fcmod, lfr100k, algo, tau):
         assert s > 0.8
 
 
-def test_c3_consensus_nmi_vs_reference_semantics(fcmod, lfr100k):
+def test_c3_consensus_nmi_vs_reference_semantics(fcmod, lfr100k, engine_opts):
     """BASELINE configs[2] louvain and lpm, n_p=64: the device's whole-consensus NMI to the
     planted communities (mean of the n_p final partitions, fast_consensus.py:383-392), averaged
     over 8 seeds, against the reference loop's distribution at the same size
@@ -258,7 +274,7 @@ def test_c3_consensus_nmi_vs_reference_semantics(fcmod, lfr100k):
     n, e, planted = lfr100k
     for algo, name, tau, tol in ((0, "lfr100k_louvain_np64", 0.2, 0.01), (1, "lfr100k_lpm_np64", 0.8, 0.02)):
         ref = refsem(name)
-        got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 308))
+        got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 308), engine_opts)
         print("C3 %s consensus NMI: device mean %.4f sd %.4f min %.4f | reference semantics mean %.4f sd %.4f min %.4f"
               % (name, got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"], min(ref["nmi"])))
         assert got.mean() >= ref["nmi_mean"] - tol
