@@ -403,100 +403,24 @@ __device__ __forceinline__ void oem_sort(int32_t (&x)[K]) {
 // colw and kept 4 per register while the label gathers are in flight (weights < 256), WM_WIDE a
 // separate cw row (one register per entry)
 constexpr int WM_WIDE = 0, WM_UNIT = 1, WM_W8 = 2;
+// FC_RL_LPA_OWN (A/B switch, default on): LPA keeps its own-label entries out of the keys too
+// (counted in k_own; the own label a candidate when k_own is the largest count), so a wave whose
+// lanes are all settled (2 k_own > d: own is the unique majority) skips like Louvain's, and the
+// sort networks hold fewer live keys (LPA K = 32: 146 -> 126 VGPRs, 3 -> 4 waves per SIMD)
+#ifndef FC_RL_LPA_OWN
+#define FC_RL_LPA_OWN 1
+#endif
+// The decision from a lane's K keys ((label << wbits) | weight, -1 for empty and own-label
+// entries -- LPA's too under FC_RL_LPA_OWN): sort, runs, candidates (rl_sorted's second half).
 template <bool LOUV, int K, int WM>
-__device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
-                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
+__device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep, int32_t (&x)[K], int32_t own,
+                                           long long kown, int32_t tot_own, uint32_t home, unsigned long long& c_dq,
+                                           uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
     constexpr bool UNITW = WM == WM_UNIT;
-    slow_out = false;
     const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
     const int wb = UNITW ? 0 : a.wbits;
     const int32_t wm = (1 << wb) - 1;
     const bool wk = h.work;
-    // padding / idle lanes read a slot of their own vertex's row (cached, distinct per wave)
-    // instead of branching; never a shared row, which every wave would hit on one L2 channel
-    const uint32_t home = (h.v >= 0 ? (uint32_t)h.v : 0u) * ldT + rr;
-    const int32_t own0 = ld_off(a.lab, home);
-    const int32_t own = wk ? own0 : -1;
-    // entry j of the lane's row is live iff j < dsw: the selects below test that, not the
-    // loaded values, so a neighbour id is dead once its label load is issued (one register
-    // per entry)
-    const int dsw = wk ? h.ds : 0;
-    int32_t x[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j)                                 // idle / padding lanes read col[rb] (a hit)
-        x[j] = ld_off(WM == WM_W8 ? a.colw : a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
-    int32_t tot_own = 0;
-    if (LOUV) {
-        const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
-        tot_own = wk ? t0 : 0;
-    }
-    long long kown = 0;
-    if constexpr (UNITW) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)x[j] * ldT + rr : home);
-            x[j] = j < dsw ? lj : -1;
-        }
-        if (LOUV) {
-            int ko = 0;
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const bool mine = x[j] == own && x[j] >= 0;
-                ko += mine ? 1 : 0;
-                x[j] = mine ? -1 : x[j];
-            }
-            kown = ko;
-        }
-    } else if constexpr (WM == WM_W8) {
-        uint32_t wpk[(K + 3) / 4];                              // 4 weights per register
-#pragma unroll
-        for (int i = 0; i < (K + 3) / 4; ++i) wpk[i] = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) wpk[j >> 2] |= (uint32_t)(x[j] & wm) << (8 * (j & 3));
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)(x[j] >> wb) * ldT + rr : home);
-            x[j] = j < dsw ? lj : -1;
-        }
-        int ko = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int32_t wj = (int32_t)((wpk[j >> 2] >> (8 * (j & 3))) & 0xffu);
-            const bool mine = LOUV && x[j] == own && x[j] >= 0;
-            ko += mine ? wj : 0;
-            x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wj);
-        }
-        kown = ko;
-    } else {
-        int32_t wv[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int32_t wj = ld_off(a.cw, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
-            wv[j] = j < dsw ? wj : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)x[j] * ldT + rr : home);
-            x[j] = j < dsw ? lj : -1;
-        }
-        int ko = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const bool mine = LOUV && x[j] == own && x[j] >= 0;
-            ko += mine ? wv[j] : 0;
-            x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wv[j]);
-        }
-        kown = ko;
-    }
-    // Louvain, settled vertex: every foreign community weighs at most k_v - k_own, so no move can
-    // gain when (k_v - 2 k_own)*2M + k_v*(Sigma_own - k_v) <= 0.  When that holds on every lane
-    // (the vertex is settled in all the wave's replicas -- most of a consensus graph), the sort
-    // and the passes are skipped.
-    if (LOUV) {
-        const long long kvl = h.kvi;
-        const bool settled = !wk || (kvl - 2 * kown) * a.M2 + kvl * ((long long)tot_own - kvl) <= 0;
-        if (__ballot(!settled) == 0) return -1;                 // wave-uniform
-    }
     oem_sort<K>(x);
     // run ends and summed weights: e = bit q set when the run of equal labels ends at q
     // pass A: the largest weight vm
@@ -511,9 +435,10 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             acc = (q > 0 && l == (x[q - 1] >> wb)) ? acc + w : w;
             const bool end = x[q] >= 0 && (q == K - 1 || (x[q + 1] >> wb) != l);
             vm = end ? max(vm, acc) : vm;
-            if (!LOUV) kl = (end && l == own) ? acc : kl;
+            if (!LOUV && !FC_RL_LPA_OWN) kl = (end && l == own) ? acc : kl;
         }
-        if (!LOUV) kown = kl;
+        if (!LOUV && !FC_RL_LPA_OWN) kown = kl;
+        if (!LOUV && FC_RL_LPA_OWN) vm = max(vm, (int)kown);  // the own label's count is a run too
     }
     // Louvain: no candidate can gain when even weight vm at Sigma = 0 cannot, i.e. when
     // (vm - k_own)*2M + k_v*(Sigma_own - k_v) <= 0 (score_c <= vm*2M for every c): then no
@@ -534,7 +459,9 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             else cm_hi |= (uint32_t)cand << (q & 31);
         }
     }
-    const int ncand = __popc(cm_lo) + __popc(cm_hi);
+    // LPA, own entries out of the keys: the own label is a candidate when its count is the largest
+    const bool own_cand = !LOUV && FC_RL_LPA_OWN && wk && kown > 0 && kown == (long long)vm;
+    const int ncand = __popc(cm_lo) + __popc(cm_hi) + (own_cand ? 1 : 0);
     if (wk) c_cand += (uint32_t)ncand;
     const uint32_t tvh = hash32(stream_key(a.seed, (uint32_t)(a.rbase + h.rr), a.iter, (uint32_t)sweep, 2) ^ (uint32_t)h.v);
     int32_t dcs = -1;
@@ -595,12 +522,121 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             best_h = take ? hh : best_h;
             best_c = take ? x[q] : best_c;
         }
+        if (own_cand) {
+            const uint32_t hh = hash32(tvh ^ (uint32_t)own);
+            if (best_c < 0 || hh > best_h) { best_h = hh; best_c = own; }
+        }
         if (wk && ncand != 0) {
             c_unst += (kown != (long long)vm) ? 1 : 0;
             dcs = best_c != own ? best_c : -1;
         }
     }
     return dcs;
+}
+
+template <bool LOUV, int K, int WM>
+__device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
+                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
+    constexpr bool UNITW = WM == WM_UNIT;
+    slow_out = false;
+    const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
+    const int wb = UNITW ? 0 : a.wbits;
+    const int32_t wm = (1 << wb) - 1;
+    const bool wk = h.work;
+    // padding / idle lanes read a slot of their own vertex's row (cached, distinct per wave)
+    // instead of branching; never a shared row, which every wave would hit on one L2 channel
+    const uint32_t home = (h.v >= 0 ? (uint32_t)h.v : 0u) * ldT + rr;
+    const int32_t own0 = ld_off(a.lab, home);
+    const int32_t own = wk ? own0 : -1;
+    // entry j of the lane's row is live iff j < dsw: the selects below test that, not the
+    // loaded values, so a neighbour id is dead once its label load is issued (one register
+    // per entry)
+    const int dsw = wk ? h.ds : 0;
+    int32_t x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)                                 // idle / padding lanes read col[rb] (a hit)
+        x[j] = ld_off(WM == WM_W8 ? a.colw : a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
+    int32_t tot_own = 0;
+    if (LOUV) {
+        const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
+        tot_own = wk ? t0 : 0;
+    }
+    long long kown = 0;
+    if constexpr (UNITW) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)x[j] * ldT + rr : home);
+            x[j] = j < dsw ? lj : -1;
+        }
+        if (LOUV || FC_RL_LPA_OWN) {
+            int ko = 0;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const bool mine = x[j] == own && x[j] >= 0;
+                ko += mine ? 1 : 0;
+                x[j] = mine ? -1 : x[j];
+            }
+            kown = ko;
+        }
+    } else if constexpr (WM == WM_W8) {
+        uint32_t wpk[(K + 3) / 4];                              // 4 weights per register
+#pragma unroll
+        for (int i = 0; i < (K + 3) / 4; ++i) wpk[i] = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) wpk[j >> 2] |= (uint32_t)(x[j] & wm) << (8 * (j & 3));
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)(x[j] >> wb) * ldT + rr : home);
+            x[j] = j < dsw ? lj : -1;
+        }
+        int ko = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t wj = (int32_t)((wpk[j >> 2] >> (8 * (j & 3))) & 0xffu);
+            const bool mine = LOUV && x[j] == own && x[j] >= 0;
+            ko += mine ? wj : 0;
+            x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wj);
+        }
+        kown = ko;
+    } else {
+        int32_t wv[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t wj = ld_off(a.cw, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
+            wv[j] = j < dsw ? wj : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int32_t lj = ld_off(a.lab, j < dsw ? (uint32_t)x[j] * ldT + rr : home);
+            x[j] = j < dsw ? lj : -1;
+        }
+        int ko = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const bool mine = LOUV && x[j] == own && x[j] >= 0;
+            ko += mine ? wv[j] : 0;
+            x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wv[j]);
+        }
+        kown = ko;
+    }
+    // Louvain, settled vertex: every foreign community weighs at most k_v - k_own, so no move can
+    // gain when (k_v - 2 k_own)*2M + k_v*(Sigma_own - k_v) <= 0.  When that holds on every lane
+    // (the vertex is settled in all the wave's replicas -- most of a consensus graph), the sort
+    // and the passes are skipped.
+    if (LOUV) {
+        const long long kvl = h.kvi;
+        const bool settled = !wk || (kvl - 2 * kown) * a.M2 + kvl * ((long long)tot_own - kvl) <= 0;
+        if (__ballot(!settled) == 0) return -1;                 // wave-uniform
+    } else if (FC_RL_LPA_OWN) {
+        // LPA: the own label holds more than half the row -- the unique largest count, no move
+        // and a stable vertex -- on every lane: nothing to sort
+        const bool settled = !wk || 2 * kown > (long long)dsw;
+        if (__ballot(!settled) == 0) {
+            if (wk) c_cand += 1u;                               // the own label, the one candidate
+            return -1;
+        }
+    }
+    return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
 }
 
 // Light rows with sortable keys (label and weight fit 31 bits): no LDS, one sorting network

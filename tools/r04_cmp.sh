@@ -5,11 +5,10 @@ set -u
 OUT=gpurun_out/r04cmp
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_leiden.py \
-    -k "twin or full_run or heavy or weighted or dense or leiden" -m gpu > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+    -k "twin or full_run or heavy or weighted or dense" -m gpu > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 600 python3 tools/cd_ab.py --config lfr1m --reps 3 base "$@" base "$@" && \
 timeout -k 10 300 python3 tools/cd_ab.py --config lfr1m --algo 1 --reps 3 base "$@" && \
-timeout -k 10 300 python3 tools/cd_ab.py --config lfr1m --np 8 --reps 3 base "base@FC_AB_OPTS=rl_min_replicas=8" && \
-timeout -k 10 400 python3 tools/lv_ab.py --config lfr1m_leiden --reps 2 base lvns && \
+timeout -k 10 500 python3 tools/cd_ab.py --config sbm4m --algo 1 --reps 2 base "$@" && \
 FC_TRACE=1 timeout -k 10 300 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/trace.json 2> $OUT/trace.err
