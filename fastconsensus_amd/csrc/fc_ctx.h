@@ -194,6 +194,8 @@ struct Ctx {
     DevBuf lv[64];                  // Leiden level state (leiden.hip)
     int infomap_trials = 10;        // FC_OPT_INFOMAP_TRIALS (igraph community_infomap default)
     int lv_dense_div = getenv("FC_LV_DENSE_DIV") ? atoi(getenv("FC_LV_DENSE_DIV")) : 0;   // leiden.hip level buckets
+    // leiden.hip aggregate levels: buckets per move sweep (0: B, the level-0 count)
+    int lv_level_b = getenv("FC_LV_LEVEL_B") ? atoi(getenv("FC_LV_LEVEL_B")) : 4;
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     // CD kernel variant that leaves every decision unchanged (A/B switch, default on):
     // own-label entries summed in registers (ballots / wave scan) instead of the LDS table

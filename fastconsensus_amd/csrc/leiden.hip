@@ -1507,10 +1507,16 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         k_lv_fill_u8<<<nb(nU), LTB, 0, c.stream>>>(nU, act, done, cur.rep);
         set_graph();
         a.P = P; a.R = R; a.tot = ptot; a.rsize = rsize; a.act = act;
-        // dense aggregate levels: more buckets, so that fewer neighbours of a vertex decide in
-        // the same bucket (FC_LV_DENSE_DIV: buckets >= average degree / div, up to 1024; 0 = B)
+        // aggregate levels: lv_level_b buckets per move sweep (default 4, not level 0's 32).  The
+        // dense levels run tens of sweeps whose queues are a few re-queued vertices per replica;
+        // a bucket is a launch chain (decide, heavy tiers, apply) of ~100 us whatever it holds,
+        // and more simultaneous deciders did not cost sweeps or modularity (LFR-1M: 2.37 s with
+        // 32 buckets, 2.11 s with 16, 1.97 s with 8, 1.92 s with 4; modularity 0.46515 /
+        // 0.46517 / 0.46517 at 32 / 8 / 4, LFR-100k 0.46454 / 0.46457 / 0.46457;
+        // profiles/r04_leiden_buckets.txt).  FC_LV_DENSE_DIV (off): more buckets on dense levels,
+        // buckets >= average degree / div, up to 1024 -- measured slower (DESIGN).
         const int64_t avgdeg = cur.E / std::max<int64_t>(nU, 1);
-        int Bl = B;
+        int Bl = c.lv_level_b > 0 ? c.lv_level_b : B;
         if (c.lv_dense_div > 0)
             while (Bl < 1024 && (int64_t)Bl * c.lv_dense_div < avgdeg) Bl <<= 1;
         a.B = Bl;

@@ -3,7 +3,7 @@
 one graph, best-of-reps wall time and a hash of the labelings (variants claiming identical
 decisions must print the same hash).
 
-    python tools/lv_ab.py [--config lfr1m_leiden] [--reps 2] base name1 ...
+    python tools/lv_ab.py [--config lfr1m_leiden] [--reps 2] base name1[@ENV=VAL,...] ...
 """
 import hashlib
 import json
@@ -56,11 +56,17 @@ def main():
             config = val
         elif k == "--reps":
             reps = int(val)
-    for name in args or ["base"]:
+    for spec in args or ["base"]:
+        # name[@ENV=VAL,ENV=VAL]: a variant library and engine environment switches
+        name, _, envs = spec.partition("@")
+        env = dict(os.environ)
+        for kv in filter(None, envs.split(",")):
+            k, _, v = kv.partition("=")
+            env[k] = v
         lib = os.path.join(ROOT, "fastconsensus_amd", "lib",
                            "libfastconsensus_amd.so" if name == "base" else name + "/libfastconsensus_amd.so")
-        print("variant", name, flush=True)
-        rc = subprocess.call([sys.executable, __file__, "--child", lib, config, str(reps)])
+        print("variant", spec, flush=True)
+        rc = subprocess.call([sys.executable, __file__, "--child", lib, config, str(reps)], env=env)
         if rc != 0:
             print("variant %s failed rc=%d" % (name, rc), flush=True)
             sys.exit(rc)
