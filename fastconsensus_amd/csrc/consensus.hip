@@ -205,9 +205,9 @@ void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* parti
 }
 
 // ------------------------------------------------------------------ closure
-__device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int32_t* col, int32_t a,
-                                                int32_t b) {
-    int64_t lo = rowptr[a], hi = rowptr[a + 1];
+// b in the ascending row col[lo, end)
+__device__ __forceinline__ bool has_edge_row(const int32_t* col, int64_t lo, int64_t end, int32_t b) {
+    int64_t hi = end;
     if (hi - lo <= 16) {   // short row: 16 independent loads (one round trip), not a dependent search
         bool f = false;
 #pragma unroll
@@ -221,7 +221,11 @@ __device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int
         if (x < b) lo = mid + 1;
         else hi = mid;
     }
-    return lo < rowptr[a + 1] && col[lo] == b;
+    return lo < end && col[lo] == b;
+}
+__device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int32_t* col, int32_t a,
+                                                int32_t b) {
+    return has_edge_row(col, rowptr[a], rowptr[a + 1], b);
 }
 
 // Attempt t (fast_consensus.py:175-184): node uniform over all N (np.random.choice over
@@ -237,14 +241,42 @@ __device__ __forceinline__ bool has_edge_sorted(const int64_t* rowptr, const int
 // whose CAS creates a slot lists it.  The table holds one block's pairs only (2x slots), so
 // it stays in the Infinity Cache; earlier blocks' candidates are C edges (has_edge in C).
 constexpr uint64_t CLO_EMPTY = ~0ull;
+// A table slot: the pair key and the first attempt that drew it in one 16-byte record, so the
+// attempt's atomicMin lands on the line its CAS just brought in (two arrays cost a second
+// random line per candidate).  Cleared to all ones (key EMPTY, attempt UINT_MAX).
+struct __align__(16) CloSlot {
+    unsigned long long key;
+    unsigned int att;
+    unsigned int pad;
+};
 __device__ __forceinline__ uint64_t clo_slot(uint64_t key, uint64_t mask) { return mix64(key) & mask; }
+// insert key with attempt a; returns the slot if this call created it, else -1
+__device__ __forceinline__ int64_t clo_insert(CloSlot* tab, uint64_t hmask, uint64_t key, uint32_t a) {
+    uint64_t h = clo_slot(key, hmask);
+    while (true) {
+        unsigned long long k = tab[h].key;
+        if (k == CLO_EMPTY) {
+            k = atomicCAS(&tab[h].key, (unsigned long long)CLO_EMPTY, (unsigned long long)key);
+            if (k == CLO_EMPTY) {                 // created: a candidate of this block
+                atomicMin(&tab[h].att, a);
+                return (int64_t)h;
+            }
+        }
+        if (k == key) { atomicMin(&tab[h].att, a); return -1; }   // drawn again in this block
+        h = (h + 1) & hmask;
+    }
+}
+// PK: the node's kept row and C row from one 16-byte record (rec[x] = {kept start, kept length,
+// C start, C length}; 32-bit offsets, used while both graphs hold < 2^31 entries): one line per
+// node lookup instead of krowptr's and crowptr's two.
+template <bool PK>
 __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt, int64_t n, uint32_t k0, uint32_t k1,
                                                         uint32_t iter, const int64_t* __restrict__ krowptr,
                                                         const int32_t* __restrict__ kcol,
                                                         const int64_t* __restrict__ crowptr,
-                                                        const int32_t* __restrict__ ccol, int bits,
-                                                        uint64_t* hkey, uint32_t* hval, uint64_t hmask,
-                                                        int64_t* slot) {
+                                                        const int32_t* __restrict__ ccol,
+                                                        const int4* __restrict__ rec, int bits,
+                                                        CloSlot* tab, uint64_t hmask, int64_t* slot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cnt) return;
     slot[i] = -1;
@@ -252,10 +284,16 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
     U4 ctr = {(uint32_t)t, (uint32_t)(t >> 32), iter, 0x5eedu};
     const U4 r = philox(ctr, k0, k1);
     const int32_t x = (int32_t)below(r.x, (uint32_t)n);
-    const int64_t kb = krowptr[x];
-    const int64_t dk = krowptr[x + 1] - kb;
-    const int64_t cb = crowptr ? crowptr[x] : 0;
-    const int64_t d = dk + (crowptr ? crowptr[x + 1] - cb : 0);
+    int64_t kb, dk, cb = 0, dc = 0;
+    if (PK) {
+        const int4 rx = rec[x];
+        kb = (uint32_t)rx.x; dk = rx.y; cb = (uint32_t)rx.z; dc = rx.w;
+    } else {
+        kb = krowptr[x];
+        dk = krowptr[x + 1] - kb;
+        if (crowptr) { cb = crowptr[x]; dc = crowptr[x + 1] - cb; }
+    }
+    const int64_t d = dk + dc;
     if (d < 2) return;
     const uint32_t i1 = below(r.y, (uint32_t)d);
     uint32_t i2 = below(r.z, (uint32_t)(d - 1));
@@ -263,23 +301,23 @@ __global__ __launch_bounds__(256) void k_closure_sample(int64_t t0, int64_t cnt,
     const int32_t a = (int64_t)i1 < dk ? kcol[kb + i1] : ccol[cb + i1 - dk];
     const int32_t b = (int64_t)i2 < dk ? kcol[kb + i2] : ccol[cb + i2 - dk];
     const int32_t u = a < b ? a : b, v = a < b ? b : a;
-    if (has_edge_sorted(krowptr, kcol, u, v)) return;
-    if (crowptr && has_edge_sorted(crowptr, ccol, u, v)) return;   // an earlier block's candidate
-    const uint64_t key = ((uint64_t)u << bits) | (uint64_t)v;
-    uint64_t h = clo_slot(key, hmask);
-    while (true) {
-        uint64_t k = hkey[h];
-        if (k == CLO_EMPTY) {
-            k = atomicCAS((unsigned long long*)&hkey[h], (unsigned long long)CLO_EMPTY, (unsigned long long)key);
-            if (k == CLO_EMPTY) {                 // created: a candidate of this block
-                atomicMin(&hval[h], (uint32_t)i);
-                slot[i] = (int64_t)h;            // dense: no shared counter (one hot address serialised the block)
-                return;
-            }
-        }
-        if (k == key) { atomicMin(&hval[h], (uint32_t)i); return; }   // drawn again in this block
-        h = (h + 1) & hmask;
+    if (PK) {
+        const int4 ru = rec[u];
+        if (has_edge_row(kcol, (uint32_t)ru.x, (int64_t)(uint32_t)ru.x + ru.y, v)) return;
+        if (ru.w > 0 && has_edge_row(ccol, (uint32_t)ru.z, (int64_t)(uint32_t)ru.z + ru.w, v)) return;   // an earlier block's candidate
+    } else {
+        if (has_edge_sorted(krowptr, kcol, u, v)) return;
+        if (crowptr && has_edge_sorted(crowptr, ccol, u, v)) return;   // an earlier block's candidate
     }
+    const uint64_t key = ((uint64_t)u << bits) | (uint64_t)v;
+    slot[i] = clo_insert(tab, hmask, key, (uint32_t)i);   // dense: no shared counter (one hot address serialised the block)
+}
+// rec[x] = {kept row start, kept length, 0, 0}: the closure's first block (empty C graph)
+__global__ void k_clo_rec_init(int64_t n, const int64_t* krowptr, int4* rec) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n) return;
+    const int64_t kb = krowptr[x];
+    rec[x] = make_int4((int32_t)kb, (int32_t)(krowptr[x + 1] - kb), 0, 0);
 }
 // This block's candidates (the attempts that created a slot, in attempt order) appended to
 // the accumulated list at the device-side count *nacc (no host round trip per block).
@@ -291,14 +329,14 @@ __global__ void k_slot_flags(int64_t n, const int64_t* slot, int64_t* flag, int6
     flag[i] = (i < n && slot[i] >= 0) ? 1 : 0;
     if (i == n) nacc[1] = nacc[0];
 }
-__global__ void k_append_cand(int64_t n, const int64_t* slot, const int64_t* pos, const uint64_t* hkey,
-                              const uint32_t* hval, int64_t t0, int64_t* nacc, uint64_t* akey, int64_t* aval) {
+__global__ void k_append_cand(int64_t n, const int64_t* slot, const int64_t* pos, const CloSlot* tab, int64_t t0,
+                              int64_t* nacc, uint64_t* akey, int64_t* aval) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t base = nacc[1];                  // the block's first entry (k_slot_flags); not written here
     if (i < n && slot[i] >= 0) {
-        const int64_t h = slot[i];
-        akey[base + pos[i]] = hkey[h];
-        aval[base + pos[i]] = t0 + (int64_t)hval[h];
+        const CloSlot e = tab[slot[i]];
+        akey[base + pos[i]] = e.key;
+        aval[base + pos[i]] = t0 + (int64_t)e.att;
     }
     if (i == n) nacc[0] = base + pos[n];           // nobody in this launch reads [0]
 }
@@ -322,13 +360,17 @@ __global__ void k_cgraph_nfill(const int64_t* nacc, const uint64_t* akey, int bi
     ncol[nrow[v] + atomicAdd(&cur[v], 1)] = u;
 }
 __global__ void k_cgraph_merge(int64_t n, const int64_t* crow, const int32_t* col, const int32_t* nrow,
-                               int32_t* ncol, int64_t* crow2, int32_t* col2) {
+                               int32_t* ncol, int64_t* crow2, int32_t* col2, int4* rec) {
     const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x > n) return;
     const int64_t o = crow[x] + nrow[x];
     crow2[x] = o;
     if (x == n) return;
     const int32_t nb = nrow[x], ne = nrow[x + 1];
+    if (rec) {   // the node's C row in its closure record (k_closure_sample<true>)
+        int2* rc = (int2*)(rec + x) + 1;
+        *rc = make_int2((int32_t)o, (int32_t)(crow[x + 1] - crow[x] + (ne - nb)));
+    }
     for (int32_t i = nb + 1; i < ne; ++i) {      // the node's new entries (a few): insertion sort
         const int32_t y = ncol[i];
         int32_t j = i - 1;
@@ -403,8 +445,8 @@ struct Clo {
     int R;
     int64_t rcap;
     uint64_t hsize;
-    uint64_t* hkey;
-    uint32_t* hval;
+    CloSlot* tab;
+    int4* rec;                     // packed node records, or null (graphs past 2^31 entries)
     int64_t *slot, *fl, *ps, *aval, *nacc;
     uint64_t* akey;
     int32_t *nrow, *ncur, *ncol;
@@ -418,8 +460,9 @@ static Clo clo_bufs(Ctx& c, int64_t attempts) {
     const int64_t N = c.N;
     b.hsize = 1024;
     while (b.hsize < 2 * (uint64_t)b.rcap) b.hsize <<= 1;          // one block's pairs, load <= 1/2
-    b.hkey = ensure<uint64_t>(c.clo_hkey, b.hsize);
-    b.hval = ensure<uint32_t>(c.clo_hval, b.hsize);
+    b.tab = ensure<CloSlot>(c.clo_hkey, b.hsize);
+    // the kept graph holds 2 * kept_m entries (consensus_apply), the C graph at most 2 * attempts
+    b.rec = (2 * c.kept_m < ((int64_t)1 << 31) && 2 * cap < ((int64_t)1 << 31)) ? ensure<int4>(c.clo_rec, N) : nullptr;
     b.slot = ensure<int64_t>(c.clo_list, b.rcap);
     b.fl = ensure<int64_t>(c.nodetmp, std::max<int64_t>(b.rcap + 1, N + 1));
     b.ps = ensure<int64_t>(c.nodetmp2, std::max<int64_t>(b.rcap + 1, N + 1));
@@ -438,19 +481,26 @@ static Clo clo_bufs(Ctx& c, int64_t attempts) {
 static void clo_reset(Ctx& c, const Clo& b) {
     FC_HIP(hipMemsetAsync(b.nacc, 0, 2 * sizeof(int64_t), c.stream));
     FC_HIP(hipMemsetAsync(c.clo_rowptr.p, 0, sizeof(int64_t) * (c.N + 1), c.stream));   // empty C graph
+    if (b.rec) k_clo_rec_init<<<nblk(c.N), TB, 0, c.stream>>>(c.N, c.krowptr.as<int64_t>(), b.rec);
 }
 static void clo_clear_table(Ctx& c, const Clo& b) {
-    FC_HIP(hipMemsetAsync(b.hkey, 0xff, sizeof(uint64_t) * b.hsize, c.stream));
-    FC_HIP(hipMemsetAsync(b.hval, 0xff, sizeof(uint32_t) * b.hsize, c.stream));
+    FC_HIP(hipMemsetAsync(b.tab, 0xff, sizeof(CloSlot) * b.hsize, c.stream));
 }
 // attempts [t0, t0 + n) of block r drawn into the (cleared) table; slot[i] >= 0 lists a new pair
 static void clo_draw(Ctx& c, const Clo& b, int64_t t0, int64_t n, int iteration, int r) {
     const uint64_t s = mix64(c.seed ^ 0xC105u);
-    k_closure_sample<<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32), (uint32_t)iteration,
-                                                  c.krowptr.as<int64_t>(), c.kcol.as<int32_t>(),
-                                                  r > 0 ? c.clo_rowptr.as<int64_t>() : nullptr,
-                                                  r > 0 ? c.clo_col.as<int32_t>() : nullptr, c.key_bits, b.hkey, b.hval,
-                                                  b.hsize - 1, b.slot);
+    const int64_t* crow = r > 0 ? c.clo_rowptr.as<int64_t>() : nullptr;
+    const int32_t* ccol = r > 0 ? c.clo_col.as<int32_t>() : nullptr;
+    if (b.rec)
+        k_closure_sample<true><<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32),
+                                                             (uint32_t)iteration, c.krowptr.as<int64_t>(),
+                                                             c.kcol.as<int32_t>(), crow, ccol, b.rec, c.key_bits, b.tab,
+                                                             b.hsize - 1, b.slot);
+    else
+        k_closure_sample<false><<<nblk(n), TB, 0, c.stream>>>(t0, n, c.N, (uint32_t)s, (uint32_t)(s >> 32),
+                                                              (uint32_t)iteration, c.krowptr.as<int64_t>(),
+                                                              c.kcol.as<int32_t>(), crow, ccol, nullptr, c.key_bits,
+                                                              b.tab, b.hsize - 1, b.slot);
 }
 // the listed slots of the table (slot[0..n)) appended to the accumulated candidates; unless r is
 // the last block, the C graph grows by them (rows ascending) for the next block
@@ -459,7 +509,7 @@ static void clo_append(Ctx& c, const Clo& b, int64_t n, int64_t t0, int r) {
     const int64_t N = c.N;
     k_slot_flags<<<nblk(n + 1), TB, 0, c.stream>>>(n, b.slot, b.fl, b.nacc);
     exclusive_scan(c, b.fl, b.ps, n + 1);
-    k_append_cand<<<nblk(n + 1), TB, 0, c.stream>>>(n, b.slot, b.ps, b.hkey, b.hval, t0, b.nacc, b.akey, b.aval);
+    k_append_cand<<<nblk(n + 1), TB, 0, c.stream>>>(n, b.slot, b.ps, b.tab, t0, b.nacc, b.akey, b.aval);
     if (r + 1 == b.R) return;
     FC_HIP(hipMemsetAsync(b.nrow, 0, sizeof(int32_t) * 2 * (N + 1), c.stream));
     k_cgraph_ndeg<<<nblk(n), TB, 0, c.stream>>>(b.nacc, b.akey, bits, b.ncur);
@@ -467,7 +517,7 @@ static void clo_append(Ctx& c, const Clo& b, int64_t n, int64_t t0, int r) {
     FC_HIP(hipMemsetAsync(b.ncur, 0, sizeof(int32_t) * (N + 1), c.stream));
     k_cgraph_nfill<<<nblk(n), TB, 0, c.stream>>>(b.nacc, b.akey, bits, b.nrow, b.ncur, b.ncol);
     k_cgraph_merge<<<nblk(N + 1), TB, 0, c.stream>>>(N, c.clo_rowptr.as<int64_t>(), c.clo_col.as<int32_t>(), b.nrow,
-                                                     b.ncol, c.clo_rowptr2.as<int64_t>(), c.clo_col2.as<int32_t>());
+                                                     b.ncol, c.clo_rowptr2.as<int64_t>(), c.clo_col2.as<int32_t>(), b.rec);
     std::swap(c.clo_rowptr, c.clo_rowptr2);
     std::swap(c.clo_col, c.clo_col2);
 }
@@ -496,35 +546,20 @@ void closure_sample(Ctx& c, int64_t attempts, int iteration) {
 // (key, attempt); the ranks' lists, all-gathered, are re-inserted into the table keeping the
 // smallest attempt per key (atomicMin, as a single rank drawing the whole block does), and
 // appended and grown exactly as closure_sample does: every rank ends with the same candidates.
-__global__ void k_emit_cand(int64_t n, const int64_t* slot, const int64_t* pos, const uint64_t* hkey,
-                            const uint32_t* hval, int64_t t0, int64_t* out) {
+__global__ void k_emit_cand(int64_t n, const int64_t* slot, const int64_t* pos, const CloSlot* tab, int64_t t0,
+                            int64_t* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || slot[i] < 0) return;
-    const int64_t h = slot[i], p = pos[i];
-    out[2 * p] = (int64_t)hkey[h];
-    out[2 * p + 1] = t0 + (int64_t)hval[h];
+    const CloSlot e = tab[slot[i]];
+    const int64_t p = pos[i];
+    out[2 * p] = (int64_t)e.key;
+    out[2 * p + 1] = t0 + (int64_t)e.att;
 }
-__global__ void k_closure_insert(int64_t cnt, const int64_t* __restrict__ in, int64_t t0, uint64_t* hkey,
-                                 uint32_t* hval, uint64_t hmask, int64_t* slot) {
+__global__ void k_closure_insert(int64_t cnt, const int64_t* __restrict__ in, int64_t t0, CloSlot* tab, uint64_t hmask,
+                                 int64_t* slot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cnt) return;
-    slot[i] = -1;
-    const uint64_t key = (uint64_t)in[2 * i];
-    const uint32_t a = (uint32_t)(in[2 * i + 1] - t0);
-    uint64_t h = clo_slot(key, hmask);
-    while (true) {
-        uint64_t k = hkey[h];
-        if (k == CLO_EMPTY) {
-            k = atomicCAS((unsigned long long*)&hkey[h], (unsigned long long)CLO_EMPTY, (unsigned long long)key);
-            if (k == CLO_EMPTY) {
-                atomicMin(&hval[h], a);
-                slot[i] = (int64_t)h;
-                return;
-            }
-        }
-        if (k == key) { atomicMin(&hval[h], a); return; }
-        h = (h + 1) & hmask;
-    }
+    slot[i] = clo_insert(tab, hmask, (uint64_t)in[2 * i], (uint32_t)(in[2 * i + 1] - t0));
 }
 
 int closure_begin(Ctx& c, int64_t attempts, int iteration) {
@@ -553,7 +588,7 @@ int64_t closure_block_sample(Ctx& c, int r, int64_t t_lo, int64_t t_hi, int64_t*
         FC_REQUIRE(count <= capacity, FC_EINVAL,
                    "closure block output holds " + std::to_string(capacity) + " pairs; " + std::to_string(count) +
                        " drawn");
-        if (count > 0) k_emit_cand<<<nblk(n), TB, 0, c.stream>>>(n, b.slot, b.ps, b.hkey, b.hval, t_lo, out);
+        if (count > 0) k_emit_cand<<<nblk(n), TB, 0, c.stream>>>(n, b.slot, b.ps, b.tab, t_lo, out);
     }
     timer_end(c, 2, sl);
     return count;
@@ -565,7 +600,7 @@ void closure_block_add(Ctx& c, int r, const int64_t* in, int64_t count) {
     const int64_t t0 = c.clo_attempts * r / b.R;
     if (count > 0) {
         clo_clear_table(c, b);
-        k_closure_insert<<<nblk(count), TB, 0, c.stream>>>(count, in, t0, b.hkey, b.hval, b.hsize - 1, b.slot);
+        k_closure_insert<<<nblk(count), TB, 0, c.stream>>>(count, in, t0, b.tab, b.hsize - 1, b.slot);
         clo_append(c, b, count, t0, r);
     }
     c.clo_next = r + 1;
