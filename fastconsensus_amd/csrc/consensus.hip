@@ -462,7 +462,8 @@ static Clo clo_bufs(Ctx& c, int64_t attempts) {
     while (b.hsize < 2 * (uint64_t)b.rcap) b.hsize <<= 1;          // one block's pairs, load <= 1/2
     b.tab = ensure<CloSlot>(c.clo_hkey, b.hsize);
     // the kept graph holds 2 * kept_m entries (consensus_apply), the C graph at most 2 * attempts
-    b.rec = (2 * c.kept_m < ((int64_t)1 << 31) && 2 * cap < ((int64_t)1 << 31)) ? ensure<int4>(c.clo_rec, N) : nullptr;
+    b.rec = (c.clo_pack && 2 * c.kept_m < ((int64_t)1 << 31) && 2 * cap < ((int64_t)1 << 31))
+                ? ensure<int4>(c.clo_rec, N) : nullptr;
     b.slot = ensure<int64_t>(c.clo_list, b.rcap);
     b.fl = ensure<int64_t>(c.nodetmp, std::max<int64_t>(b.rcap + 1, N + 1));
     b.ps = ensure<int64_t>(c.nodetmp2, std::max<int64_t>(b.rcap + 1, N + 1));

@@ -164,6 +164,9 @@ struct Ctx {
     // first attempt), the C graph of the earlier blocks' closure edges (CSR rowptr int64
     // [N+1] / col int32, ping-pong), a block's new entries (int32 row offsets + cursors, cols)
     DevBuf clo_rec;                 // closure: per node {kept row start, length, C row start, length}
+    // closure sampler reads the packed node records (0: krowptr / crowptr, the path of graphs past
+    // 2^31 entries; FC_CLO_PACK=0 lets the tests run it at small sizes)
+    int clo_pack = getenv("FC_CLO_PACK") ? atoi(getenv("FC_CLO_PACK")) : 1;
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
     int closure_rounds = 8;         // FC_OPT_CLOSURE_ROUNDS

@@ -328,11 +328,15 @@ def test_c5_lpm_count_update_and_closure_growth_full_size(fcmod):
 
 
 # ------------------------------------------------------------------------------ closure
+@pytest.mark.parametrize("pack", [1, 0])
 @pytest.mark.parametrize("name", ["lfr1k_louvain_np20", "lfr1k_lpm_np20", "karate_louvain_np50"])
-def test_device_closure_sampler_is_the_measured_one(fcmod, name):
+def test_device_closure_sampler_is_the_measured_one(fcmod, name, pack, monkeypatch):
     """fc_closure_sample on the reference's kept graph draws exactly the candidates of the
     restated sampler (orc_closure_sample) -- the one whose deviation from the reference's
-    sequential sampler tests/test_closure_deviation.py measures."""
+    sequential sampler tests/test_closure_deviation.py measures.  pack = 0: the sampler's
+    krowptr / crowptr path (graphs past 2^31 entries), forced at this size (FC_CLO_PACK, read
+    when the engine context is created)."""
+    monkeypatch.setenv("FC_CLO_PACK", str(pack))
     case = golden_io.load(name)
     graphs, traces, _ = orc.replay(case.algo, case.N, case.edges_file, case.n_p, case.tau, case.delta,
                                    case.cd_batches, case.pair_batches)
