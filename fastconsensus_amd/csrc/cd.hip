@@ -100,7 +100,9 @@ struct CDArgs {
     // serialise every block's atomic (~12 ns each, MI355X_MICROARCH.md "fanin").
     unsigned long long* red;
     // pruning (list mode): per sweep >= 1 only vertices whose neighbour moved are visited
-    uint8_t* aff;                // [n_r][N] affected flags (set by moves, read+cleared by list build)
+    uint32_t* aff;               // [n_r][aw] affected bits, bit v & 31 of word v >> 5 (set by moves,
+                                 // read + cleared by the list build): N/8 bytes per replica
+    int64_t aw;                  // words per replica
     int own_bal;                 // 1: own-label entries of weight w0 summed by wave ballots, not inserted in the LDS table
     int w0;                      // that weight: 1 on unit-weight graphs, n_p on consensus graphs (their typical weight)
     int wbits;                   // bits of the largest edge weight (LPA: 1)
@@ -798,6 +800,11 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     }
 }
 
+// Affected bits: one atomic OR per flag (a moved vertex's neighbour); 8x less memory than a
+// byte per vertex, so a replica's flags (N/8 bytes) stay cache-resident between the movers
+// that set them and the next sweep's list build
+__device__ __forceinline__ void aff_set(uint32_t* affr, int32_t v) { atomicOr(affr + (v >> 5), 1u << (v & 31)); }
+__device__ __forceinline__ bool aff_get(const uint32_t* affr, int64_t v) { return (affr[v >> 5] >> (v & 31)) & 1u; }
 // Apply a bucket's decisions (fixed grid: blockIdx.y = replica, blocks stride over the
 // replica's list).  Label + community totals only (the replica neither pushes nor tracks
 // this sweep): one thread per decision slot.  Otherwise one 16-lane tile per slot: lane 0
@@ -844,7 +851,7 @@ __global__ __launch_bounds__(ATB) void k_apply(CDArgs a, int bucket) {
     } else {
         const int tile = threadIdx.x / TILE, lane = threadIdx.x % TILE;
         int32_t* nlr = a.nlab + (int64_t)r * a.m2;
-        uint8_t* aff = a.aff + (int64_t)r * a.N;
+        uint32_t* aff = a.aff + (int64_t)r * a.aw;
         for (int64_t di = (int64_t)blockIdx.x * TILES + tile; di < len; di += (int64_t)gridDim.x * TILES) {
             const int4 dv = decr[di];
             const int32_t d = dv.x, v = dv.y;
@@ -855,12 +862,12 @@ __global__ __launch_bounds__(ATB) void k_apply(CDArgs a, int bucket) {
             if (push && trk) {
                 for (int64_t j = rb + lane; j < re; j += TILE) {
                     nlr[a.rev[j]] = d;     // neighbours now see v's new community
-                    aff[a.col[j]] = 1;     // ... and are revisited next sweep (pruning)
+                    aff_set(aff, a.col[j]);   // ... and are revisited next sweep (pruning)
                 }
             } else if (push) {
                 for (int64_t j = rb + lane; j < re; j += TILE) nlr[a.rev[j]] = d;
             } else {
-                for (int64_t j = rb + lane; j < re; j += TILE) aff[a.col[j]] = 1;
+                for (int64_t j = rb + lane; j < re; j += TILE) aff_set(aff, a.col[j]);
             }
         }
     }
@@ -890,7 +897,7 @@ __global__ __launch_bounds__(256) void k_mark_lm(CDArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t v0 = v - lane;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
-    uint8_t* aff = a.aff + (int64_t)r * a.N;
+    uint32_t* aff = a.aff + (int64_t)r * a.aw;
     while (m) {
         const int b = __ffsll((long long)m) - 1;
         m &= m - 1;
@@ -898,7 +905,7 @@ __global__ __launch_bounds__(256) void k_mark_lm(CDArgs a) {
         const int32_t d = labr[vr.w];
         const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
         for (int64_t j = rb + lane; j < re; j += 64)
-            if (labr[a.colp[j]] != d) aff[a.col[j]] = 1;
+            if (labr[a.colp[j]] != d) aff_set(aff, a.col[j]);
     }
 }
 
@@ -995,11 +1002,9 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
     int32_t* wl2 = wl + a.N;
     int32_t* bl = wl2 + a.N;
     int32_t* mark = tmark + (int64_t)r * a.N;
-    uint8_t* aff = a.aff + (int64_t)r * a.N;
     int4* decr = a.dec + (int64_t)r * a.dstride;
     int32_t* hv = a.heavy + (int64_t)r * a.hcap;
     int32_t* scratch = a.heavy_scratch ? a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots : nullptr;
-    (void)aff;
     const int32_t* lo0 = a.loff + (int64_t)r * (B + 1);
     if (threadIdx.x == 0) s_n = lo0[B];       // the first sweep's list (k_list_fill), when filtered
     __syncthreads();
@@ -1179,11 +1184,11 @@ __device__ __forceinline__ uint32_t vertex_bucket(const CDArgs& a, const Perm& P
 __global__ __launch_bounds__(256) void k_aff_count(CDArgs a, int32_t* vcnt) {
     const int r = blockIdx.y;
     if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
-    const uint8_t* aff = a.aff + (int64_t)r * a.N;
+    const uint32_t* aff = a.aff + (int64_t)r * a.aw;
     int c = 0;
     for (int64_t v = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x; v < a.N && v < (int64_t)(blockIdx.x + 1) * TB * LB_PER;
          v += TB)
-        c += aff[v] != 0;
+        c += aff_get(aff, v) ? 1 : 0;
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(vcnt + r, c);
 }
@@ -1194,12 +1199,12 @@ __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t
     for (int k = threadIdx.x; k < B; k += TB) s_lb[k] = 0;
     __syncthreads();
     const Perm P = sweep_perm(a, order_rg(a, r, rep_dense(a, r)), sweep);
-    const uint8_t* aff = a.aff + (int64_t)r * a.N;
+    const uint32_t* aff = a.aff + (int64_t)r * a.aw;
     const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
 #pragma unroll
     for (int i = 0; i < LB_PER; ++i) {
         const int64_t v = v0 + (int64_t)i * TB;
-        if (v < a.N && aff[v]) atomicAdd(&s_lb[vertex_bucket(a, P, (uint32_t)v)], 1);
+        if (v < a.N && aff_get(aff, v)) atomicAdd(&s_lb[vertex_bucket(a, P, (uint32_t)v)], 1);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < B; k += TB)
@@ -1275,17 +1280,22 @@ __global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const in
     __syncthreads();
     const int g = gco[r];
     const Perm P = sweep_perm(a, order_rg(a, r, rep_dense(a, r)), sweep);
-    uint8_t* aff = a.aff + (int64_t)r * a.N;
+    uint32_t* aff = a.aff + (int64_t)r * a.aw;
     int bk[LB_PER], loc[LB_PER];
-    const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;   // a multiple of 32 at lanes 0, 32
 #pragma unroll
     for (int i = 0; i < LB_PER; ++i) {
         const int64_t v = v0 + (int64_t)i * TB;
         bk[i] = -1;
-        if (v >= a.N || !aff[v]) continue;   // filter: vertices whose neighbour moved last sweep
-        aff[v] = 0;
+        if (v >= a.N || !aff_get(aff, v)) continue;   // filter: vertices whose neighbour moved last sweep
         bk[i] = (int)vertex_bucket(a, P, (uint32_t)v) / g;
         loc[i] = atomicAdd(&s_cnt[bk[i]], 1);
+    }
+    // clear the words read: a word's 32 vertices are 32 lanes of one wave, which read it above
+#pragma unroll
+    for (int i = 0; i < LB_PER; ++i) {
+        const int64_t v = v0 + (int64_t)i * TB;
+        if (v < a.N && (v & 31) == 0) aff[v >> 5] = 0u;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < B; k += TB)
@@ -1368,10 +1378,11 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     int64_t n_heavy = 0;
     if (g.max_deg > LIGHT_MAX_DEG) n_heavy = count_heavy(c, LIGHT_MAX_DEG);
     int32_t* heavy = ensure<int32_t>(c.heavy_list, 3 * (size_t)rcount * (size_t)std::max<int64_t>(n_heavy, 1) + 3);
-    uint8_t* aff = ensure<uint8_t>(c.aff, (size_t)rcount * N);
+    const int64_t aw = (N + 31) / 32;
+    uint32_t* aff = ensure<uint32_t>(c.aff, (size_t)rcount * aw);
     int32_t* track = ensure<int32_t>(c.track, 4 * (size_t)rcount);
     if (!h) {
-        FC_HIP(hipMemsetAsync(aff, 0, (size_t)rcount * N, c.stream));
+        FC_HIP(hipMemsetAsync(aff, 0, 4 * (size_t)rcount * aw, c.stream));
         FC_HIP(hipMemsetAsync(track, 0, 16 * (size_t)rcount, c.stream));   // pull mode, no tracking
     }
     int32_t* list = ensure<int32_t>(c.vlist, (size_t)rcount * PN);
@@ -1431,7 +1442,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     a.vcnt = vcnt;
     a.dense_div = c.dense_div;
     a.heavy = heavy; a.heavy_cnt = heavy_cnt; a.heavy_scratch = hscr; a.heavy_slots = heavy_slots;
-    a.aff = aff; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
+    a.aff = aff; a.aw = aw; a.list = list; a.loff = loff; a.lcnt = lcnt; a.rrec = rrec; a.track = track; a.prune = c.prune;
     a.hcap = std::max<int64_t>(n_heavy, 1);
     a.track_div = c.track_div;
     // push mode only on unit-weight graphs: on consensus graphs the pull sweeps measured

@@ -1266,21 +1266,39 @@ __global__ __launch_bounds__(256) void k_rl_colw(int64_t n, const int32_t* col, 
 }
 
 // Hybrid hand-off: the affected bits [banks][N] as cd.hip's per-replica flags u8 [n_r][N].
-__global__ __launch_bounds__(256) void k_rl_aff_export(int64_t N, const uint64_t* aff, uint8_t* out) {
-    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int r = blockIdx.y;
-    if (v < N) out[(int64_t)r * N + v] = (uint8_t)((aff[(int64_t)(r >> 6) * N + v] >> (r & 63)) & 1ull);
+// the bank's 64-bit replica masks per vertex -> cd.hip's per-replica bit words (word v >> 5 of
+// replica r, aw words per replica): a wave takes 64 vertices of one bank and turns them, one
+// ballot per replica, into that replica's two words
+__global__ __launch_bounds__(256) void k_rl_aff_export(int64_t N, int n_r, const uint64_t* aff, int64_t aw, uint32_t* out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t v0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+    const int bank = blockIdx.y;
+    if (v0 >= N) return;                                        // wave-uniform
+    const int64_t v = v0 + lane;
+    const uint64_t m = v < N ? aff[(int64_t)bank * N + v] : 0ull;
+    uint64_t mine = 0;
+#pragma unroll 8
+    for (int q = 0; q < 64; ++q) {
+        const uint64_t b = __ballot((m >> q) & 1ull);
+        mine = lane == q ? b : mine;
+    }
+    const int r = bank * 64 + lane;
+    if (r < n_r) {
+        uint32_t* o = out + (int64_t)r * aw + (v0 >> 5);
+        o[0] = (uint32_t)mine;
+        if ((v0 >> 5) + 1 < aw) o[1] = (uint32_t)(mine >> 32);
+    }
 }
 
 // CDHandoff::fill: the batch's state in cd.hip's layout (labels in slot order, int32 totals by
 // community, affected flags, tracked / filtered flags with pull mode, active flags)
-void rl_handoff_fill(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint8_t* aff, int32_t* track,
+void rl_handoff_fill(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint32_t* aff, int32_t* track,
                      int32_t* active) {
     const RL& a = *(const RL*)user;
     const dim3 tg(nb(a.N, 64), (a.n_r + 63) / 64);
     k_rl_export<<<tg, 256, 0, c.stream>>>(a.N, a.n_r, a.ldT, a.lab, c.sinv.as<int32_t>(), lab);
     if (tot) k_rl_export<<<tg, 256, 0, c.stream>>>(a.N, a.n_r, a.ldT, a.tot, nullptr, tot);
-    k_rl_aff_export<<<dim3(nb(a.N, 256), a.n_r), 256, 0, c.stream>>>(a.N, a.aff, aff);
+    k_rl_aff_export<<<dim3(nb(a.N, 256), a.banks), 256, 0, c.stream>>>(a.N, a.n_r, a.aff, (a.N + 31) / 32, aff);
     FC_HIP(hipMemcpyAsync(track, a.track, 8 * (size_t)a.n_r, hipMemcpyDeviceToDevice, c.stream));
     FC_HIP(hipMemsetAsync(track + 2 * a.n_r, 0, 8 * (size_t)a.n_r, c.stream));
     FC_HIP(hipMemcpyAsync(active, a.active, 4 * (size_t)a.n_r, hipMemcpyDeviceToDevice, c.stream));

@@ -223,7 +223,7 @@ struct Ctx;
 // sweep0.
 struct CDHandoff {
     int sweep0;
-    void (*fill)(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint8_t* aff, int32_t* track, int32_t* active);
+    void (*fill)(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint32_t* aff, int32_t* track, int32_t* active);
     const void* user;
 };
 

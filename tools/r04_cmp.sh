@@ -6,7 +6,7 @@ OUT=gpurun_out/r04cmp
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
-    -k "twin or full_run or heavy or weighted or dense" -m gpu > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+    -k "twin or full_run or heavy or weighted or dense or hybrid or handoff or prune" -m gpu > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 600 python3 tools/cd_ab.py --config lfr1m --reps 3 base "$@" base "$@" && \
 timeout -k 10 300 python3 tools/cd_ab.py --config lfr1m --algo 1 --reps 3 base "$@" && \
