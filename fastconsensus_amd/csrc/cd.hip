@@ -1356,7 +1356,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // vertices in a random chunk order (coalesced per-vertex accesses)
     const int CH = c.chunk;
     const int64_t NC = CH ? (N + 2 * CH - 2) / CH : N;   // room for the chunk-grid shift (sweep_perm)
-    const int B = (int)std::min<int64_t>(c.buckets, NC);
+    const int B = (int)std::min<int64_t>(cd_buckets(c, algo), NC);
     const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
     int32_t* lab = ensure<int32_t>(c.lab, (size_t)rcount * N);
     // tot in int32 whenever every community total fits (all <= 2M < 2^31): half the gathers

@@ -1352,7 +1352,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     rl_layout(rcount, &LG, &VPW, &banks, &ldT);
     const int CH = c.chunk;
     const int64_t NC = CH ? (N + 2 * CH - 2) / CH : N;   // room for the chunk-grid shift (as cd.hip)
-    const int B = (int)std::min<int64_t>(c.buckets, NC);
+    const int B = (int)std::min<int64_t>(cd_buckets(c, algo), NC);
     const int64_t S = CH ? ((NC + B - 1) / B) * CH : (N + B - 1) / B;
     const int64_t PN = CH ? NC * CH : N;
 

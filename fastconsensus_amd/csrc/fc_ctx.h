@@ -179,7 +179,7 @@ struct Ctx {
     DevBuf nodetmp, nodetmp2, nodetmp3;  // int64 [N+1] scratch
     DevBuf part, ccount;            // consensus partial / closure counts (single-GPU driver)
     // params
-    int buckets = 32, max_sweeps = 200, max_iters = 1000;
+    int buckets = 0, max_sweeps = 200, max_iters = 1000;   // buckets 0: cd_buckets' default per algorithm
     int chunk = 16;                 // CD order granularity (0 = per vertex), FC_OPT_CHUNK
     int relabel = 1;                // FC_OPT_RELABEL (applies at the next fc_load_graph)
     int64_t apply_blocks = getenv("FC_APPLY_BLOCKS") ? atoll(getenv("FC_APPLY_BLOCKS")) : 32;   // per replica
@@ -226,6 +226,17 @@ struct CDHandoff {
     void (*fill)(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint32_t* aff, int32_t* track, int32_t* active);
     const void* user;
 };
+
+// CD buckets per sweep: FC_OPT_BUCKETS when set, else 16 for Louvain (louvain, louvain_nc and
+// Leiden's level-0 move phase) and 32 for LPA.  16 buckets (twice the simultaneous deciders)
+// cut LFR-1M louvain from 149 to 121 ms with the CPU model's consensus NMI within the reference
+// loop's spread (0.912 vs 0.917, reference 0.905 +- 0.035); LPA keeps 32: at its detectability
+// edge its bucketed batches must stay within 0.25 of sequential LPA's structured fraction
+// (tests/test_gpu_cd_parity.py), and 16 buckets measured 0.28 off (profiles/r04_buckets_ab.txt)
+constexpr int CD_BUCKETS_LOUVAIN = 16, CD_BUCKETS_LPA = 32;
+inline int cd_buckets(const Ctx& c, int algo) {
+    return c.buckets > 0 ? c.buckets : (is_louvain(algo) ? CD_BUCKETS_LOUVAIN : CD_BUCKETS_LPA);
+}
 
 // graph.cpp
 void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v);

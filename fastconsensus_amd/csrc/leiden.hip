@@ -1137,7 +1137,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
 
     const int n_r = rcount * tu;   // union replicas
     const int64_t nU0 = (int64_t)n_r * N;
-    const int B = std::max(1, c.buckets);
+    const int B = std::max(1, c.buckets > 0 ? c.buckets : CD_BUCKETS_LPA);   // refine / Infomap sweeps (level 0 Louvain: cd_buckets)
     auto I32 = [&](int k, int64_t n) { return ensure<int32_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };
     auto I64 = [&](int k, int64_t n) { return ensure<int64_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };
     auto U8 = [&](int k, int64_t n) { return ensure<uint8_t>(c.lv[k], (size_t)std::max<int64_t>(n, 1)); };

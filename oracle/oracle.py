@@ -282,9 +282,17 @@ def infomap_full(g, seed, trials=10):
 
 
 DENSE_DIV = 0   # the engine's default (fc_ctx.h dense_div, FC_OPT_DENSE_DIV)
+# the engine's default buckets per sweep (fc_ctx.h cd_buckets): Louvain 16, LPA 32
+BUCKETS_LOUVAIN, BUCKETS_LPA = 16, 32
 
 
-def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, chunk=16, prune=1, coarsen=8,
+def cd_buckets(algo, buckets=None):
+    if buckets:
+        return int(buckets)
+    return BUCKETS_LOUVAIN if algo in (LOUVAIN, LOUVAIN_NC) else BUCKETS_LPA
+
+
+def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=None, max_sweeps=200, chunk=16, prune=1, coarsen=8,
               prune_mark=1, shared=2, dense_div=DENSE_DIV):
     """CPU twin of the engine's bucketed CD (bit-exact target for the HIP kernels).  Defaults = the
     default engine (fc_ctx.h): the hybrid, FC_OPT_CD_ENGINE=2, shared=2 (a replica's full sweeps
@@ -294,6 +302,7 @@ def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=32, max_sweeps=200, 
     rowptr, col, cw = g.csr()
     lab = np.empty((n_r, g.N), np.int32)
     sw = np.empty(n_r, np.int32)
+    buckets = cd_buckets(algo, buckets)
     lib().orc_engine_cd(_cd_algo(algo), g.N, rowptr, col, cw, n_r, rbase, iteration, int(seed) & (2**64 - 1), buckets,
                         max_sweeps, chunk, prune, coarsen, prune_mark, shared, dense_div, lab, sw)
     return lab, sw

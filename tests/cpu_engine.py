@@ -12,7 +12,7 @@ from oracle import oracle as orc
 
 
 class OracleEngine:
-    def __init__(self, seed, buckets=32, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1, shared=2,
+    def __init__(self, seed, buckets=None, chunk=16, prune=1, sigma=None, coarsen=8, prune_mark=1, shared=2,
                  dense_div=orc.DENSE_DIV):
         """sigma: node id -> internal id (the engine's fc_get_node_map); None = identity.  Defaults:
         the default (hybrid) CD engine, FC_OPT_CD_ENGINE=2; shared=0 models the classic engine,

@@ -65,7 +65,15 @@ def test_cpu_twin_defaults_match_engine_defaults():
     from oracle import oracle as orc
     from tests.cpu_engine import OracleEngine
     src = open(os.path.join(ROOT, "fastconsensus_amd", "csrc", "fc_ctx.h")).read()
-    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("buckets", "max_sweeps", "chunk", "prune", "coarsen", "prune_mark", "dense_div")}
+    eng = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in ("max_sweeps", "chunk", "prune", "coarsen", "prune_mark", "dense_div")}
+    # buckets: 0 in the context = cd_buckets' per-algorithm default (Louvain 16, LPA 32), which the
+    # twin restates (orc.cd_buckets; engine_cd / OracleEngine default None)
+    assert int(re.search(r"\bbuckets = (\d+)", src).group(1)) == 0
+    bl, bp = (int(x) for x in re.search(r"CD_BUCKETS_LOUVAIN = (\d+), CD_BUCKETS_LPA = (\d+)", src).groups())
+    assert (orc.BUCKETS_LOUVAIN, orc.BUCKETS_LPA) == (bl, bp)
+    assert orc.cd_buckets(orc.LOUVAIN) == bl and orc.cd_buckets(orc.LOUVAIN_NC) == bl and orc.cd_buckets(orc.LPM) == bp
+    assert inspect.signature(orc.engine_cd).parameters["buckets"].default is None
+    assert inspect.signature(OracleEngine.__init__).parameters["buckets"].default is None
     # the default CD engine is the hybrid (FC_OPT_CD_ENGINE=2): the twin's shared=2
     assert int(re.search(r"\bcd_engine = (\d+)", src).group(1)) == 2
     eng["shared"] = 2
