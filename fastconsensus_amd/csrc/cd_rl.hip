@@ -746,6 +746,24 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
     }
 }
 
+// Resident waves of a decide instantiation on this device (occupancy x CUs), once per
+// instantiation: the grid is sized to them (c.rl_grid_mul x) instead of up to 8192 blocks, so a
+// launch's blocks split its items evenly in one generation -- 8192 blocks ran ~2.7 generations of
+// 4-5 items, the last one on two thirds of the SIMDs.
+template <bool LOUV, int K, int WM>
+static int64_t rl_decide_slots() {
+    static int64_t slots = 0;
+    if (!slots) {
+        int nb = 0, dev = 0;
+        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM>, RTB, 0));
+        FC_HIP(hipGetDevice(&dev));
+        int cus = 0;
+        FC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        slots = (int64_t)std::max(1, nb) * std::max(1, cus);
+    }
+    return slots;
+}
+
 // Fallback for keys that do not pack into 31 bits (huge graphs or weights): the row's labels
 // staged in LDS as L[j][lane], equal labels merged per lane by a triangular scan.
 struct RLShared {
@@ -1500,8 +1518,16 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     const int seg = k * NCLS + cls;
                     const int64_t n = hb[seg + 1] - hb[seg];
                     if (n <= 0) continue;
-                    const unsigned grid = grid_of(n);
-#define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep); timer_end(c, 7, ev); } while (0)
+                    const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
+#define RL_LAUNCH(L, KK, U)                                                                                        \
+    do {                                                                                                           \
+        const unsigned grid = c.rl_grid_mul > 0                                                                    \
+            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U>() * c.rl_grid_mul)) \
+            : grid_of(n);                                                                                          \
+        const int ev = timer_begin(c);                                                                             \
+        k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                          \
+        timer_end(c, 7, ev);                                                                                       \
+    } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
