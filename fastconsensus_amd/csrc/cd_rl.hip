@@ -747,9 +747,11 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
 }
 
 // Resident waves of a decide instantiation on this device (occupancy x CUs), once per
-// instantiation: the grid is sized to them (c.rl_grid_mul x) instead of up to 8192 blocks, so a
-// launch's blocks split its items evenly in one generation -- 8192 blocks ran ~2.7 generations of
-// 4-5 items, the last one on two thirds of the SIMDs.
+// instantiation: Louvain's grid is sized to them (c.rl_grid_mul x) instead of up to 8192 blocks,
+// so a launch's blocks split its items evenly in one generation -- 8192 blocks ran ~2.7
+// generations of 4-5 items, the last one on two thirds of the SIMDs.  LPA keeps the 8192 cap:
+// its items' cost varies more (most waves settled, a few sorting) and the extra blocks balance
+// it (SBM-4M 687 vs 695 ms).
 template <bool LOUV, int K, int WM>
 static int64_t rl_decide_slots() {
     static int64_t slots = 0;
@@ -1521,7 +1523,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
 #define RL_LAUNCH(L, KK, U)                                                                                        \
     do {                                                                                                           \
-        const unsigned grid = c.rl_grid_mul > 0                                                                    \
+        const unsigned grid = (c.rl_grid_mul > 0 && L)                                                             \
             ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U>() * c.rl_grid_mul)) \
             : grid_of(n);                                                                                          \
         const int ev = timer_begin(c);                                                                             \

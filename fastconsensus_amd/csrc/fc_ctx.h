@@ -200,7 +200,7 @@ struct Ctx {
     int lv_dense_div = getenv("FC_LV_DENSE_DIV") ? atoi(getenv("FC_LV_DENSE_DIV")) : 0;   // leiden.hip level buckets
     // leiden.hip aggregate levels: buckets per move sweep (0: B, the level-0 count)
     int lv_level_b = getenv("FC_LV_LEVEL_B") ? atoi(getenv("FC_LV_LEVEL_B")) : 4;
-    // cd_rl.hip decide grid: resident waves x rl_grid_mul (0: up to 8192 blocks, round 3)
+    // cd_rl.hip Louvain decide grid: resident waves x rl_grid_mul (0: up to 8192 blocks, as LPA)
     int rl_grid_mul = getenv("FC_RL_GRID_MUL") ? atoi(getenv("FC_RL_GRID_MUL")) : 1;
     int prune = 1;                  // FC_OPT_PRUNE: visit only vertices whose neighbour moved (once moves < N/4)
     // CD kernel variant that leaves every decision unchanged (A/B switch, default on):
