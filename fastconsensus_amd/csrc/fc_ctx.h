@@ -129,10 +129,13 @@ struct Ctx {
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
     int cd_engine = 2;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip), 1 replica-lane (cd_rl.hip), 2 hybrid (default)
-    // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many replicas
-    int64_t rl_min_replicas = getenv("FC_RL_MIN_REPLICAS") ? atoll(getenv("FC_RL_MIN_REPLICAS")) : 16;
+    // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many
+    // replicas (8 lanes per vertex at 8: LFR-1M n_p = 8 run 40.3 vs 42.9 ms on cd.hip since the
+    // 16-bucket / resident-grid changes; 51.3 vs 46.2 before them)
+    int64_t rl_min_replicas = getenv("FC_RL_MIN_REPLICAS") ? atoll(getenv("FC_RL_MIN_REPLICAS")) : 8;
     // ... and the graph this many vertices (a bucket of a smaller graph is too few waves for the
-    // replica-lane kernels: LFR-100k louvain 45.9 vs 31.2 ms, LFR-1M 175.8 vs 211 ms)
+    // replica-lane kernels: LFR-100k louvain 45.9 vs 31.2 ms, LFR-1M 175.8 vs 211 ms; at the
+    // round-4 end LFR-100k louvain 33.0 vs 26.5, lpm 24.2 vs 16.6 ms)
     int64_t rl_min_vertices = getenv("FC_RL_MIN_VERTICES") ? atoll(getenv("FC_RL_MIN_VERTICES")) : 262144;
     // hybrid semantics: a filtered sweep visiting >= N/dense_div vertices keeps the shared order
     // (without coarse rounds); 0 = never (FC_OPT_DENSE_DIV).  Measured no gain: LFR-1M 175.9 /

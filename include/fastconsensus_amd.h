@@ -159,7 +159,7 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 All three are bit-exact against oracle/fc_oracle.c orc_engine_cd
                                 (shared = 0 / 1 / 2).                                            */
 #define FC_OPT_RL_MIN_REPLICAS 15 /* hybrid: the smallest batch whose full sweeps run on the
-                                replica-lane engine (default 16).  Speed only: same results.     */
+                                replica-lane engine (default 8).  Speed only: same results.      */
 #define FC_OPT_RL_MIN_VERTICES 16 /* hybrid: ... and the smallest graph (default 262144 vertices;
                                 below it cd.hip runs the full sweeps too).  Speed only.          */
 #define FC_OPT_DENSE_DIV 17  /* hybrid semantics: a filtered sweep that still visits >= n/dense_div
