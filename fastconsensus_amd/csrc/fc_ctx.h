@@ -172,7 +172,7 @@ struct Ctx {
     int clo_pack = getenv("FC_CLO_PACK") ? atoi(getenv("FC_CLO_PACK")) : 1;
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
-    int closure_rounds = 8;         // FC_OPT_CLOSURE_ROUNDS
+    int closure_rounds = 4;         // FC_OPT_CLOSURE_ROUNDS (round 3: 8; DESIGN, closure)
     // sharded closure (fc_closure_begin / _block_sample / _block_add / _finish): the run's
     // attempts and block count, the next block to add (blocks go in order), -1 = not begun
     int64_t clo_attempts = 0;

@@ -190,7 +190,7 @@ def closure_from_pairs(algo, g, pairs, labels, n_p):
     return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), of[:k].copy()
 
 
-CLOSURE_ROUNDS = 8   # the engine's default (fc_ctx.h closure_rounds, FC_OPT_CLOSURE_ROUNDS)
+CLOSURE_ROUNDS = 4   # the engine's default (fc_ctx.h closure_rounds, FC_OPT_CLOSURE_ROUNDS)
 
 
 def closure_sample_pairs(kept, attempts, seed, iteration, rounds=CLOSURE_ROUNDS):
