@@ -71,7 +71,7 @@ def test_closure_small_graph_printed():
 
 
 def test_blocked_vs_sequential_closure_at_c3():
-    """BASELINE configs[2] scale (LFR n=100k mu=0.5): the engine's blocked sampler (8 blocks,
+    """BASELINE configs[2] scale (LFR n=100k mu=0.5): the engine's blocked sampler (orc.CLOSURE_ROUNDS blocks,
     orc_closure_sample = the device's, bit for bit) against the reference's SEQUENTIAL sampler
     over the growing graph (orc_closure_sequential: fast_consensus.py:175-184, its distribution
     with the oracle's RNG) on the same post-threshold graph of a 16-replica louvain consensus
