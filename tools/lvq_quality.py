@@ -23,4 +23,4 @@ for n, reps in ((100_000, 8), (1_000_000, 4)):
         lab = eng.get_labels(reps)
     q = np.mean([orc.modularity(g, x) for x in lab])
     k = np.mean([len(np.unique(x)) for x in lab])
-    print("n=%d env LEVEL_B=%s QUEUE_DIV=%s: Q %.5f k %.1f" % (n, os.environ.get("FC_LV_LEVEL_B"), os.environ.get("FC_LV_QUEUE_DIV"), q, k), flush=True)
+    print("n=%d env LEVEL_B=%s REFINE_B=%s: Q %.5f k %.1f" % (n, os.environ.get("FC_LV_LEVEL_B"), os.environ.get("FC_LV_REFINE_B"), q, k), flush=True)
