@@ -191,7 +191,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
     FC_CTX(ctx)
     FC_API_BEGIN
     switch (option) {
-        case FC_OPT_BUCKETS: FC_REQUIRE(value >= 1, FC_EINVAL, "buckets >= 1"); c.buckets = (int)value; break;
+        case FC_OPT_BUCKETS: FC_REQUIRE(value >= 0, FC_EINVAL, "buckets >= 0 (0: per-algorithm default)"); c.buckets = (int)value; break;
         case FC_OPT_MAX_SWEEPS: FC_REQUIRE(value >= 1, FC_EINVAL, "max_sweeps >= 1"); c.max_sweeps = (int)value; break;
         case FC_OPT_MAX_ITERS: FC_REQUIRE(value >= 1, FC_EINVAL, "max_iters >= 1"); c.max_iters = (int)value; break;
         case FC_OPT_CHUNK:

@@ -44,6 +44,8 @@ constexpr int RTB = 64;                 // decide / apply / mark blocks: one wav
 constexpr int DM = 64;                  // light rows: degree <= DM
 constexpr int VPWMAX = 8;               // sub-groups per wave (lane groups of >= 8 replicas)
 constexpr int RL_CHUNK = 16;            // = cd.hip CHUNK (chunked visit orders)
+// slow-visit and visit-mode list entries pack the local replica in 14 bits ((e << 14) | rr)
+constexpr int RL_MAX_REPLICAS = 16384;
 constexpr int32_t DONE = -1;            // merged / own / empty table entry (labels are >= 0)
 constexpr int NSH = 16;                 // counter shards per replica
 constexpr int RF = 8;                   // fields: 0 dq, 1 unstable, 2 moves, 3 visits, 4 entries, 5 cands, 6 units
@@ -1088,8 +1090,8 @@ __global__ __launch_bounds__(HTB) void k_rl_exact(RL a, int k, int sweep) {
                 }
             }
             a.dec[e * a.ldT + rr] = dcs;
-            if (ncand) atomicAdd(rl_red(a, rr, 5), (unsigned long long)ncand);
-            if (heavy) {
+            if (heavy) {                                      // slow visits: k_rl_decide counted them
+                if (ncand) atomicAdd(rl_red(a, rr, 5), (unsigned long long)ncand);
                 atomicAdd(rl_red(a, rr, 3), 1ull);
                 atomicAdd(rl_red(a, rr, 4), (unsigned long long)d);
             }
@@ -1285,7 +1287,8 @@ __global__ __launch_bounds__(256) void k_rl_colw(int64_t n, const int32_t* col, 
     if (j < n) out[j] = (col[j] << wb) | cw[j];
 }
 
-// Hybrid hand-off: the affected bits [banks][N] as cd.hip's per-replica flags u8 [n_r][N].
+// Hybrid hand-off: the affected bits [banks][N] as cd.hip's per-replica bit words [n_r][aw]
+// (aw = (N+31)/32; vertex v is bit v & 31 of word v >> 5):
 // the bank's 64-bit replica masks per vertex -> cd.hip's per-replica bit words (word v >> 5 of
 // replica r, aw words per replica): a wave takes 64 vertices of one bank and turns them, one
 // ballot per replica, into that replica's two words
@@ -1354,7 +1357,8 @@ bool cd_rl_supported(const Ctx& c, int algo) { return c.cd_engine == 1 && cd_rl_
 // throughout, with the same semantics (its full sweeps use the shared order too), so results
 // never depend on how replicas are sharded over GPUs.
 void cd_run_hybrid(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration) {
-    if (cd_rl_fits(c, algo) && (int64_t)rcount >= c.rl_min_replicas && c.N >= c.rl_min_vertices)
+    if (cd_rl_fits(c, algo) && (int64_t)rcount >= c.rl_min_replicas && rcount <= RL_MAX_REPLICAS &&
+        c.N >= c.rl_min_vertices)
         cd_run_rl(c, algo, rbegin, rcount, n_p_total, iteration, true);
     else
         cd_run(c, algo, rbegin, rcount, n_p_total, iteration, 1);
@@ -1362,6 +1366,7 @@ void cd_run_hybrid(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int 
 
 void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iteration, bool hybrid) {
     FC_REQUIRE(rcount >= 1 && rbegin >= 0 && rbegin + rcount <= n_p_total, FC_EINVAL, "bad replica range");
+    FC_REQUIRE(rcount <= RL_MAX_REPLICAS, FC_ELIMIT, "replica-lane engine: more than 16384 replicas per GPU");
     FC_REQUIRE(c.N > 0 && c.g.rowptr.p, FC_ESTATE, "no graph loaded");
     const int sl0 = timer_begin(c);
     const bool louv = is_louvain(algo);

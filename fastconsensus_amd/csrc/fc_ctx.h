@@ -223,7 +223,8 @@ struct Ctx {
 struct Ctx;
 // State the replica-lane engine hands to cd_run at the first filtered sweep of a hybrid batch
 // (FC_OPT_CD_ENGINE=2, cd_rl.hip): fill() writes it in cd.hip's layout on c.stream -- labels
-// [n_r][N] in slot order, int32 totals [n_r][N], affected flags u8 [n_r][N], track int32
+// [n_r][N] in slot order, int32 totals [n_r][N], affected flags as bit words uint32
+// [n_r][aw] (aw = (N+31)/32 words per replica; vertex v is bit v & 31 of word v >> 5), track int32
 // [4][n_r] (tracked, filtered, push, transition) and active [n_r] -- and the sweeps go on from
 // sweep0.
 struct CDHandoff {

@@ -1516,7 +1516,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         // profiles/r04_leiden_buckets.txt).  FC_LV_DENSE_DIV (off): more buckets on dense levels,
         // buckets >= average degree / div, up to 1024 -- measured slower (DESIGN).
         const int64_t avgdeg = cur.E / std::max<int64_t>(nU, 1);
-        int Bl = c.lv_level_b > 0 ? c.lv_level_b : B;
+        int Bl = (c.buckets == 0 && c.lv_level_b > 0) ? c.lv_level_b : B;   // FC_OPT_BUCKETS wins
         if (c.lv_dense_div > 0)
             while (Bl < 1024 && (int64_t)Bl * c.lv_dense_div < avgdeg) Bl <<= 1;
         a.B = Bl;

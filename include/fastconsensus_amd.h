@@ -109,7 +109,10 @@ int fc_set_timing(fc_ctx* ctx, int enable);
 int fc_collect_timing(fc_ctx* ctx, fc_stats* stats);
 /* Tunables (0 = default): buckets per sweep, max sweeps per CD run, max iterations. */
 int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
-#define FC_OPT_BUCKETS 1     /* rounds per CD sweep (default 16)                            */
+#define FC_OPT_BUCKETS 1     /* rounds per CD sweep; 0 (default) = per algorithm: 16 for louvain,
+                                louvain_nc and Leiden's level-0 move; 32 for lpm (LPA), Infomap
+                                and Leiden's refinement; 4 for Leiden's aggregate-level moves.
+                                A value >= 1 applies to all of them.                          */
 #define FC_OPT_MAX_SWEEPS 2  /* cap on sweeps per CD run (default 200)                      */
 #define FC_OPT_MAX_ITERS 3   /* cap on consensus iterations (default 1000)                  */
 #define FC_OPT_CHUNK 4       /* CD visit order granularity: 0 per vertex, 16 (default) chunks */

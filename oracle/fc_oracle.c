@@ -928,7 +928,18 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
             for (i64 v = 0; v < N; ++v) V += aff[v] != 0;
             dense = (i64)dense_div * V >= N;
         }
-        const uint32_t prg = (shared == 1 || (shared == 2 && (!filtered || dense))) ? TW_SHARED_RG : rg;
+        /* experimental (semantics study): shared == 3 -- sweep 0 in the replica's own order, then
+         * as 2; shared >= 0x100 -- as 2 with replicas grouped by (shared & 0xff): the group's
+         * shared order (key TW_SHARED_RG - group) */
+        uint32_t prg;
+        if (shared >= 0x100) {
+            const uint32_t gs = (uint32_t)(shared & 0xff);
+            prg = (!filtered || dense) ? TW_SHARED_RG - rg / gs : rg;
+        } else if (shared == 3) {
+            prg = (sweep > 0 && (!filtered || dense)) ? TW_SHARED_RG : rg;
+        } else {
+            prg = (shared == 1 || (shared == 2 && (!filtered || dense))) ? TW_SHARED_RG : rg;
+        }
         const tw_perm P = tw_make_perm((uint32_t)NC, tw_stream_key(seed, prg, iter, (uint32_t)sweep, 1));
         const uint32_t tbk = tw_stream_key(seed, rg, iter, (uint32_t)sweep, 2);
         const uint32_t off = tw_chunk_off(chunk, seed, prg, iter, (uint32_t)sweep);
@@ -1032,6 +1043,14 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
     }
     free(tot); free(csz); free(acc); free(seen); free(keys); free(dec); free(aff); free(mvf); free(lists); free(loff);
     return sweep;
+}
+
+/* The engine's internal vertex numbering (graph.hip k_sigma, FC_OPT_RELABEL=1): node i ->
+ * perm_apply(make_perm(n, (uint32_t)mix64(seed ^ 0x51A7E5ED)), i).  With it the CPU model
+ * (tests/cpu_engine.py, sigma=...) reproduces a device run of the same seed exactly. */
+void orc_device_sigma(i64 n, u64 seed, i32* sigma) {
+    const tw_perm P = tw_make_perm((uint32_t)n, (uint32_t)tw_mix64(seed ^ 0x51A7E5EDull));
+    for (i64 i = 0; i < n; ++i) sigma[i] = (i32)tw_perm_apply(&P, (uint32_t)i);
 }
 
 /* Replicas [rbase, rbase+n_r) of the engine's bucketed CD on a symmetric CSR.

@@ -76,6 +76,7 @@ def lib():
         L.orc_engine_cd.argtypes = [ctypes.c_int, i64, _i64p, _i32p, _i32p, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
+        L.orc_device_sigma.argtypes = [i64, u64, _i32p]
         L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
         L.orc_infomap_full.argtypes = [i64, _i64p, _i32p, u64, ctypes.c_int, _i32p, ctypes.POINTER(dbl)]
@@ -290,6 +291,13 @@ def cd_buckets(algo, buckets=None):
     if buckets:
         return int(buckets)
     return BUCKETS_LOUVAIN if algo in (LOUVAIN, LOUVAIN_NC) else BUCKETS_LPA
+
+
+def device_sigma(n, seed):
+    """The engine's internal vertex numbering for a seed (graph.hip k_sigma, relabel on)."""
+    out = np.empty(max(int(n), 1), np.int32)
+    lib().orc_device_sigma(int(n), int(seed) & (2**64 - 1), out)
+    return out[:n]
 
 
 def engine_cd(algo, g, n_r, rbase, iteration, seed, buckets=None, max_sweeps=200, chunk=16, prune=1, coarsen=8,

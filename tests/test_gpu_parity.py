@@ -176,6 +176,18 @@ def _twin(eng, algo, N, e, count, r0, iteration, seed, **kw):
     return lab[:, sigma], sw
 
 
+@pytest.mark.parametrize("n,seed", [(1000, 100), (1000, 259), (34, 7), (1_000_003, 42)])
+def test_node_map_is_the_oracle_device_sigma(fcmod, n, seed):
+    """fc_get_node_map equals orc.device_sigma (graph.hip k_sigma restated), so the CPU model
+    predicts a device run of any seed exactly (tools/semantics_dist.py SEM_DEVSIGMA)."""
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, n, 4 * n).astype(np.int32)
+    v = rng.integers(0, n, 4 * n).astype(np.int32)
+    with fcmod.Engine(seed=seed) as eng:
+        eng.load_graph(n, u, v)
+        np.testing.assert_array_equal(eng.node_map(), orc.device_sigma(n, seed))
+
+
 def _lfr1k_graph():
     case = golden_io.load("lfr1k_louvain_np20")
     return case, orc.EdgeGraph.from_lines(case.N, case.edges_file)
