@@ -232,6 +232,11 @@ __device__ __forceinline__ uint32_t tie_hash(uint32_t tbk, int32_t v, int32_t c)
     return hash32(hash32(tbk ^ (uint32_t)v) ^ (uint32_t)c);
 }
 
+// Affected bits: one atomic OR per flag (a moved vertex's neighbour); 8x less memory than a
+// byte per vertex, so a replica's flags (N/8 bytes) stay cache-resident between the movers
+// that set them and the next sweep's list build
+__device__ __forceinline__ void aff_set(uint32_t* affr, int32_t v) { atomicOr(affr + (v >> 5), 1u << (v & 31)); }
+__device__ __forceinline__ bool aff_get(const uint32_t* affr, int64_t v) { return (affr[v >> 5] >> (v & 31)) & 1u; }
 // Final decision shared by the light and heavy kernels (runs on one lane).
 // Returns the target community or -1; writes predicted dQ (fixed point) / unstable flag.
 template <bool LOUV, typename TT>
@@ -266,6 +271,7 @@ struct Visit {
     int64_t d;                 // degree
     int32_t own, kvw;          // own label and k_v (int32 when 2M < 2^31) for the decision record
     bool work, heavy;
+    bool tied;                 // LPA: >= 2 dominant labels (the vertex redraws at every visit)
 };
 #ifdef FC_PHASE_PROF
 // Diagnostic build only: cycles per phase of decide_wave, sampled on 1/64 of the blocks.
@@ -294,6 +300,7 @@ struct WaveShared {
     int32_t vm[WNT], own[WNT], kown[WNT];
     uint32_t tvh[WNT];
     int32_t hope[WNT];           // Louvain: some candidate may gain (else no Sigma is gathered)
+    int32_t ntie[WNT];           // LPA: labels at the largest count
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -357,6 +364,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         for (int s = lane; s < WNT * HCAP / 4; s += 64) { k4[s] = make_int4(-1, -1, -1, -1); v4[s] = make_int4(0, 0, 0, 0); }
         if (lane < WNT) {
             ws.best2[lane] = LLONG_MIN; ws.tmin[lane] = LLONG_MAX; ws.tb[lane] = ~0ull; ws.k2[lane] = 0; ws.vm[lane] = INT_MIN; ws.kown[lane] = 0;
+            ws.ntie[lane] = 0;
             ws.own[lane] = work ? own : -1;
             ws.kv[lane] = kv;
             ws.tvh[lane] = hash32(stream_key(a.seed, rg, a.iter, sweep, 2) ^ (uint32_t)v);
@@ -482,6 +490,22 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
         if (ko > ws.k2[lane]) ws.k2[lane] = ko;   // every other lane's max landed before the barrier
     }
     if (!LOUV && lane < WNT && ws.k2[lane]) ws.vm[lane] = (int32_t)(ws.k2[lane] >> 32);   // read by this lane only
+    bool tied = false;
+    if (!LOUV) {
+        // ties at the top count: the table's labels at vm, plus the own label (counted by the
+        // ballots, never in the table) when its count is vm too
+        wave_sync();
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            if (it >= nl) break;
+            if (rec[it] < 0) continue;
+            const int t = rec[it] >> 8, sl = t * HCAP + (rec[it] & 255);
+            if (ws.val[sl] == ws.vm[t]) atomicAdd(&ws.ntie[t], 1);
+        }
+        wave_sync();
+        if (lane < WNT && ws.vm[lane] != INT_MIN)
+            tied = ws.ntie[lane] + ((a.own_bal && kacc > 0 && kacc == ws.vm[lane]) ? 1 : 0) >= 2;
+    }
     if (LOUV) {
         // no candidate can gain when even weight vm at Sigma = 0 cannot: (vm - k_own)*2M +
         // k_v*(Sigma_own - k_v) <= 0 (score_c <= vm*2M for every c) -- then the vertex stays and
@@ -603,6 +627,7 @@ __device__ __forceinline__ Visit decide_wave(const CDArgs& a, int r, int rg, int
     // ---- the decision, lanes 0..7
     Visit out;
     out.dcs = -1; out.dq = 0; out.unst = 0; out.ncand = ncand; out.d = d; out.work = work; out.heavy = heavy;
+    out.tied = tied && work;
     out.own = own; out.kvw = (int32_t)kv;
     if (work && ws.vm[lane] != INT_MIN && (!LOUV || ws.hope[lane])) {   // a candidate that may gain (Louvain)
         const long long best_s = best_of(lane);
@@ -661,6 +686,8 @@ __global__ __launch_bounds__(DTB) __attribute__((amdgpu_waves_per_eu(8))) void k
     const Visit vis = decide_wave<LOUV, TT>(a, r, rg, sweep, valid, v, (rr.z & RR_PUSH) != 0, (rr.z & RR_TRANS) != 0,
                                             s_ws[wv]);
     if (in_range) {
+        // LPA, tracked sweep: a vertex with several dominant labels is revisited next sweep
+        if (!LOUV && vis.tied && a.track[r]) aff_set(a.aff + (int64_t)r * a.aw, v);
         a.dec[(int64_t)r * a.dstride + di] = make_int4(v >= 0 ? vis.dcs : -1, v, vis.own, vis.kvw);   // heavy: .x later
         if (vis.heavy) {
             const int hq = atomicAdd(a.heavy_cnt, 1);
@@ -710,7 +737,7 @@ struct HeavyShared {
 };
 template <bool LOUV, typename TT, int NTH>
 __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, HeavyShared<NTH>& sh, int32_t* scratch,
-                               unsigned long long* dq_out, int* unst_out) {
+                               unsigned long long* dq_out, int* unst_out, bool* tied_out = nullptr) {
     const int rg = a.rbase + r;
     const uint32_t tbk = stream_key(a.seed, rg, a.iter, sweep, 2);
     const int64_t rb = a.rowptr[v], d = a.rowptr[v + 1] - rb;
@@ -773,6 +800,23 @@ __device__ int32_t heavy_visit(const CDArgs& a, int r, int sweep, int32_t v, Hea
         __syncthreads();
     }
     int32_t dcs = -1;
+    if (!LOUV) {   // LPA: labels at the top count (ties redraw at every visit: revisited while tracking)
+        const long long top = sh.s[0];
+        const int hv0 = sh.have[0];
+        __syncthreads();                         // every thread has read the reduction's result
+        if (threadIdx.x == 0) sh.have[0] = 0;
+        __syncthreads();
+        int nt = 0;
+        if (hv0)
+            for (uint32_t s = threadIdx.x; s < slots; s += NTH) nt += (keys[s] >= 0 && (long long)vals[s] == top) ? 1 : 0;
+        if (nt) atomicAdd(&sh.have[0], nt);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (tied_out) *tied_out = sh.have[0] >= 2;
+            sh.have[0] = hv0;
+        }
+        __syncthreads();
+    }
     if (threadIdx.x == 0)
         dcs = decide_final<LOUV, TT>(a, r, v, own, sh.s[0], sh.c[0], sh.kown[0], sh.have[0], dq_out, unst_out);
     __syncthreads();
@@ -790,9 +834,11 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
         const int32_t v = a.heavy[3 * item + 2];
         unsigned long long dq = 0;
         int unst = 0;
+        bool tied = false;
         const int32_t dcs = heavy_visit<LOUV, TT, TB>(a, r, sweep, v, sh, a.heavy_scratch + (int64_t)blockIdx.x * 2 * a.heavy_slots,
-                                                  &dq, &unst);
+                                                  &dq, &unst, &tied);
         if (threadIdx.x == 0) {
+            if (!LOUV && tied && a.track[r]) aff_set(a.aff + (int64_t)r * a.aw, v);
             a.dec[(int64_t)r * a.dstride + di].x = dcs;   // the light kernel wrote v, own, k_v
             if (dq) atomicAdd(red_slot(a, r, 0), dq);
             if (unst) atomicAdd(red_slot(a, r, 1), 1ull);
@@ -800,11 +846,6 @@ __global__ __launch_bounds__(256) void k_decide_heavy(CDArgs a, int bucket, int 
     }
 }
 
-// Affected bits: one atomic OR per flag (a moved vertex's neighbour); 8x less memory than a
-// byte per vertex, so a replica's flags (N/8 bytes) stay cache-resident between the movers
-// that set them and the next sweep's list build
-__device__ __forceinline__ void aff_set(uint32_t* affr, int32_t v) { atomicOr(affr + (v >> 5), 1u << (v & 31)); }
-__device__ __forceinline__ bool aff_get(const uint32_t* affr, int64_t v) { return (affr[v >> 5] >> (v & 31)) & 1u; }
 // Apply a bucket's decisions (fixed grid: blockIdx.y = replica, blocks stride over the
 // replica's list).  Label + community totals only (the replica neither pushes nor tracks
 // this sweep): one thread per decision slot.  Otherwise one 16-lane tile per slot: lane 0
@@ -1063,6 +1104,8 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 if (lane == 0 && nc) atomicAdd(&s_acc[5], (unsigned long long)nc);
                 if (in) {
                     decr[idx] = make_int4(v >= 0 ? vis.dcs : -1, v, vis.own, vis.kvw);
+                    // LPA, tracked: a tied vertex joins the next worklist itself
+                    if (!LOUV && vis.tied && trk && atomicMax(&mark[v], stamp) < stamp) wl2[atomicAdd(&s_nnext, 1)] = v;
                     if (vis.heavy) hv[atomicAdd(&s_nheavy, 1)] = (int32_t)idx;
                     if (vis.dq) atomicAdd(&s_acc[0], vis.dq);
                     if (vis.unst) atomicAdd(&s_acc[1], 1ull);
@@ -1079,8 +1122,10 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
                 const int32_t v = decr[idx].y;
                 unsigned long long dq = 0;
                 int unst = 0;
-                const int32_t dcs = heavy_visit<LOUV, TT, NTH>(a, r, sweep, v, sh, scratch, &dq, &unst);
+                bool tied = false;
+                const int32_t dcs = heavy_visit<LOUV, TT, NTH>(a, r, sweep, v, sh, scratch, &dq, &unst, &tied);
                 if (threadIdx.x == 0) {
+                    if (!LOUV && tied && trk && atomicMax(&mark[v], stamp) < stamp) wl2[atomicAdd(&s_nnext, 1)] = v;
                     decr[idx].x = dcs;
                     if (dq) atomicAdd(&s_acc[0], dq);
                     if (unst) atomicAdd(&s_acc[1], 1ull);
@@ -1428,7 +1473,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
                "edge weights too large for exact int64 modularity gains");
 
     CDArgs a;
-    a.N = N; a.S = S; a.PN = PN; a.B = B; a.dstride = PN; a.coarsen = c.coarsen; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
+    a.N = N; a.S = S; a.PN = PN; a.B = B; a.dstride = PN; a.coarsen = louv ? c.coarsen : 0; a.chunk = CH; a.perm_n = (uint32_t)NC; a.n_r = rcount; a.rbase = rbegin; a.iter = (uint32_t)iteration; a.seed = c.seed;
     a.rowptr = g.rowptr.as<int64_t>(); a.col = g.col.as<int32_t>(); a.cw = g.cw.as<int32_t>();
     a.colp = g.colp.as<int32_t>(); a.spos = spos; a.vrec = g.vrec.as<int4>();
     a.kdeg = g.kdeg.as<int64_t>(); a.M2 = g.M2;

@@ -156,6 +156,12 @@ __device__ __forceinline__ void wsync() {
     asm volatile("" ::: "memory");
 }
 
+// LPA, tracked sweep: a visit with several dominant labels flags its own vertex for the next
+// sweep (igraph redraws among them at every visit; oracle tw_replica) -- one lane's bit
+__device__ __forceinline__ void rl_tie_flag(const RL& a, int rr, int32_t v) {
+    atomicOr((unsigned long long*)&a.aff[(int64_t)(rr >> 6) * a.N + v], 1ull << (rr & 63));
+}
+
 // ------------------------------------------------------------------ init / export
 __global__ void k_rl_init(int64_t N, int ldT, const int64_t* kdeg, int32_t* lab, int32_t* tot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -405,6 +411,10 @@ __device__ __forceinline__ void oem_sort(int32_t (&x)[K]) {
 // colw and kept 4 per register while the label gathers are in flight (weights < 256), WM_WIDE a
 // separate cw row (one register per entry)
 constexpr int WM_WIDE = 0, WM_UNIT = 1, WM_W8 = 2;
+#ifndef FC_RL_SB
+#define FC_RL_SB 16
+#endif
+constexpr int SB = FC_RL_SB;            // Sigma gathers per batch in rl_runs
 // FC_RL_LPA_OWN (A/B switch, default on): LPA keeps its own-label entries out of the keys too
 // (counted in k_own; the own label a candidate when k_own is the largest count), so a wave whose
 // lanes are all settled (2 k_own > d: own is the unique majority) skips like Louvain's, and the
@@ -417,7 +427,7 @@ constexpr int WM_WIDE = 0, WM_UNIT = 1, WM_W8 = 2;
 template <bool LOUV, int K, int WM>
 __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep, int32_t (&x)[K], int32_t own,
                                            long long kown, int32_t tot_own, uint32_t home, unsigned long long& c_dq,
-                                           uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
+                                           uint32_t& c_unst, uint32_t& c_cand, bool& slow_out, bool& tied_out) {
     constexpr bool UNITW = WM == WM_UNIT;
     const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
     const int wb = UNITW ? 0 : a.wbits;
@@ -474,18 +484,19 @@ __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep,
         // unsigned 64-bit minimum of (Sigma << 32) | ~hash; the hash is a bijection of the id
         // (no id tie is left), inverted for the winner
         uint64_t bkey = ~0ull;
+        // SB positions per batch: FC_RL_SB (default 16; 8 holds 8 fewer VGPRs live)
 #pragma unroll
-        for (int c0 = 0; c0 < K; c0 += 16) {
-            const uint32_t bits = ((c0 < 32 ? cm_lo : cm_hi) >> (c0 & 31)) & 0xffffu;
+        for (int c0 = 0; c0 < K; c0 += SB) {
+            const uint32_t bits = ((c0 < 32 ? cm_lo : cm_hi) >> (c0 & 31)) & ((1u << SB) - 1u);
             if (__ballot(bits != 0) == 0) continue;             // wave-uniform
-            int32_t tq[16];
+            int32_t tq[SB];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {                     // non-candidates read the lane's own slot (a hit)
+            for (int i = 0; i < SB; ++i) {                     // non-candidates read the lane's own slot (a hit)
                 const bool b = (bits >> i) & 1u;
                 tq[i] = ld_off(a.tot, b ? (uint32_t)(x[c0 + i] >> wb) * ldT + rr : home);
             }
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < SB; ++i) {
                 const bool b = (bits >> i) & 1u;
                 const uint32_t hh = hash32(tvh ^ (uint32_t)(x[c0 + i] >> wb));
                 const uint64_t key = ((uint64_t)(kv ? (uint32_t)tq[i] : 0u) << 32) | (uint32_t)~hh;
@@ -532,15 +543,23 @@ __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep,
             c_unst += (kown != (long long)vm) ? 1 : 0;
             dcs = best_c != own ? best_c : -1;
         }
+        tied_out = wk && ncand >= 2;
     }
     return dcs;
 }
 
-template <bool LOUV, int K, int WM>
+// UN (LG = 64, one vertex per wave): the row is wave-uniform, so its neighbour ids (and W8
+// weights) are read by scalar loads through the constant address space (16 per s_load_dwordx16,
+// into SGPRs) and every label gather is one global load with the row's scalar base and the
+// lane's replica offset as its only VGPR: no per-entry address VGPRs or VALU address math.
+// The CSR arrays carry 64 entries of padding, so a 16-entry scalar load never reads past them.
+typedef const int32_t __attribute__((address_space(4))) cint32_t;
+template <bool LOUV, int K, int WM, bool UN = false>
 __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
-                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
+                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out, bool& tied_out) {
     constexpr bool UNITW = WM == WM_UNIT;
     slow_out = false;
+    tied_out = false;
     const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
     const int wb = UNITW ? 0 : a.wbits;
     const int32_t wm = (1 << wb) - 1;
@@ -555,6 +574,68 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
     // per entry)
     const int dsw = wk ? h.ds : 0;
     int32_t x[K];
+    if constexpr (UN && WM != WM_WIDE) {
+        static_assert(K % 16 == 0, "scalar rows load 16 entries at a time");
+        const uint32_t rbs = __builtin_amdgcn_readfirstlane((uint32_t)h.rb);
+        const int dss = __builtin_amdgcn_readfirstlane(h.ds);    // entry-level: uniform in a one-vertex wave
+        cint32_t* cp = (cint32_t*)(WM == WM_W8 ? a.colw : a.col) + rbs;
+        const uint32_t rr4 = rr << 2;
+        int32_t kown_w = 0;
+        int ko = 0;
+        int32_t own_l = own;
+#pragma unroll
+        for (int c0 = 0; c0 < K; c0 += 16) {
+            int32_t cs[16];
+            if (c0 < dss) {                                     // scalar branch
+#pragma unroll
+                for (int i = 0; i < 16; ++i) cs[i] = cp[c0 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int j = c0 + i;
+                int32_t lj = -1;
+                if (j < dss) {                                  // scalar branch
+                    const int32_t cid = WM == WM_W8 ? (cs[i] >> a.wbits) : cs[i];
+                    const char* base = reinterpret_cast<const char*>(a.lab + (int64_t)(uint32_t)cid * ldT);
+                    lj = *reinterpret_cast<const int32_t*>(base + rr4);
+                }
+                x[j] = j < dsw ? lj : -1;
+            }
+            // own-label entries out of the keys (counted), weights packed from the scalar row
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int j = c0 + i;
+                if (j >= dss) continue;                         // scalar
+                const bool mine = (LOUV || FC_RL_LPA_OWN) && x[j] == own_l && x[j] >= 0;
+                if constexpr (WM == WM_W8) {
+                    const int32_t wj = cs[i] & wm;
+                    kown_w += mine ? wj : 0;
+                    x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wj);
+                } else {
+                    ko += mine ? 1 : 0;
+                    x[j] = mine ? -1 : x[j];
+                }
+            }
+        }
+        int32_t tot_own_u = 0;
+        if (LOUV) {
+            const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
+            tot_own_u = wk ? t0 : 0;
+        }
+        const long long kown_u = WM == WM_W8 ? (long long)kown_w : (long long)ko;
+        if (LOUV) {
+            const long long kvl = h.kvi;
+            const bool settled = !wk || (kvl - 2 * kown_u) * a.M2 + kvl * ((long long)tot_own_u - kvl) <= 0;
+            if (__ballot(!settled) == 0) return -1;             // wave-uniform
+        } else if (FC_RL_LPA_OWN) {
+            const bool settled = !wk || 2 * kown_u > (long long)dsw;
+            if (__ballot(!settled) == 0) {
+                if (wk) c_cand += 1u;
+                return -1;
+            }
+        }
+        return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown_u, tot_own_u, home, c_dq, c_unst, c_cand, slow_out, tied_out);
+    }
 #pragma unroll
     for (int j = 0; j < K; ++j)                                 // idle / padding lanes read col[rb] (a hit)
         x[j] = ld_off(WM == WM_W8 ? a.colw : a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
@@ -638,7 +719,7 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             return -1;
         }
     }
-    return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
+    return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out, tied_out);
 }
 
 // Light rows with sortable keys (label and weight fit 31 bits): no LDS, one sorting network
@@ -661,7 +742,7 @@ __device__ __forceinline__ void rl_push_slow(const RL& a, bool slow, int64_t e, 
 #ifndef FC_RLW32
 #define FC_RLW32 1
 #endif
-template <bool LOUV, int K, int WM>
+template <bool LOUV, int K, int WM, bool UN>
 __global__ __launch_bounds__(RTB) __attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 32 ? FC_RLW32 : 1)))
 void k_rl_decide(RL a, int seg, int sweep) {
     const int lane = threadIdx.x & 63;
@@ -696,9 +777,14 @@ void k_rl_decide(RL a, int seg, int sweep) {
         const Rec cur = nxt;
         nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
         const Hdr h = rl_header(a, u, cur);
-        bool slow;
-        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
+        bool slow, tied;
+        const int32_t dcs = rl_sorted<LOUV, K, WM, UN>(a, h, sweep, c_dq, c_unst, c_cand, slow, tied);
         rl_push_slow(a, slow, u.e, h.rr);
+        if (!LOUV) {                                            // LPA ties of tracked replicas: one OR per sub-group
+            const uint64_t tb = __ballot(tied && a.track[h.rr]);
+            const uint64_t ts = (tb >> (u.s * LG)) & (LG == 64 ? ~0ull : ((1ull << LG) - 1ull));
+            if (u.valid && u.rl == 0 && ts) atomicOr((unsigned long long*)&a.aff[(int64_t)u.bank * a.N + h.v], (unsigned long long)ts);
+        }
         if (h.work) { c_vis += 1; c_ent += (uint32_t)h.d; }
         if (u.valid && u.rl == 0 && h.msk) c_units += 1;
         if (u.valid && h.rr < a.n_r) a.dec[u.e * a.ldT + h.rr] = h.work ? dcs : -1;
@@ -732,9 +818,10 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
         h.ds = valid ? h.d : 0;
         unsigned long long c_dq = 0;
         uint32_t c_unst = 0, c_cand = 0;
-        bool slow;
-        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
+        bool slow, tied;
+        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow, tied);
         rl_push_slow(a, slow, e, h.rr);
+        if (!LOUV && valid && tied && a.track[h.rr]) rl_tie_flag(a, h.rr, h.v);
         if (valid) {
             a.dec[e * a.ldT + h.rr] = h.work ? dcs : -1;
             if (c_dq) atomicAdd(rl_red(a, h.rr, 0), c_dq);
@@ -754,12 +841,12 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
 // generations of 4-5 items, the last one on two thirds of the SIMDs.  LPA keeps the 8192 cap:
 // its items' cost varies more (most waves settled, a few sorting) and the extra blocks balance
 // it (SBM-4M 687 vs 695 ms).
-template <bool LOUV, int K, int WM>
+template <bool LOUV, int K, int WM, bool UN>
 static int64_t rl_decide_slots() {
     static int64_t slots = 0;
     if (!slots) {
         int nb = 0, dev = 0;
-        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM>, RTB, 0));
+        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM, UN>, RTB, 0));
         FC_HIP(hipGetDevice(&dev));
         int cus = 0;
         FC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -974,6 +1061,7 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_lds(RL a, int k, int sweep) {
                     c_unst += (kown != (long long)vm) ? 1 : 0;
                     dcs = best_c != own ? best_c : -1;
                 }
+                if (nc >= 2 && a.track[rr]) rl_tie_flag(a, rr, v);
             }
         }
         if (work) { c_vis += 1; c_ent += (unsigned long long)d; }
@@ -1073,6 +1161,14 @@ __global__ __launch_bounds__(HTB) void k_rl_exact(RL a, int k, int sweep) {
             kown += __shfl_xor(kown, off);
             ncand += __shfl_xor(ncand, off);
         }
+        if (!LOUV && best_c != INT_MAX && a.track[rr]) {          // LPA ties at the top count (wave-uniform)
+            int nt = 0;
+            for (uint32_t q = lane; q < slots; q += 64) nt += (keys[q] >= 0 && (long long)vals[q] == best_s) ? 1 : 0;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) nt += __shfl_xor(nt, off);
+            if (lane == 0 && nt >= 2) rl_tie_flag(a, rr, v);
+        }
+        wsync();                                              // the table is reused by the next visit
         if (lane == 0) {
             int32_t dcs = -1;
             if (best_c != INT_MAX) {
@@ -1396,7 +1492,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     const bool pack = ((int64_t)(N - 1) << (a.unitw ? 0 : a.wbits)) < (int64_t(1) << 31);
     a.colw = nullptr;
     if (pack && louv && !a.unitw && a.wbits <= 8 && g.m > 0) {
-        int32_t* cwp = ensure<int32_t>(c.rl_colw, 2 * (size_t)g.m);
+        int32_t* cwp = ensure<int32_t>(c.rl_colw, 2 * (size_t)g.m + CSR_PAD);
         k_rl_colw<<<nb(2 * g.m, 256), 256, 0, c.stream>>>(2 * g.m, g.col.as<int32_t>(), g.cw.as<int32_t>(), a.wbits, cwp);
         a.colw = cwp;
     }
@@ -1496,6 +1592,8 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             exclusive_scan(c, (const int32_t*)nvv, nvv + n_ent + 1, n_ent);
             k_rl_visits_fill<<<nb(n_ent, LTB), LTB, 0, c.stream>>>(a, n_ent, nvv + n_ent + 1);
         }
+        // one vertex per wave (LG = 64): wave-uniform rows, read by scalar loads (FC_RL_UNIFORM=0: off)
+        const bool uniform_rows = LG == 64 && c.rl_uniform;
         auto grid_of = [&](int64_t n) {
             const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
             return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
@@ -1526,15 +1624,17 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     const int64_t n = hb[seg + 1] - hb[seg];
                     if (n <= 0) continue;
                     const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
-#define RL_LAUNCH(L, KK, U)                                                                                        \
+#define RL_LAUNCH_UN(L, KK, U, UNF)                                                                                \
     do {                                                                                                           \
         const unsigned grid = (c.rl_grid_mul > 0 && L)                                                             \
-            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U>() * c.rl_grid_mul)) \
+            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U, UNF>() * c.rl_grid_mul)) \
             : grid_of(n);                                                                                          \
         const int ev = timer_begin(c);                                                                             \
-        k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                          \
+        k_rl_decide<L, KK, U, UNF><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                     \
         timer_end(c, 7, ev);                                                                                       \
     } while (0)
+#define RL_LAUNCH(L, KK, U) \
+    do { if (uniform_rows && U != WM_WIDE) RL_LAUNCH_UN(L, KK, U, true); else RL_LAUNCH_UN(L, KK, U, false); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
@@ -1543,6 +1643,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     else RL_LAUNCH_K(false, WM_UNIT);
 #undef RL_LAUNCH_K
 #undef RL_LAUNCH
+#undef RL_LAUNCH_UN
                 }
             } else {
                 const int64_t n = hb[k * NCLS + NCLS - 1] - hb[k * NCLS];

@@ -128,6 +128,8 @@ struct Ctx {
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
+    // replica-lane decide with one vertex per wave: rows through scalar loads (A/B switch)
+    int rl_uniform = getenv("FC_RL_UNIFORM") ? atoi(getenv("FC_RL_UNIFORM")) : 1;
     int cd_engine = 2;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip), 1 replica-lane (cd_rl.hip), 2 hybrid (default)
     // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many
     // replicas (8 lanes per vertex at 8: LFR-1M n_p = 8 run 40.3 vs 42.9 ms on cd.hip since the
@@ -301,6 +303,7 @@ void shards_fold(Ctx& c, int F, unsigned max_mask, int64_t* host_out);
 int64_t read_i64(Ctx& c, const int64_t* dev);
 
 constexpr int64_t AGE_ITER_SHIFT = 40;
+constexpr int64_t CSR_PAD = 64;   // extra entries behind col / cw / colw (scalar row loads read up to 15 past a row)
 constexpr int64_t AGE_REPAIR_OFFSET = int64_t(1) << 39;
 
 }  // namespace fc

@@ -152,7 +152,8 @@ def engine_opts(request):
     return ENGINE_OPTS[request.param]
 
 
-def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds, opts=None):
+def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds, opts=None, nmi_fn=None):
+    nmi_fn = nmi_fn or nmi
     out = []
     for seed in seeds:
         with fcmod.Engine(seed=seed) as eng:
@@ -161,26 +162,56 @@ def device_runs(fcmod, algo, N, e, n_p, tau, delta, planted, seeds, opts=None):
             eng.load_graph(N, e[:, 0], e[:, 1])
             labels, st = eng.run(algo, n_p, tau, delta)
         assert st["iterations"] >= 1 and not st["hit_iter_cap"]
-        out.append(float(np.mean([nmi(planted, l) for l in labels])))
+        out.append(float(np.mean([nmi_fn(planted, l) for l in labels])))
     return np.array(out)
 
 
-def test_c2_louvain_consensus_nmi_vs_reference(fcmod, engine_opts):
-    """The whole louvain consensus against the reference's own output.  The consensus NMI
-    varies from run to run (0.78-0.95 on LFR-1k), so the device's mean over 32 seeds is held
-    to the REFERENCE LOOP's mean over 30 seeds (its unmodified code with the restated CD,
-    refsem fixture): >= reference - 0.025 (about 2.5 standard errors of the difference); the
-    reference run's recorded final partitions (fast_consensus.py:383-392, one sample) are
-    printed beside it."""
+def test_c2_louvain_consensus_distribution_default_engine(fcmod):
+    """The whole louvain consensus of the DEFAULT engine against the reference loop's
+    distribution (its unmodified code with the restated CD, refsem fixture, >= 400 seeds).
+    The consensus NMI is bimodal (0.70-0.95 on LFR-1k), so the gates are on the distribution
+    (tests/dist_gates.py: mean >= reference - 0.015, sd <= 1.3 x reference, 10th percentile >=
+    reference - 0.03, one-sided KS at alpha 0.01) over 400 device seeds.  The device's NMIs must
+    also equal, seed for seed, the CPU model's (model_c2_louvain.json, written by
+    tests/test_engine_semantics.py with the device's vertex numbering): 400 whole runs
+    bit-exact.  The hybrid with its replica-lane kernels forced at this size gives the same
+    runs (same semantics); checked on the first 48 seeds."""
+    import json
+    from tests import dist_gates
     case = golden_io.load("lfr1k_louvain_np20")
     _, g, planted = lfr1k()
     ref = refsem("lfr1k_louvain_np20")
-    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(100, 132), engine_opts)
+    with open(golden_io.GOLDEN + "/model_c2_louvain.json") as f:
+        fix = json.load(f)
+    seeds = fix["seeds"]
+    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, seeds, nmi_fn=dist_gates.nmi)
+    bad = np.flatnonzero(np.abs(got - np.array(fix["nmi"])) > 1e-12)
+    assert bad.size == 0, "device differs from the CPU model at seeds %s" % [seeds[i] for i in bad[:10]]
+    rl = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, seeds[:48],
+                     ENGINE_OPTS["hybrid_rl"], nmi_fn=dist_gates.nmi)
+    np.testing.assert_allclose(rl, got[:48], rtol=0, atol=1e-12)
     one = float(np.mean([nmi(planted, l) for l in case.z["final_labels"]]))
-    print("C2 louvain consensus NMI: device mean %.4f sd %.4f min %.4f | reference loop mean %.4f sd %.4f min %.4f "
-          "| reference run's recorded output %.4f" % (got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"],
-                                                        min(ref["nmi"]), one))
-    assert got.mean() >= ref["nmi_mean"] - 0.025
+    print("reference run's recorded output %.4f" % one)
+    dist_gates.check(got, ref["nmi"], 0.015, "C2 louvain consensus NMI (default engine)")
+
+
+@pytest.mark.parametrize("engine", ["classic", "replica_lane"])
+def test_c2_louvain_consensus_nmi_other_engines(fcmod, engine):
+    """The opt-in engines (per-replica orders throughout; one shared order in every sweep):
+    mean over 160 seeds >= the reference loop's mean - 0.02; the distribution statistics are
+    printed (DESIGN.md "Consensus distribution": the classic engine's lower tail is the
+    heavier one at 16 buckets)."""
+    from tests import dist_gates
+    case = golden_io.load("lfr1k_louvain_np20")
+    _, g, planted = lfr1k()
+    ref = refsem("lfr1k_louvain_np20")
+    got = device_runs(fcmod, 0, case.N, case.edges_file, 20, 0.2, 0.02, planted, range(1000, 1160),
+                      ENGINE_OPTS[engine], nmi_fn=dist_gates.nmi)
+    try:
+        dist_gates.check(got, ref["nmi"], 0.02, "C2 louvain consensus NMI (%s)" % engine)
+    except AssertionError as e:
+        print("(not gated beyond the mean for this opt-in engine)", str(e)[:60])
+    assert got.mean() >= np.mean(ref["nmi"]) - 0.02
 
 
 def test_c2_lpm_consensus_nmi_vs_reference(fcmod, engine_opts):
@@ -264,19 +295,48 @@ def test_c3_consensus_update_bit_exact_and_run(fcmod, lfr100k, algo, tau):
         assert s > 0.8
 
 
-def test_c3_consensus_nmi_vs_reference_semantics(fcmod, lfr100k, engine_opts):
-    """BASELINE configs[2] louvain and lpm, n_p=64: the device's whole-consensus NMI to the
-    planted communities (mean of the n_p final partitions, fast_consensus.py:383-392), averaged
-    over 8 seeds, against the reference loop's distribution at the same size
-    (refsem_lfr100k_*_np64.json: orc.refsem_run, the golden-pinned loop with the sequential CD
-    restatements and the reference's sequential closure; 16 / 8 seeds, make_refsem.py c3).
-    Tolerance: device mean >= reference mean - 0.01 (louvain) / - 0.02 (lpm)."""
-    n, e, planted = lfr100k
-    for algo, name, tau, tol in ((0, "lfr100k_louvain_np64", 0.2, 0.01), (1, "lfr100k_lpm_np64", 0.8, 0.02)):
+@pytest.fixture(scope="module")
+def lfr100k_sparse():
+    """C3's mu = 0.5 at average degree 8 (max 25): LPA's consensus does not saturate here
+    (reference loop NMI ~0.956; on C3's own graph every lpm run, reference and device, sits at
+    1.0000 and the gate could not discriminate)."""
+    from fastconsensus_amd import synth
+    u, v, planted = synth.lfr(100_000, 0.5, seed=42, avg_deg=8, max_deg=25)
+    return 100_000, np.stack([u, v], 1), planted
+
+
+C3_CASES = {"louvain": (0, "lfr100k_louvain_np64", 0.2, "lfr100k"),
+            "lpm": (1, "lfr100k_sparse_lpm_np64", 0.8, "lfr100k_sparse")}
+
+
+@pytest.mark.parametrize("alg", sorted(C3_CASES))
+def test_c3_consensus_distribution_default_engine(fcmod, request, alg):
+    """BASELINE configs[2], n_p=64, the DEFAULT engine: the whole-consensus NMI to the planted
+    communities (mean of the n_p final partitions, fast_consensus.py:383-392) over 40 device
+    seeds against the reference loop's distribution at the same size (orc.refsem_run, the
+    golden-pinned loop with the sequential CD restatements and the reference's sequential
+    closure; make_refsem.py c3v2: 64 seeds louvain, 32 lpm), with tests/dist_gates.py's
+    gates (mean >= reference - 0.01)."""
+    from tests import dist_gates
+    algo, name, tau, graph = C3_CASES[alg]
+    n, e, planted = request.getfixturevalue(graph)
+    ref = refsem(name)
+    got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 340), nmi_fn=dist_gates.nmi)
+    dist_gates.check(got, ref["nmi"], 0.01, "C3 %s consensus NMI (default engine)" % name, ks=False)
+
+
+def test_c3_consensus_nmi_other_engines(fcmod, lfr100k, lfr100k_sparse, engine_opts):
+    """Every engine (incl. the opt-in ones): mean over 8 seeds >= reference mean - 0.01
+    (louvain) / - 0.02 (lpm, on the non-saturated graph)."""
+    from tests import dist_gates
+    for alg, tol in (("louvain", 0.01), ("lpm", 0.02)):
+        algo, name, tau, graph = C3_CASES[alg]
+        n, e, planted = lfr100k if graph == "lfr100k" else lfr100k_sparse
         ref = refsem(name)
-        got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 308), engine_opts)
-        print("C3 %s consensus NMI: device mean %.4f sd %.4f min %.4f | reference semantics mean %.4f sd %.4f min %.4f"
-              % (name, got.mean(), got.std(), got.min(), ref["nmi_mean"], ref["nmi_sd"], min(ref["nmi"])))
+        got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 308), engine_opts,
+                          nmi_fn=dist_gates.nmi)
+        print("C3 %s consensus NMI: device %s | reference %s" % (name, dist_gates.describe(got),
+                                                                dist_gates.describe(ref["nmi"])))
         assert got.mean() >= ref["nmi_mean"] - tol
 
 
