@@ -125,7 +125,7 @@ int fc_create(int device, uint64_t seed, fc_ctx** out) {
         FC_HIP(hipSetDevice(device));
         FC_HIP(hipStreamCreateWithFlags(&c.own_stream, hipStreamNonBlocking));
         c.stream = c.own_stream;
-        FC_HIP(hipHostMalloc((void**)&c.hpin, 64 * sizeof(int64_t), hipHostMallocDefault));
+        FC_HIP(hipHostMalloc((void**)&c.hpin, FC_HPIN_I64 * sizeof(int64_t), hipHostMallocDefault));
     } catch (...) {
         delete x;
         throw;

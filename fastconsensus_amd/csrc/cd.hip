@@ -1258,9 +1258,18 @@ __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t
 // Rounds per replica: lcnt[k][r] (entries of round k), loff[r][k] (offsets into the
 // replica's list), fill cursors, coarsening g; info[0] = max rounds, info[2..3] = visits,
 // info[4] = the largest replica's visits.
-__global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int32_t* cursor, int32_t* gco,
-                            int32_t* lcnt, int4* rrec, int32_t* info) {
+// One block.  It also resets what the sweep's bookkeeping accumulates -- info (zeroed before
+// the atomics below) and cntfine (each replica's row, once read: the next sweep's k_list_count
+// finds it zero) -- and copies the active count left by the previous sweep into info[6], so a
+// sweep costs one host read and no memset launches.
+__global__ void k_list_plan(CDArgs a, int32_t* cntfine, int32_t* loff, int32_t* cursor, int32_t* gco,
+                            int32_t* lcnt, int4* rrec, int32_t* info, const int32_t* n_active) {
     const int B = a.B;
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) info[i] = 0;
+        info[6] = n_active[0];
+    }
+    __syncthreads();
     for (int r = threadIdx.x; r < a.n_r; r += blockDim.x) {
         int32_t* lo = loff + (int64_t)r * (B + 1);
         if (!a.active[r]) {
@@ -1289,7 +1298,7 @@ __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int
             atomicMax(info + 4, (int)min(tot, (int64_t)INT_MAX));
             continue;
         }
-        const int32_t* cf = cntfine + (int64_t)r * B;
+        int32_t* cf = cntfine + (int64_t)r * B;
         int64_t V = 0;
         for (int k = 0; k < B; ++k) V += cf[k];
         const int g = (a.coarsen && !rep_dense(a, r)) ? coarse_factor(a.N, V, B, a.coarsen) : 1;
@@ -1307,6 +1316,7 @@ __global__ void k_list_plan(CDArgs a, const int32_t* cntfine, int32_t* loff, int
             acc += c;
         }
         lo[B] = acc;
+        for (int k = 0; k < B; ++k) cf[k] = 0;   // consumed: zero for the next sweep
         gco[r] = g;
         atomicMax(info + 1, (cmax + LNT - 1) / LNT);
         atomicMax(info, rounds);
@@ -1525,17 +1535,15 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int sweep0 = h ? h->sweep0 : 0;
     int sweep = sweep0;
     if (c.trace && !h) { sync(c); trace_dt_us(true); }   // a hand-off's first sweep includes the conversion
+    FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));   // then kept zero by k_list_plan
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
-        FC_HIP(hipMemsetAsync(cntfine, 0, sizeof(int32_t) * (size_t)rcount * B, c.stream));
-        FC_HIP(hipMemsetAsync(info, 0, 8 * sizeof(int32_t), c.stream));
         if (vcnt && sweep > 0) {
             FC_HIP(hipMemsetAsync(vcnt, 0, sizeof(int32_t) * (size_t)rcount, c.stream));
             k_aff_count<<<dim3(lb_grid, rcount), TB, 0, c.stream>>>(a, vcnt);
         }
         k_list_count<<<dim3(lb_grid, rcount), TB, sizeof(int) * B, c.stream>>>(a, sweep, cntfine);
-        k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, rrec, info);
-        FC_HIP(hipMemcpyAsync(hinfo, info, 20, hipMemcpyDeviceToHost, c.stream));
-        FC_HIP(hipMemcpyAsync(hinfo + 6, n_active, 4, hipMemcpyDeviceToHost, c.stream));
+        k_list_plan<<<1, TB, 0, c.stream>>>(a, cntfine, loff, cursor, gco, lcnt, rrec, info, n_active);
+        FC_HIP(hipMemcpyAsync(hinfo, info, 28, hipMemcpyDeviceToHost, c.stream));
         sync(c);
         const int rounds = hinfo[0];
         const unsigned long long visits = *(unsigned long long*)(hinfo + 2);

@@ -247,16 +247,22 @@ __global__ __launch_bounds__(LTB) void k_rl_list_count(RL a, int sweep, int list
         if (s_v[k]) atomicAdd(&vcnt[k], s_v[k]);
     }
 }
-__global__ void k_rl_list_plan(int nseg, const int32_t* bcnt, int32_t* boff, int32_t* cursor, const int32_t* vcnt,
-                               int32_t* voff, int32_t* vcursor) {
+// Offsets of the sweep's segments; the counts are zeroed once read (the next sweep's
+// k_rl_list_count finds them zero: no memset launches per sweep) and the active counts the
+// previous sweep left are copied behind voff, so boff | voff | n_active[0..1] is ONE host read.
+__global__ void k_rl_list_plan(int nseg, int32_t* bcnt, int32_t* boff, int32_t* cursor, int32_t* vcnt,
+                               int32_t* voff, int32_t* vcursor, const int32_t* n_active) {
     if (threadIdx.x != 0) return;
     int32_t acc = 0, vacc = 0;
     for (int k = 0; k < nseg; ++k) {
         boff[k] = acc; cursor[k] = acc; acc += bcnt[k];
         voff[k] = vacc; vcursor[k] = vacc; vacc += vcnt[k];
+        bcnt[k] = 0; vcnt[k] = 0;
     }
     boff[nseg] = acc;
     voff[nseg] = vacc;
+    voff[nseg + 1] = n_active[0];
+    voff[nseg + 2] = n_active[1];
 }
 // Visit mode: each listed entry's replicas as (entry, replica) pairs.  The entries are
 // segment-major, so an exclusive scan of the per-entry visit counts lays the visits out
@@ -548,13 +554,7 @@ __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep,
     return dcs;
 }
 
-// UN (LG = 64, one vertex per wave): the row is wave-uniform, so its neighbour ids (and W8
-// weights) are read by scalar loads through the constant address space (16 per s_load_dwordx16,
-// into SGPRs) and every label gather is one global load with the row's scalar base and the
-// lane's replica offset as its only VGPR: no per-entry address VGPRs or VALU address math.
-// The CSR arrays carry 64 entries of padding, so a 16-entry scalar load never reads past them.
-typedef const int32_t __attribute__((address_space(4))) cint32_t;
-template <bool LOUV, int K, int WM, bool UN = false>
+template <bool LOUV, int K, int WM>
 __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
                                              uint32_t& c_unst, uint32_t& c_cand, bool& slow_out, bool& tied_out) {
     constexpr bool UNITW = WM == WM_UNIT;
@@ -574,68 +574,6 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
     // per entry)
     const int dsw = wk ? h.ds : 0;
     int32_t x[K];
-    if constexpr (UN && WM != WM_WIDE) {
-        static_assert(K % 16 == 0, "scalar rows load 16 entries at a time");
-        const uint32_t rbs = __builtin_amdgcn_readfirstlane((uint32_t)h.rb);
-        const int dss = __builtin_amdgcn_readfirstlane(h.ds);    // entry-level: uniform in a one-vertex wave
-        cint32_t* cp = (cint32_t*)(WM == WM_W8 ? a.colw : a.col) + rbs;
-        const uint32_t rr4 = rr << 2;
-        int32_t kown_w = 0;
-        int ko = 0;
-        int32_t own_l = own;
-#pragma unroll
-        for (int c0 = 0; c0 < K; c0 += 16) {
-            int32_t cs[16];
-            if (c0 < dss) {                                     // scalar branch
-#pragma unroll
-                for (int i = 0; i < 16; ++i) cs[i] = cp[c0 + i];
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int j = c0 + i;
-                int32_t lj = -1;
-                if (j < dss) {                                  // scalar branch
-                    const int32_t cid = WM == WM_W8 ? (cs[i] >> a.wbits) : cs[i];
-                    const char* base = reinterpret_cast<const char*>(a.lab + (int64_t)(uint32_t)cid * ldT);
-                    lj = *reinterpret_cast<const int32_t*>(base + rr4);
-                }
-                x[j] = j < dsw ? lj : -1;
-            }
-            // own-label entries out of the keys (counted), weights packed from the scalar row
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int j = c0 + i;
-                if (j >= dss) continue;                         // scalar
-                const bool mine = (LOUV || FC_RL_LPA_OWN) && x[j] == own_l && x[j] >= 0;
-                if constexpr (WM == WM_W8) {
-                    const int32_t wj = cs[i] & wm;
-                    kown_w += mine ? wj : 0;
-                    x[j] = (mine || x[j] < 0) ? -1 : ((x[j] << wb) | wj);
-                } else {
-                    ko += mine ? 1 : 0;
-                    x[j] = mine ? -1 : x[j];
-                }
-            }
-        }
-        int32_t tot_own_u = 0;
-        if (LOUV) {
-            const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
-            tot_own_u = wk ? t0 : 0;
-        }
-        const long long kown_u = WM == WM_W8 ? (long long)kown_w : (long long)ko;
-        if (LOUV) {
-            const long long kvl = h.kvi;
-            const bool settled = !wk || (kvl - 2 * kown_u) * a.M2 + kvl * ((long long)tot_own_u - kvl) <= 0;
-            if (__ballot(!settled) == 0) return -1;             // wave-uniform
-        } else if (FC_RL_LPA_OWN) {
-            const bool settled = !wk || 2 * kown_u > (long long)dsw;
-            if (__ballot(!settled) == 0) {
-                if (wk) c_cand += 1u;
-                return -1;
-            }
-        }
-        return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown_u, tot_own_u, home, c_dq, c_unst, c_cand, slow_out, tied_out);
-    }
 #pragma unroll
     for (int j = 0; j < K; ++j)                                 // idle / padding lanes read col[rb] (a hit)
         x[j] = ld_off(WM == WM_W8 ? a.colw : a.col, (uint32_t)h.rb + (uint32_t)(j < dsw ? j : 0));
@@ -742,7 +680,7 @@ __device__ __forceinline__ void rl_push_slow(const RL& a, bool slow, int64_t e, 
 #ifndef FC_RLW32
 #define FC_RLW32 1
 #endif
-template <bool LOUV, int K, int WM, bool UN>
+template <bool LOUV, int K, int WM>
 __global__ __launch_bounds__(RTB) __attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 32 ? FC_RLW32 : 1)))
 void k_rl_decide(RL a, int seg, int sweep) {
     const int lane = threadIdx.x & 63;
@@ -778,7 +716,7 @@ void k_rl_decide(RL a, int seg, int sweep) {
         nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
         const Hdr h = rl_header(a, u, cur);
         bool slow, tied;
-        const int32_t dcs = rl_sorted<LOUV, K, WM, UN>(a, h, sweep, c_dq, c_unst, c_cand, slow, tied);
+        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow, tied);
         rl_push_slow(a, slow, u.e, h.rr);
         if (!LOUV) {                                            // LPA ties of tracked replicas: one OR per sub-group
             const uint64_t tb = __ballot(tied && a.track[h.rr]);
@@ -841,12 +779,12 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
 // generations of 4-5 items, the last one on two thirds of the SIMDs.  LPA keeps the 8192 cap:
 // its items' cost varies more (most waves settled, a few sorting) and the extra blocks balance
 // it (SBM-4M 687 vs 695 ms).
-template <bool LOUV, int K, int WM, bool UN>
+template <bool LOUV, int K, int WM>
 static int64_t rl_decide_slots() {
     static int64_t slots = 0;
     if (!slots) {
         int nb = 0, dev = 0;
-        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM, UN>, RTB, 0));
+        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM>, RTB, 0));
         FC_HIP(hipGetDevice(&dev));
         int cus = 0;
         FC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1492,7 +1430,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     const bool pack = ((int64_t)(N - 1) << (a.unitw ? 0 : a.wbits)) < (int64_t(1) << 31);
     a.colw = nullptr;
     if (pack && louv && !a.unitw && a.wbits <= 8 && g.m > 0) {
-        int32_t* cwp = ensure<int32_t>(c.rl_colw, 2 * (size_t)g.m + CSR_PAD);
+        int32_t* cwp = ensure<int32_t>(c.rl_colw, 2 * (size_t)g.m);
         k_rl_colw<<<nb(2 * g.m, 256), 256, 0, c.stream>>>(2 * g.m, g.col.as<int32_t>(), g.cw.as<int32_t>(), a.wbits, cwp);
         a.colw = cwp;
     }
@@ -1507,13 +1445,17 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
     a.lmask = (uint64_t*)ensure<uint64_t>(c.rl_lmask, (size_t)PN * banks);
     a.vmask = (uint64_t*)ensure<uint64_t>(c.rl_vmask, (size_t)N * banks);
     const int nseg = B * NCLS;
+    // boff [nseg+1] | voff [nseg+1] | n_active copy [2] | bcnt | cursor | vcnt | vcursor
     int32_t* plan = ensure<int32_t>(c.vcnt, 6 * (size_t)nseg + 16);
-    int32_t* bcnt = plan;
-    a.boff = bcnt + nseg;
-    a.cursor = a.boff + nseg + 1;
+    a.boff = plan;
+    a.voff = a.boff + nseg + 1;
+    int32_t* bcnt = a.voff + nseg + 3;
+    a.cursor = bcnt + nseg;
     int32_t* vcnt = a.cursor + nseg;
-    a.voff = vcnt + nseg;
-    a.vcursor = a.voff + nseg + 1;
+    a.vcursor = vcnt + nseg;
+    FC_REQUIRE(16 + 2 * (nseg + 1) + 2 <= 2 * FC_HPIN_I64, FC_ELIMIT, "too many CD buckets for the pinned sweep record");
+    FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * nseg, c.stream));   // kept zero by k_rl_list_plan
+    FC_HIP(hipMemsetAsync(vcnt, 0, sizeof(int32_t) * nseg, c.stream));
     a.vlist = nullptr;
     a.aff = (uint64_t*)ensure<uint64_t>(c.rl_aff, (size_t)banks * N);
     a.mvf = (uint64_t*)ensure<uint64_t>(c.rl_mvf, (size_t)banks * N);
@@ -1555,27 +1497,22 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
 
     k_rl_init<<<nb(N * ldT, 256), 256, 0, c.stream>>>(N, ldT, g.kdeg.as<int64_t>(), a.lab, a.tot);
 
-    int32_t* hinfo = (int32_t*)(c.hpin + 8);   // n_active[0..1] copy
-    std::vector<int32_t> hb(2 * (nseg + 1));   // boff | voff
+    int32_t* hb = (int32_t*)(c.hpin + 8);   // boff | voff | n_active[0..1] (pinned: one DMA per sweep)
+    int32_t* hinfo = hb + 2 * (nseg + 1);
     const unsigned lgrid = nb(N, LTB * LPER);
     const size_t lcount_lds = sizeof(unsigned long long) * 2 * banks + 2 * sizeof(int) * nseg;
     int sweep = 0, handoff = -1;
     if (c.trace) { sync(c); trace_dt_us(true); }
     for (; sweep < c.max_sweeps && g.M2 > 0; ++sweep) {
         const int listed = (c.prune && sweep > 0) ? 1 : 0;
-        FC_HIP(hipMemsetAsync(bcnt, 0, sizeof(int32_t) * nseg, c.stream));
-        FC_HIP(hipMemsetAsync(vcnt, 0, sizeof(int32_t) * nseg, c.stream));
         if (hybrid && listed) {   // per-replica list sizes: a sparse one hands the batch to cd.hip
             FC_HIP(hipMemsetAsync(acnt, 0, sizeof(int32_t) * (size_t)rcount, c.stream));
             if (a.dense_div) k_rl_aff_count<<<lgrid, LTB, sizeof(int) * 64 * banks, c.stream>>>(a, acnt);
             k_rl_hand<<<1, 256, 0, c.stream>>>(a, n_active);
         }
         k_rl_list_count<<<lgrid, LTB, lcount_lds, c.stream>>>(a, sweep, listed, bcnt, vcnt);
-        k_rl_list_plan<<<1, 64, 0, c.stream>>>(nseg, bcnt, a.boff, a.cursor, vcnt, a.voff, a.vcursor);
-        FC_HIP(hipMemcpyAsync(hb.data(), a.boff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost, c.stream));
-        FC_HIP(hipMemcpyAsync(hb.data() + nseg + 1, a.voff, sizeof(int32_t) * (nseg + 1), hipMemcpyDeviceToHost,
-                              c.stream));
-        FC_HIP(hipMemcpyAsync(hinfo, n_active, 8, hipMemcpyDeviceToHost, c.stream));
+        k_rl_list_plan<<<1, 64, 0, c.stream>>>(nseg, bcnt, a.boff, a.cursor, vcnt, a.voff, a.vcursor, n_active);
+        FC_HIP(hipMemcpyAsync(hb, a.boff, sizeof(int32_t) * (2 * (nseg + 1) + 2), hipMemcpyDeviceToHost, c.stream));
         sync(c);
         if (sweep > 0 && hinfo[0] == 0) break;                      // every replica has stopped
         if (hybrid && listed && hinfo[1] > 0) { handoff = sweep; break; }   // a sparse filtered list: cd.hip
@@ -1592,8 +1529,6 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             exclusive_scan(c, (const int32_t*)nvv, nvv + n_ent + 1, n_ent);
             k_rl_visits_fill<<<nb(n_ent, LTB), LTB, 0, c.stream>>>(a, n_ent, nvv + n_ent + 1);
         }
-        // one vertex per wave (LG = 64): wave-uniform rows, read by scalar loads (FC_RL_UNIFORM=0: off)
-        const bool uniform_rows = LG == 64 && c.rl_uniform;
         auto grid_of = [&](int64_t n) {
             const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
             return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
@@ -1624,17 +1559,15 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     const int64_t n = hb[seg + 1] - hb[seg];
                     if (n <= 0) continue;
                     const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
-#define RL_LAUNCH_UN(L, KK, U, UNF)                                                                                \
+#define RL_LAUNCH(L, KK, U)                                                                                        \
     do {                                                                                                           \
         const unsigned grid = (c.rl_grid_mul > 0 && L)                                                             \
-            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U, UNF>() * c.rl_grid_mul)) \
+            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U>() * c.rl_grid_mul)) \
             : grid_of(n);                                                                                          \
         const int ev = timer_begin(c);                                                                             \
-        k_rl_decide<L, KK, U, UNF><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                     \
+        k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                          \
         timer_end(c, 7, ev);                                                                                       \
     } while (0)
-#define RL_LAUNCH(L, KK, U) \
-    do { if (uniform_rows && U != WM_WIDE) RL_LAUNCH_UN(L, KK, U, true); else RL_LAUNCH_UN(L, KK, U, false); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
@@ -1643,7 +1576,6 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     else RL_LAUNCH_K(false, WM_UNIT);
 #undef RL_LAUNCH_K
 #undef RL_LAUNCH
-#undef RL_LAUNCH_UN
                 }
             } else {
                 const int64_t n = hb[k * NCLS + NCLS - 1] - hb[k * NCLS];

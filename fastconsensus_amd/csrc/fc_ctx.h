@@ -128,8 +128,6 @@ struct Ctx {
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
-    // replica-lane decide with one vertex per wave: rows through scalar loads (A/B switch)
-    int rl_uniform = getenv("FC_RL_UNIFORM") ? atoi(getenv("FC_RL_UNIFORM")) : 1;
     int cd_engine = 2;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip), 1 replica-lane (cd_rl.hip), 2 hybrid (default)
     // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many
     // replicas (8 lanes per vertex at 8: LFR-1M n_p = 8 run 40.3 vs 42.9 ms on cd.hip since the
@@ -219,10 +217,11 @@ struct Ctx {
     Timer timer;
     fc_stats acc{};                 // accumulated during a run (fc_run)
     fc_stats prof{};                // accumulated since the last fc_collect_timing
-    int64_t* hpin = nullptr;        // pinned host scratch (64 int64)
+    int64_t* hpin = nullptr;        // pinned host scratch (FC_HPIN_I64 int64)
 };
 
 struct Ctx;
+constexpr int FC_HPIN_I64 = 1024;   // pinned host scratch: per-sweep records (cd_rl.hip: boff | voff | n_active)
 // State the replica-lane engine hands to cd_run at the first filtered sweep of a hybrid batch
 // (FC_OPT_CD_ENGINE=2, cd_rl.hip): fill() writes it in cd.hip's layout on c.stream -- labels
 // [n_r][N] in slot order, int32 totals [n_r][N], affected flags as bit words uint32
@@ -303,7 +302,6 @@ void shards_fold(Ctx& c, int F, unsigned max_mask, int64_t* host_out);
 int64_t read_i64(Ctx& c, const int64_t* dev);
 
 constexpr int64_t AGE_ITER_SHIFT = 40;
-constexpr int64_t CSR_PAD = 64;   // extra entries behind col / cw / colw (scalar row loads read up to 15 past a row)
 constexpr int64_t AGE_REPAIR_OFFSET = int64_t(1) << 39;
 
 }  // namespace fc

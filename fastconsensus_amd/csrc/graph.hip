@@ -283,7 +283,7 @@ void graph_copy(Ctx& c, Graph& dst, const Graph& src) {
     };
     cp(dst.eu, src.eu, 4 * m); cp(dst.ev, src.ev, 4 * m); cp(dst.ew, src.ew, 4 * m); cp(dst.eage, src.eage, 8 * m);
     cp(dst.rowptr, src.rowptr, 8 * (n + 1));
-    cp(dst.col, src.col, 8 * m + 4 * CSR_PAD); cp(dst.cw, src.cw, 8 * m + 4 * CSR_PAD); cp(dst.ceid, src.ceid, 8 * m);
+    cp(dst.col, src.col, 8 * m); cp(dst.cw, src.cw, 8 * m); cp(dst.ceid, src.ceid, 8 * m);
     cp(dst.crev, src.crev, 8 * m);
     cp(dst.colp, src.colp, 8 * m);
     cp(dst.vrec, src.vrec, 16 * n);
@@ -402,8 +402,8 @@ void graph_build_csr(Ctx& c, Graph& g) {
     int64_t* vs = us + (n + 1);
     int64_t* rowptr = ensure<int64_t>(g.rowptr, n + 1);
     int64_t m2 = 2 * m > 0 ? 2 * m : 1;
-    int32_t* col = ensure<int32_t>(g.col, m2 + CSR_PAD);   // padding: 16-entry scalar row loads (cd_rl.hip)
-    int32_t* cw = ensure<int32_t>(g.cw, m2 + CSR_PAD);
+    int32_t* col = ensure<int32_t>(g.col, m2);
+    int32_t* cw = ensure<int32_t>(g.cw, m2);
     int32_t* ceid = ensure<int32_t>(g.ceid, m2);
     uint32_t* k1 = (uint32_t*)ensure<uint64_t>(c.mkey, m > 0 ? m : 1);
     uint32_t* k2 = (uint32_t*)ensure<uint64_t>(c.mkey2, m > 0 ? m : 1);

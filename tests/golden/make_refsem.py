@@ -18,7 +18,11 @@ partitions to the planted communities is recorded, so a device run is compared w
 reference's distribution, not with a single sample (the consensus NMI varies from run to run:
 0.80-0.95 on LFR-1k).  Output: tests/golden/refsem_*.json (data only).
 
-Usage:  python tests/golden/make_refsem.py [c3]   (c3: the LFR-100k records, see run_c3)
+Usage:  python tests/golden/make_refsem.py            the LFR-1k records (30 seeds each)
+        python tests/golden/make_refsem.py c2 480     LFR-1k louvain over 480 seeds (worker processes)
+        python tests/golden/make_refsem.py c3         the round-3 LFR-100k records
+        python tests/golden/make_refsem.py c3v2       LFR-100k louvain over 64 seeds and lpm on the
+                                                      average-degree-8 graph over 32 (see run_c3)
 """
 import importlib.util
 import json
