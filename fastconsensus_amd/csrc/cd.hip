@@ -1473,7 +1473,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     const int32_t* sinv = c.sinv.as<int32_t>();
     if (h) {   // a hybrid batch from its first filtered sweep: the replica-lane engine's state
         FC_REQUIRE(tot32 || !louv, FC_ESTATE, "hybrid hand-off needs int32 totals");
-        h->fill(c, h->user, lab, (int32_t*)tot, aff, track, active);
+        h->fill(c, h->user, lab, (int32_t*)tot, aff, track, active, nlab);
     } else if (tot32) {
         k_cd_init<int32_t><<<ig, TB, 0, c.stream>>>(N, rcount, g.kdeg.as<int64_t>(), sinv, lab, (int32_t*)tot, louv ? 1 : 0);
     } else {

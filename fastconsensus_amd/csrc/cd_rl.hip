@@ -46,6 +46,10 @@ constexpr int VPWMAX = 8;               // sub-groups per wave (lane groups of >
 constexpr int RL_CHUNK = 16;            // = cd.hip CHUNK (chunked visit orders)
 // slow-visit and visit-mode list entries pack the local replica in 14 bits ((e << 14) | rr)
 constexpr int RL_MAX_REPLICAS = 16384;
+#ifndef FC_LPA_TIES
+#define FC_LPA_TIES 1                   // LPA tie revisits under pruning (oracle tw_replica); 0: bisect builds only
+#endif
+
 constexpr int32_t DONE = -1;            // merged / own / empty table entry (labels are >= 0)
 constexpr int NSH = 16;                 // counter shards per replica
 constexpr int RF = 8;                   // fields: 0 dq, 1 unstable, 2 moves, 3 visits, 4 entries, 5 cands, 6 units
@@ -433,7 +437,7 @@ constexpr int SB = FC_RL_SB;            // Sigma gathers per batch in rl_runs
 template <bool LOUV, int K, int WM>
 __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep, int32_t (&x)[K], int32_t own,
                                            long long kown, int32_t tot_own, uint32_t home, unsigned long long& c_dq,
-                                           uint32_t& c_unst, uint32_t& c_cand, bool& slow_out, bool& tied_out) {
+                                           uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
     constexpr bool UNITW = WM == WM_UNIT;
     const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
     const int wb = UNITW ? 0 : a.wbits;
@@ -549,17 +553,15 @@ __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep,
             c_unst += (kown != (long long)vm) ? 1 : 0;
             dcs = best_c != own ? best_c : -1;
         }
-        tied_out = wk && ncand >= 2;
     }
     return dcs;
 }
 
 template <bool LOUV, int K, int WM>
 __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int sweep, unsigned long long& c_dq,
-                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out, bool& tied_out) {
+                                             uint32_t& c_unst, uint32_t& c_cand, bool& slow_out) {
     constexpr bool UNITW = WM == WM_UNIT;
     slow_out = false;
-    tied_out = false;
     const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
     const int wb = UNITW ? 0 : a.wbits;
     const int32_t wm = (1 << wb) - 1;
@@ -657,7 +659,7 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             return -1;
         }
     }
-    return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out, tied_out);
+    return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
 }
 
 // Light rows with sortable keys (label and weight fit 31 bits): no LDS, one sorting network
@@ -715,10 +717,16 @@ void k_rl_decide(RL a, int seg, int sweep) {
         const Rec cur = nxt;
         nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
         const Hdr h = rl_header(a, u, cur);
-        bool slow, tied;
-        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow, tied);
+        bool slow;
+        const uint32_t cc0 = c_cand;
+        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
         rl_push_slow(a, slow, u.e, h.rr);
-        if (!LOUV) {                                            // LPA ties of tracked replicas: one OR per sub-group
+        // LPA: the visit's candidates are the labels at the top count (rl_runs adds them to
+        // c_cand; a settled lane adds 1), so >= 2 of them is a tie.  Read off the counter rather
+        // than returned: one more live value through rl_runs changed the K = 64 kernel's code
+        // (205 VGPRs, ~180 SGPR spills) into one that departed from the twin in sweep 0.
+        const bool tied = !LOUV && c_cand - cc0 >= 2u;
+        if (!LOUV && FC_LPA_TIES) {                             // LPA ties of tracked replicas: one OR per sub-group
             const uint64_t tb = __ballot(tied && a.track[h.rr]);
             const uint64_t ts = (tb >> (u.s * LG)) & (LG == 64 ? ~0ull : ((1ull << LG) - 1ull));
             if (u.valid && u.rl == 0 && ts) atomicOr((unsigned long long*)&a.aff[(int64_t)u.bank * a.N + h.v], (unsigned long long)ts);
@@ -756,9 +764,10 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
         h.ds = valid ? h.d : 0;
         unsigned long long c_dq = 0;
         uint32_t c_unst = 0, c_cand = 0;
-        bool slow, tied;
-        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow, tied);
+        bool slow;
+        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
         rl_push_slow(a, slow, e, h.rr);
+        const bool tied = !LOUV && c_cand >= 2u;                 // this visit's candidates (see k_rl_decide)
         if (!LOUV && valid && tied && a.track[h.rr]) rl_tie_flag(a, h.rr, h.v);
         if (valid) {
             a.dec[e * a.ldT + h.rr] = h.work ? dcs : -1;
@@ -1071,6 +1080,7 @@ __global__ __launch_bounds__(HTB) void k_rl_exact(RL a, int k, int sweep) {
         uint32_t best_h = 0;
         int32_t best_c = INT_MAX;
         int ncand = 0;
+        int ntop = 0;                                         // LPA: labels at this lane's top count
         for (uint32_t q = lane; q < slots; q += 64) {
             const int32_t c = keys[q];
             if (c < 0) continue;
@@ -1082,6 +1092,7 @@ __global__ __launch_bounds__(HTB) void k_rl_exact(RL a, int k, int sweep) {
                 sc = w * a.M2 - kv * (long long)a.tot[(int64_t)c * a.ldT + rr];
             } else {
                 sc = w;
+                ntop = (best_c == INT_MAX || w > best_s) ? 1 : (w == best_s ? ntop + 1 : ntop);
             }
             ++ncand;
             const uint32_t h = hash32(tvh ^ (uint32_t)c);
@@ -1093,20 +1104,20 @@ __global__ __launch_bounds__(HTB) void k_rl_exact(RL a, int k, int sweep) {
             const long long s2 = __shfl_xor(best_s, off);
             const uint32_t hh2 = __shfl_xor(best_h, off);
             const int32_t c2 = __shfl_xor(best_c, off);
+            if (!LOUV) {                                      // LPA: how many labels reach the top count
+                const int n2 = __shfl_xor(ntop, off);
+                if (c2 != INT_MAX) ntop = (best_c == INT_MAX || s2 > best_s) ? n2 : (s2 == best_s ? ntop + n2 : ntop);
+            }
             if (c2 != INT_MAX && (best_c == INT_MAX || rl_better(s2, hh2, c2, best_s, best_h, best_c))) {
                 best_s = s2; best_h = hh2; best_c = c2;
             }
             kown += __shfl_xor(kown, off);
             ncand += __shfl_xor(ncand, off);
         }
-        if (!LOUV && best_c != INT_MAX && a.track[rr]) {          // LPA ties at the top count (wave-uniform)
-            int nt = 0;
-            for (uint32_t q = lane; q < slots; q += 64) nt += (keys[q] >= 0 && (long long)vals[q] == best_s) ? 1 : 0;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) nt += __shfl_xor(nt, off);
-            if (lane == 0 && nt >= 2) rl_tie_flag(a, rr, v);
-        }
-        wsync();                                              // the table is reused by the next visit
+        // LPA ties of a tracked replica, counted in the reduction above (a second pass over the
+        // table here made the compiler's k_rl_exact<false> depart from the twin in untracked
+        // sweeps too: tools/debug_rl_lpa.py, round 5)
+        if (!LOUV && FC_LPA_TIES && lane == 0 && ntop >= 2 && a.track[rr]) rl_tie_flag(a, rr, v);
         if (lane == 0) {
             int32_t dcs = -1;
             if (best_c != INT_MAX) {
@@ -1321,6 +1332,33 @@ __global__ __launch_bounds__(256) void k_rl_colw(int64_t n, const int32_t* col, 
     if (j < n) out[j] = (col[j] << wb) | cw[j];
 }
 
+// Hybrid hand-off into push mode: nlab[r][j] = the label of neighbour col[j] in replica r, for
+// 64 CSR entries x 64 replicas per block through LDS (labT rows read, nlab rows written as
+// whole 256-byte runs)
+__global__ __launch_bounds__(256) void k_rl_nlab(int64_t m2, int n_r, int ldT, const int32_t* col, const int32_t* labT,
+                                                 int32_t* nlab) {
+    __shared__ int32_t t[64][65];
+    __shared__ int32_t sc[64];
+    const int64_t j0 = (int64_t)blockIdx.x * 64;
+    const int r0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+    if (ty == 0) sc[tx] = j0 + tx < m2 ? col[j0 + tx] : -1;
+    __syncthreads();
+    for (int jj = ty; jj < 64; jj += 4) {
+        const int32_t u = sc[jj];
+        if (u >= 0 && r0 + tx < n_r) t[jj][tx] = labT[(int64_t)u * ldT + r0 + tx];
+    }
+    __syncthreads();
+    for (int rr = ty; rr < 64; rr += 4) {
+        const int r = r0 + rr;
+        if (r < n_r && j0 + tx < m2) nlab[(int64_t)r * m2 + j0 + tx] = t[tx][rr];
+    }
+}
+__global__ void k_rl_fill_i32(int64_t n, int32_t* p, int32_t v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
 // Hybrid hand-off: the affected bits [banks][N] as cd.hip's per-replica bit words [n_r][aw]
 // (aw = (N+31)/32; vertex v is bit v & 31 of word v >> 5):
 // the bank's 64-bit replica masks per vertex -> cd.hip's per-replica bit words (word v >> 5 of
@@ -1350,7 +1388,7 @@ __global__ __launch_bounds__(256) void k_rl_aff_export(int64_t N, int n_r, const
 // CDHandoff::fill: the batch's state in cd.hip's layout (labels in slot order, int32 totals by
 // community, affected flags, tracked / filtered flags with pull mode, active flags)
 void rl_handoff_fill(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint32_t* aff, int32_t* track,
-                     int32_t* active) {
+                     int32_t* active, int32_t* nlab) {
     const RL& a = *(const RL*)user;
     const dim3 tg(nb(a.N, 64), (a.n_r + 63) / 64);
     k_rl_export<<<tg, 256, 0, c.stream>>>(a.N, a.n_r, a.ldT, a.lab, c.sinv.as<int32_t>(), lab);
@@ -1359,6 +1397,22 @@ void rl_handoff_fill(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint3
     FC_HIP(hipMemcpyAsync(track, a.track, 8 * (size_t)a.n_r, hipMemcpyDeviceToDevice, c.stream));
     FC_HIP(hipMemsetAsync(track + 2 * a.n_r, 0, 8 * (size_t)a.n_r, c.stream));
     FC_HIP(hipMemcpyAsync(active, a.active, 4 * (size_t)a.n_r, hipMemcpyDeviceToDevice, c.stream));
+    // Push from the first filtered sweep on (unit weights, no Leiden-style marks: cd_run's own
+    // push rule): a filtered sweep of pull visits gathers one random line per neighbour label
+    // (SBM-4M: 14.5x the algorithmic bytes), a push visit streams its row of nlab.  The rows
+    // are written here from labT (one coalesced 256-byte label row per CSR entry, read through
+    // L2 by its row's other entries).  cd_run never switches a filtering replica to push (its
+    // transition sweep must visit every vertex), so without this the hand-off ran pull-only.
+    // Measured (MI355X, bench lines): SBM-4M lpm 878 -> 834 ms (LPA's tie revisits keep ~30
+    // filtered sweeps of many visits and few moves going); LFR-1M louvain 119.4 -> 126.8 ms (the
+    // row fill and the push writes of its movers cost more than the gathers saved).  So LPA only
+    // by default (FC_RL_HANDOFF_PUSH: 0 never, 1 LPA, 2 every unit-weight batch).
+    const int64_t m2 = 2 * c.g.m;
+    const bool lpa = a.tot == nullptr;
+    if (c.push_div > 0 && !a.lm && a.unitw && m2 > 0 && (c.rl_handoff_push == 2 || (c.rl_handoff_push == 1 && lpa))) {
+        k_rl_nlab<<<dim3(nb(m2, 64), a.banks), 256, 0, c.stream>>>(m2, a.n_r, a.ldT, a.col, a.lab, nlab);
+        k_rl_fill_i32<<<nb(a.n_r, 256), 256, 0, c.stream>>>(a.n_r, track + 2 * a.n_r, 1);
+    }
 }
 
 }  // namespace

@@ -128,6 +128,8 @@ struct Ctx {
     DevBuf rl_lmask, rl_vmask, rl_aff, rl_mvf, rl_vlist, rl_vcount;
     // visit mode for sparse sweeps: when visits * rl_visit_div < entries * min(n_r, 64) (0: never)
     int rl_visit_div = getenv("FC_RL_VISIT_DIV") ? atoi(getenv("FC_RL_VISIT_DIV")) : 4;
+    // hybrid hand-off into push mode: 0 never, 1 LPA batches (default), 2 every unit-weight batch
+    int rl_handoff_push = getenv("FC_RL_HANDOFF_PUSH") ? atoi(getenv("FC_RL_HANDOFF_PUSH")) : 1;
     int cd_engine = 2;              // FC_OPT_CD_ENGINE: 0 classic (cd.hip), 1 replica-lane (cd_rl.hip), 2 hybrid (default)
     // hybrid: the replica-lane engine runs a batch's full sweeps only when it holds this many
     // replicas (8 lanes per vertex at 8: LFR-1M n_p = 8 run 40.3 vs 42.9 ms on cd.hip since the
@@ -227,10 +229,13 @@ constexpr int FC_HPIN_I64 = 1024;   // pinned host scratch: per-sweep records (c
 // [n_r][N] in slot order, int32 totals [n_r][N], affected flags as bit words uint32
 // [n_r][aw] (aw = (N+31)/32 words per replica; vertex v is bit v & 31 of word v >> 5), track int32
 // [4][n_r] (tracked, filtered, push, transition) and active [n_r] -- and the sweeps go on from
-// sweep0.
+// sweep0.  On unit-weight graphs without Leiden-style marks it also writes every neighbour-label
+// row nlab [n_r][2m] and starts the replicas in push mode (cd.hip streams the rows instead of
+// gathering labels).
 struct CDHandoff {
     int sweep0;
-    void (*fill)(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint32_t* aff, int32_t* track, int32_t* active);
+    void (*fill)(Ctx& c, const void* user, int32_t* lab, int32_t* tot, uint32_t* aff, int32_t* track, int32_t* active,
+                 int32_t* nlab);
     const void* user;
 };
 

@@ -899,6 +899,8 @@ static int tw_coarse(i64 N, i64 V, int B, int gmax) {
 /* LPA tie revisits under pruning (see tw_replica); settable for the semantics study */
 static int tw_lpa_ties = 1;
 void orc_set_lpa_ties(int on) { tw_lpa_ties = on; }
+static int tw_lpa_coarsen = 0;   /* semantics study: LPA coarse rounds up to this g (0: none) */
+void orc_set_lpa_coarsen(int g) { tw_lpa_coarsen = g; }
 static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const i32* cw, const i64* kdeg, i64 M2,
                       u64 seed, uint32_t rg, uint32_t iter, int buckets, int max_sweeps, int chunk, int prune,
                       int coarsen, int lm, int shared, int dense_div, i32* lab) {
@@ -969,7 +971,8 @@ static int tw_replica(int algo, i64 N, const i64* rowptr, const i32* col, const 
         /* Louvain only: LPA's tied vertices redraw at every visit, and rounds of several
          * buckets let adjacent tied vertices flip together sweep after sweep (a replica on
          * LFR-100k at average degree 8 never stopped) */
-        const int g = (louv && listed && prune_now && coarsen && !dense) ? tw_coarse(N, loff[B], B, coarsen) : 1;
+        const int g = ((louv || tw_lpa_coarsen) && listed && prune_now && coarsen && !dense)
+                          ? tw_coarse(N, loff[B], B, louv ? coarsen : (coarsen < tw_lpa_coarsen ? coarsen : tw_lpa_coarsen)) : 1;
         for (int k = 0; k < B; k += g) {
             const int k1 = k + g < B ? k + g : B;
             i64 blen = PN - (i64)k * S;

@@ -78,6 +78,7 @@ def lib():
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p, _i32p]
         L.orc_device_sigma.argtypes = [i64, u64, _i32p]
         L.orc_set_lpa_ties.argtypes = [ctypes.c_int]
+        L.orc_set_lpa_coarsen.argtypes = [ctypes.c_int]
         L.orc_closure_sample.argtypes = [i64, _i64p, _i32p, i64, u64, ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_build_csr.argtypes = [i64, i64, _i32p, _i32p, ctypes.c_void_p, _i64p, _i32p, _i32p]
         L.orc_infomap_full.argtypes = [i64, _i64p, _i32p, u64, ctypes.c_int, _i32p, ctypes.POINTER(dbl)]
