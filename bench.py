@@ -445,10 +445,9 @@ def main():
         dom = max(kern, key=lambda k: kern[k]["ms_per_step"]) if kern else "k_decide_light"
         kd = kern.get(dom, {"launches": 0, "avg_us": 0.0, "algorithmic_bytes_per_launch": 0.0, "achieved": 0.0})
         avg_s = kd["avg_us"] / 1e6
-        if args.n_p <= 0:
-            traffic, traffic_note = load_traffic(args.config, dom)
-        else:
-            traffic, traffic_note = None, "the PMC summary is for the config's n_p"
+        # a line run with --n-p n reads the profile taken at that n_p (tools/pmc_bench.sh, FC_PMC_NP)
+        traffic, traffic_note = load_traffic(args.config if args.n_p <= 0 else "%s_np%d" % (args.config, args.n_p),
+                                             dom)
         roof = {"bound": "hbm", "achieved": kd["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": kd["achieved"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": traffic_note,
                 "kernel": "%s<%s>" % (dom, "true" if algo != 1 else "false"),

@@ -21,7 +21,7 @@ def main():
     busy, gaps, host, per = 0, defaultdict(int), 0, defaultdict(lambda: [0, 0])
     end = ks[0][0]
     for s, e, name in ks:
-        short = name.split("(")[0].replace("void ", "")
+        short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         short = short.split("<")[0] + ("<" + short.split("<", 1)[1] if "<" in short else "")
         per[short[:70]][0] += e - s
         per[short[:70]][1] += 1
@@ -41,7 +41,7 @@ def main():
     for b in ("<2us", "2-5us", "5-10us", "10-50us", ">50us"):
         print("  gaps %-8s %.2f ms" % (b, gaps[b] / 1e6))
     print("host phases (gaps > %.1f ms): %.1f ms" % (args.host_ms, host / 1e6))
-    for name, (t, c) in sorted(per.items(), key=lambda x: -x[1][0])[:15]:
+    for name, (t, c) in sorted(per.items(), key=lambda x: -x[1][0])[:30]:
         print("  %8.2f ms %6d  %s" % (t / 1e6, c, name))
 
 
