@@ -32,6 +32,7 @@
 
 #include "fc_ctx.h"
 #include "fc_device.h"
+#include "fc_log2.h"
 
 namespace fc {
 
@@ -93,6 +94,8 @@ struct LvArgs {
     unsigned long long* moves;   // [MSH]
     unsigned long long* rmoves;  // Infomap: [n_r] moves of each replica in this pass
     const uint8_t* lvdone;       // Infomap: [n_r] replica's passes at this level are over (a pass moved nothing)
+    const int32_t* ilist;        // Infomap: this bucket's vertices, compacted once per pass (k_info_lfill);
+    int64_t icnt;                //   nullptr: every launch scans the union for its bucket (bmap below)
     const int32_t* bmap;         // Infomap, input-graph level: launch only the replicas still moving --
     int bpr;                     //   block b covers replica bmap[b / bpr], ids (b % bpr)*LTB.. of it
     int nact;                    //   replicas in bmap
@@ -126,6 +129,12 @@ template <int MODE> __device__ __forceinline__ int lv_entry_bytes(bool weighted)
 template <int MODE> __device__ __forceinline__ constexpr int lv_cand_bytes() { return MODE == MODE_INFO ? 16 : 8; }
 
 __device__ __forceinline__ double plogp2(double p) { return p > 0.0 ? p * log2(p) : 0.0; }
+// The decisions' terms use fc_log2 (~2 ulp, ~20 instructions, table in LDS) instead of the
+// library's log2 (~0.5 ulp, 89 instructions): the map-equation deltas are sums of these terms
+// compared against each other and against -1e-10, so ~1e-16 of error per term only matters for
+// candidates within ~1e-15 of each other.  Reported codelengths (k_info_codelen) keep log2.
+__constant__ Log2Entry c_log2[49] = FC_LOG2_TABLE;
+__device__ __forceinline__ double plogp2f(double p, const Log2Entry* lt) { return p > 0.0 ? p * fc_log2(p, lt) : 0.0; }
 // The map-equation change split into the part of the source module A (computed once per
 // vertex) and the per-candidate part (module B and the total exit Q'), 5 logarithms each.
 struct InfoA {
@@ -134,20 +143,21 @@ struct InfoA {
     double q0;        // plogp(Q)
 };
 __device__ __forceinline__ InfoA info_a(double inv, long long Q, long long oA, long long tA, long long kv, long long sv,
-                                        long long wA) {
+                                        long long wA, const Log2Entry* lt) {
     InfoA r;
     const long long oA2 = oA - sv + 2 * wA, tA2 = tA - kv;
     r.dA = oA2 - oA;
-    r.termA = -2.0 * (plogp2(oA2 * inv) - plogp2(oA * inv)) + (plogp2((oA2 + tA2) * inv) - plogp2((oA + tA) * inv));
-    r.q0 = plogp2(Q * inv);
+    r.termA = -2.0 * (plogp2f(oA2 * inv, lt) - plogp2f(oA * inv, lt)) +
+              (plogp2f((oA2 + tA2) * inv, lt) - plogp2f((oA + tA) * inv, lt));
+    r.q0 = plogp2f(Q * inv, lt);
     return r;
 }
 __device__ __forceinline__ double info_b(double inv, const InfoA& A, long long Q, long long oB, long long tB,
-                                         long long kv, long long sv, long long wB) {
+                                         long long kv, long long sv, long long wB, const Log2Entry* lt) {
     const long long oB2 = oB + sv - 2 * wB, tB2 = tB + kv;
     const long long Q2 = Q + A.dA + (oB2 - oB);
-    return (plogp2(Q2 * inv) - A.q0) + A.termA - 2.0 * (plogp2(oB2 * inv) - plogp2(oB * inv)) +
-           (plogp2((oB2 + tB2) * inv) - plogp2((oB + tB) * inv));
+    return (plogp2f(Q2 * inv, lt) - A.q0) + A.termA - 2.0 * (plogp2f(oB2 * inv, lt) - plogp2f(oB * inv, lt)) +
+           (plogp2f((oB2 + tB2) * inv, lt) - plogp2f((oB + tB) * inv, lt));
 }
 // smaller delta, then larger tie hash, then smaller id; c < 0 = none
 __device__ __forceinline__ bool info_better(double d1, uint32_t h1, int32_t c1, double d2, uint32_t h2, int32_t c2) {
@@ -168,9 +178,12 @@ template <bool IMPL> __device__ __forceinline__ int64_t kv_of(const LvArgs& a, i
 template <bool IMPL> __device__ __forceinline__ int64_t sv_of(const LvArgs& a, int64_t x) {
     return IMPL ? a.sv[x % a.N0] : a.sv[x];
 }
-__device__ __forceinline__ bool in_bucket(const LvArgs& a, int32_t r, int64_t x, int bucket) {
+__device__ __forceinline__ int bucket_of(const LvArgs& a, int32_t r, int64_t x) {
     const uint32_t xl = (uint32_t)(x - a.roff[r]);
-    return (int)(hash32(a.rkey[r] ^ hash32(xl)) % (uint32_t)a.B) == bucket;
+    return (int)(hash32(a.rkey[r] ^ hash32(xl)) % (uint32_t)a.B);
+}
+__device__ __forceinline__ bool in_bucket(const LvArgs& a, int32_t r, int64_t x, int bucket) {
+    return bucket_of(a, r, x) == bucket;
 }
 __device__ __forceinline__ uint32_t tie_of(const LvArgs& a, int32_t r, int64_t x, int32_t c) {
     return hash32(hash32(a.rkey[r] ^ 0x5bd1e995u ^ (uint32_t)(x - a.roff[r])) ^ (uint32_t)(c - a.roff[r]));
@@ -185,38 +198,45 @@ __device__ __forceinline__ bool lv_better(long long s1, uint32_t h1, int32_t c1,
 }
 // Infomap candidate scan over table slots [0, ts) by a group of GL lanes (a power of two
 // dividing 64, aligned): the most negative delta-L, reduced inside the group
+__device__ __forceinline__ void wsync();
+// The group's candidates (occupied slots other than the own module) are first compacted to the
+// front of its table, in place (a slot's compacted index never exceeds it, and a pass reads its
+// GL slots before any lane writes), so the map-equation terms -- five double logarithms per
+// candidate, ~450 VALU instructions -- run on full lanes: a 64-slot table of a 27-entry row held
+// ~10-27 candidates, and every lane paid for the slots of the busiest one.  The best candidate
+// is a total order (delta, tie hash, id), so the evaluation order does not change it.
 template <int GL = 64>
-__device__ __forceinline__ void wave_scan_info(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
+__device__ __forceinline__ void wave_scan_info(const LvArgs& a, int32_t* keys, int32_t* vals, uint32_t ts,
                                                int32_t own, long long kvx, long long svx, long long wown, int32_t r,
                                                int64_t x, double& bd, uint32_t& bh, int32_t& bc, int32_t& bw,
-                                               int& ncand) {
-    const int gl = threadIdx.x & (GL - 1);
+                                               int& ncand, const Log2Entry* lt) {
+    const int lane = threadIdx.x & 63, gl = lane & (GL - 1);
     bd = 0.0; bh = 0; bc = -1; bw = 0;
     const long long Q = a.qrep[r];
     const longlong2 mo = *(const longlong2*)(a.mod + 2 * (int64_t)own);
-    const InfoA A = info_a(a.inv, Q, mo.y, mo.x, kvx, svx, wown);
-    constexpr int UNR = 1;
-    for (uint32_t s0 = gl; s0 < ts; s0 += GL * UNR) {
-        int32_t k[UNR], v[UNR];
-        longlong2 mk[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t s = s0 + u * GL;
-            k[u] = s < ts ? keys[s] : -1;
-            v[u] = s < ts ? vals[s] : 0;
-            if (k[u] == own) k[u] = -1;
+    const InfoA A = info_a(a.inv, Q, mo.y, mo.x, kvx, svx, wown, lt);
+    const unsigned long long gmask = GL == 64 ? ~0ull : (((1ull << GL) - 1) << (lane & ~(GL - 1)));
+    const unsigned long long below = gmask & ((1ull << lane) - 1);
+    uint32_t n = 0;
+    for (uint32_t s0 = 0; s0 < ts; s0 += GL) {   // ts: a power of two >= 64 >= GL
+        const int32_t k = keys[s0 + gl], v = vals[s0 + gl];
+        const bool ok = k >= 0 && k != own;
+        const unsigned long long b = __ballot(ok) & gmask;
+        if (ok) {
+            const uint32_t p = n + (uint32_t)__popcll(b & below);
+            keys[p] = k;
+            vals[p] = v;
         }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-            mk[u] = k[u] >= 0 ? *(const longlong2*)(a.mod + 2 * (int64_t)k[u]) : make_longlong2(0, 0);   // flow, exit
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            if (k[u] < 0) continue;
-            ++ncand;
-            const double d = info_b(a.inv, A, Q, mk[u].y, mk[u].x, kvx, svx, v[u]);
-            const uint32_t h = tie_of(a, r, x, k[u]);
-            if (info_better(d, h, k[u], bd, bh, bc)) { bd = d; bh = h; bc = k[u]; bw = v[u]; }
-        }
+        n += (uint32_t)__popcll(b);
+    }
+    wsync();
+    for (uint32_t ci = gl; ci < n; ci += GL) {
+        const int32_t k = keys[ci], v = vals[ci];
+        const longlong2 mk = *(const longlong2*)(a.mod + 2 * (int64_t)k);   // flow, exit
+        ++ncand;
+        const double d = info_b(a.inv, A, Q, mk.y, mk.x, kvx, svx, v, lt);
+        const uint32_t h = tie_of(a, r, x, k);
+        if (info_better(d, h, k, bd, bh, bc)) { bd = d; bh = h; bc = k; bw = v; }
     }
     for (int off = GL / 2; off; off >>= 1) {
         const double d2 = __shfl_xor(bd, off);
@@ -355,8 +375,10 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     __shared__ int32_t skey[LTB / 64][TS], sval[LTB / 64][TS];
     __shared__ int s_cnt;
     __shared__ uint32_t s_bytes;
+    __shared__ Log2Entry s_lt[MODE == MODE_INFO ? 49 : 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x == 0) { s_cnt = 0; s_bytes = 0; }
+    if (MODE == MODE_INFO && threadIdx.x < 49) s_lt[threadIdx.x] = c_log2[threadIdx.x];
     __syncthreads();
     // this lane's share of the algorithmic bytes (scanned / decided vertices, movers, entries,
     // candidates), ONE accumulator: five counters cost the Infomap instance an occupancy step
@@ -364,12 +386,19 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     uint32_t c_b = 0;
     const uint32_t eb = (uint32_t)lv_entry_bytes<MODE>(a.w != nullptr);
     int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
-    if (IMPL && a.bmap) {
+    const bool listed = MODE == MODE_INFO && a.ilist != nullptr;
+    if (listed) {
+        x0 = x0 < a.icnt ? (int64_t)a.ilist[x0] : a.nU;
+    } else if (IMPL && a.bmap) {
         const int64_t loc = (int64_t)(blockIdx.x % a.bpr) * LTB + threadIdx.x;
         x0 = loc < a.N0 ? (int64_t)a.bmap[blockIdx.x / a.bpr] * a.N0 + loc : a.nU;
     }
     bool elig = false;
-    if (x0 < a.nU) {
+    if (listed) {
+        // the pass list holds exactly this bucket's vertices of the replicas still moving
+        elig = x0 < a.nU;
+        c_b = elig ? 4u : 0u;
+    } else if (x0 < a.nU) {
         // the eligibility scan: replica id (explicit levels), queue flag / refined size
         c_b = (IMPL ? 0 : 4) + (MODE == MODE_MOVE ? 1 : MODE == MODE_REFINE ? 8 : 0);
         const int32_t r = rep_of<IMPL>(a, x0);
@@ -443,7 +472,8 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
             wown = wl;
             double bd = 0.0;
             if (valid) {
-                wave_scan_info<GL>(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rx, x, bd, bh, bc, bw, ncand);
+                wave_scan_info<GL>(a, keys, vals, ts, own, kvx, sv_of<IMPL>(a, x), wown, rx, x, bd, bh, bc, bw, ncand,
+                                   s_lt);
             } else {
                 bc = -1;
             }
@@ -541,6 +571,8 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
     __shared__ long long s_wown;
     __shared__ BRed red;
     __shared__ BRedI redi;
+    __shared__ Log2Entry s_lt[MODE == MODE_INFO ? 49 : 1];
+    if (MODE == MODE_INFO && threadIdx.x < 49) s_lt[threadIdx.x] = c_log2[threadIdx.x];   // (synced below)
     const int n = a.heavy_cnt[tier];
     const int32_t* hlist = a.heavy + tier * a.hcap;
     int32_t* htgt = a.htgt + tier * a.hcap;
@@ -581,7 +613,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
         InfoA IA{};
         if (MODE == MODE_INFO) {
             const longlong2 mo = *(const longlong2*)(a.mod + 2 * (int64_t)own);
-            IA = info_a(a.inv, a.qrep[r], mo.y, mo.x, kvx, sv_of<IMPL>(a, x), wown);
+            IA = info_a(a.inv, a.qrep[r], mo.y, mo.x, kvx, sv_of<IMPL>(a, x), wown, s_lt);
         }
         const long long qr = MODE == MODE_INFO ? a.qrep[r] : 0;
         const long long svx = MODE == MODE_INFO ? sv_of<IMPL>(a, x) : 0;
@@ -616,7 +648,7 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
                 c_b += (uint32_t)lv_cand_bytes<MODE>();
                 const uint32_t h = tie_of(a, r, x, k[u]);
                 if (MODE == MODE_INFO) {
-                    const double d = info_b(a.inv, IA, qr, tk2[u], tk[u], kvx, svx, val[u]);
+                    const double d = info_b(a.inv, IA, qr, tk2[u], tk[u], kvx, svx, val[u], s_lt);
                     if (info_better(d, h, k[u], bd, bh, bc)) { bd = d; bh = h; bc = k[u]; bw = (int32_t)val[u]; }
                 } else {
                     const long long sc = val[u] * a.M2 - kvx * tk[u];
@@ -655,9 +687,11 @@ __global__ __launch_bounds__(LTB) void k_lv_heavy(LvArgs a, uint32_t stamp, int 
 // community at the END of the bucket differs from the target (a neighbour that moves in
 // this bucket is judged by its stamped target, the others by P, which this bucket leaves
 // alone), so the queue flags do not depend on thread timing.
-template <bool IMPL, int MODE>
+// GL lanes per mover (a power of two dividing 64): lane 0 of the group moves the vertex, the
+// group walks its row.
+template <bool IMPL, int MODE, int GL = 64>
 __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, uint32_t stamp, unsigned long long& mv) {
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & (GL - 1);
     if (lane == 0) {
         const long long kvx = kv_of<IMPL>(a, x);
         int32_t* lab = MODE == MODE_REFINE ? a.R : a.P;
@@ -683,7 +717,7 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
         const int32_t xo = a.mvo[x];
         const int64_t re = a.rowptr[xr + 1];
         long long dq = 0;
-        for (int64_t j = a.rowptr[xr] + lane; j < re; j += 64) {
+        for (int64_t j = a.rowptr[xr] + lane; j < re; j += GL) {
             const int64_t y = base + a.col[j];
             const long long w = a.w ? a.w[j] : 1;
             const unsigned long long my = a.mvt[y];
@@ -710,14 +744,14 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
             for (int k = 0; k < nm; ++k)
                 if (d[k]) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)m[k] + 1], (unsigned long long)d[k]);
         }
-        for (int off = 32; off; off >>= 1) dq += __shfl_xor(dq, off);
+        for (int off = GL / 2; off; off >>= 1) dq += __shfl_xor(dq, off);
         if (lane == 0 && dq) atomicAdd((unsigned long long*)&a.qrep[rep_of<IMPL>(a, x)], (unsigned long long)dq);
     }
     if (MODE == MODE_MOVE) {
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
         const int64_t re = a.rowptr[xr + 1];
-        for (int64_t j = a.rowptr[xr] + lane; j < re; j += 64) {
+        for (int64_t j = a.rowptr[xr] + lane; j < re; j += GL) {
             const int64_t y = base + a.col[j];
             const unsigned long long my = a.mvt[y];
             const int32_t fin = (uint32_t)(my >> 32) == stamp ? (int32_t)(uint32_t)my : a.P[y];
@@ -735,22 +769,29 @@ __global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk, 
     int32_t r0 = 0;
     if (MODE == MODE_INFO) {
         if (threadIdx.x < 2) s_rm[threadIdx.x] = 0;
-        if ((int)blockIdx.x < nblk)
-            r0 = (IMPL && a.bmap) ? a.bmap[blockIdx.x / a.bpr] : rep_of<IMPL>(a, (int64_t)blockIdx.x * LTB);
+        if ((int)blockIdx.x < nblk) {
+            if (a.ilist)   // a list block's vertices: mostly one replica, that of its first mover
+                r0 = a.bcnt[blockIdx.x] ? rep_of<IMPL>(a, a.blist[(int64_t)blockIdx.x * LTB]) : 0;
+            else
+                r0 = (IMPL && a.bmap) ? a.bmap[blockIdx.x / a.bpr] : rep_of<IMPL>(a, (int64_t)blockIdx.x * LTB);
+        }
         __syncthreads();
     }
-    auto count_rep = [&](int64_t x) {
-        if (MODE != MODE_INFO || lane != 0) return;
+    auto count_rep = [&](int64_t x, int gl) {
+        if (MODE != MODE_INFO || gl != 0) return;
         const int32_t r = rep_of<IMPL>(a, x);
-        if ((int)blockIdx.x < nblk && r - r0 < 2) atomicAdd(&s_rm[r - r0], 1ull);
+        if ((int)blockIdx.x < nblk && (uint32_t)(r - r0) < 2u) atomicAdd(&s_rm[r - r0], 1ull);
         else atomicAdd(&a.rmoves[r], 1ull);
     };
     if ((int)blockIdx.x < nblk) {
+        // Infomap's input-graph level: 16 lanes per mover (rows of ~27 entries; a wave per mover
+        // left most lanes idle through each row's chain of dependent gathers and atomics)
+        constexpr int AG = (MODE == MODE_INFO && IMPL) ? 16 : 64;
         const int n = a.bcnt[blockIdx.x];
-        for (int i = wv; i < n; i += LTB / 64) {
+        for (int i = wv * (64 / AG) + lane / AG; i < n; i += (LTB / 64) * (64 / AG)) {
             const int64_t q = (int64_t)blockIdx.x * LTB + i;
-            lv_move<IMPL, MODE>(a, a.blist[q], a.btgt[q], stamp, mv);
-            count_rep(a.blist[q]);
+            lv_move<IMPL, MODE, AG>(a, a.blist[q], a.btgt[q], stamp, mv);
+            count_rep(a.blist[q], lane & (AG - 1));
         }
     } else {
         for (int tier = 0; tier < NTIER; ++tier) {
@@ -761,12 +802,12 @@ __global__ __launch_bounds__(LTB) void k_lv_apply(LvArgs a, int nblk, int hblk, 
                 const int32_t t = ht[i];
                 if (t >= 0) {
                     lv_move<IMPL, MODE>(a, hl[i], t, stamp, mv);
-                    count_rep(hl[i]);
+                    count_rep(hl[i], lane);
                 }
             }
         }
     }
-    if (lane == 0 && mv) atomicAdd(&a.moves[blockIdx.x & (MSH - 1)], mv);
+    if (mv) atomicAdd(&a.moves[blockIdx.x & (MSH - 1)], mv);   // group leaders only
     if (MODE == MODE_INFO) {
         __syncthreads();
         if (threadIdx.x < 2 && s_rm[threadIdx.x]) atomicAdd(&a.rmoves[r0 + threadIdx.x], s_rm[threadIdx.x]);
@@ -1051,11 +1092,55 @@ __global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const 
     if (threadIdx.x == 0) cl[r] = plogp2(qrep[r] * inv) + sm[0];
 }
 
+// Infomap pass lists: every eligible vertex (replica neither finished nor done at this level)
+// into the list of its bucket, once per pass.  Scanning the union in every bucket launch cost B
+// scans per pass, and a wave then held ~64/B vertices of its bucket; a listed wave holds 64.
+// Decisions within a bucket are pure functions of the state before it and the apply's updates
+// are integer atomics, so the order inside a list does not change any result.
+constexpr int ILIST_MAXB = 1024;
+template <bool IMPL>
+__global__ __launch_bounds__(LTB) void k_info_lcount(LvArgs a, int32_t* cnt) {
+    __shared__ int32_t h[ILIST_MAXB];
+    for (int i = threadIdx.x; i < a.B; i += LTB) h[i] = 0;
+    __syncthreads();
+    const int64_t x = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    if (x < a.nU) {
+        const int32_t r = rep_of<IMPL>(a, x);
+        if (!a.done[r] && !a.lvdone[r]) atomicAdd(&h[bucket_of(a, r, x)], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.B; i += LTB)
+        if (h[i]) atomicAdd(&cnt[i], h[i]);
+}
+// cnt: the counts (read), cur: per-bucket cursors (zeroed), list: [sum cnt] bucket-major
+template <bool IMPL>
+__global__ __launch_bounds__(LTB) void k_info_lfill(LvArgs a, const int32_t* cnt, int32_t* cur, int32_t* list) {
+    __shared__ int32_t off[ILIST_MAXB], h[ILIST_MAXB];
+    if (threadIdx.x == 0) {   // B is small (32 by default): one thread scans the counts
+        int32_t s = 0;
+        for (int i = 0; i < a.B; ++i) { off[i] = s; s += cnt[i]; }
+    }
+    for (int i = threadIdx.x; i < a.B; i += LTB) h[i] = 0;
+    __syncthreads();
+    const int64_t x = (int64_t)blockIdx.x * LTB + threadIdx.x;
+    int b = -1, pos = 0;
+    if (x < a.nU) {
+        const int32_t r = rep_of<IMPL>(a, x);
+        if (!a.done[r] && !a.lvdone[r]) { b = bucket_of(a, r, x); pos = atomicAdd(&h[b], 1); }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.B; i += LTB)
+        if (h[i]) h[i] = atomicAdd(&cur[i], h[i]);   // the block's base in bucket i
+    __syncthreads();
+    if (b >= 0) list[off[b] + h[b] + pos] = (int32_t)x;
+}
+
 // Buffers (Ctx::lv).
 enum {
     B_P, B_R, B_RTOT, B_RSIZE, B_PTOT, B_ACT, B_BLIST, B_BTGT, B_BCNT, B_HEAVY, B_HCNT, B_HTGT, B_HKEY, B_HVAL,
     B_HLST, B_MOVES, B_MEMB, B_NID, B_ROFF, B_REND, B_DONE, B_RKEY, B_MISC, B_MVT,
     B_POUT, B_DEG, B_QREP, B_CL, B_BWA, B_BWB, B_HWA, B_HWB, B_TLAB, B_LVDONE, B_RMOVES, B_BMAP, B_LVB,
+    B_ILC, B_ILL,   // Infomap pass lists: counts | cursors, the list
     // aggregation scratch
     B_FL, B_MCNT, B_MOFF, B_UB, B_UBO, B_MCUR, B_MLIST, B_TCOL, B_TW, B_OLEN, B_AGH, B_LEN64,
     // explicit level graphs, ping-pong: rowptr, col, w, kv, rep, sv (x2)
@@ -1258,13 +1343,44 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     };
 
     // one bucketed sweep; returns moves
+    // Infomap passes: compacted bucket lists (FC_INFO_LISTS=0: every bucket launch scans the union)
+    static const bool info_lists = !getenv("FC_INFO_LISTS") || atoi(getenv("FC_INFO_LISTS")) != 0;
+    // rows of 65..128 entries: two vertices per wave (256 slots each), not one per wave
+    static const bool lv_g2 = !getenv("FC_LV_G2") || atoi(getenv("FC_LV_G2")) != 0;
+    std::vector<int32_t> h_icnt;
     auto sweep = [&](int MODE, int level, int sw) -> unsigned long long {
         set_keys(level, sw, (uint32_t)MODE);
         FC_HIP(hipMemsetAsync(moves, 0, 8 * MSH, c.stream));
-        const int nblk = a.bmap ? a.bpr * a.nact : (int)nb(nU);
+        int nblk = a.bmap ? a.bpr * a.nact : (int)nb(nU);
         const int hg = heavy_grid(a.hslots);
         const int hblk = 64;
+        // Infomap: the pass's bucket lists (one host read of the B counts per pass)
+        const bool listed = MODE == MODE_INFO && info_lists && a.B <= ILIST_MAXB;
+        int32_t* ill = nullptr;
+        a.ilist = nullptr;
+        if (listed) {
+            int32_t* ilc = I32(B_ILC, 2 * (int64_t)a.B);
+            ill = I32(B_ILL, nU);
+            FC_HIP(hipMemsetAsync(ilc, 0, 8 * (size_t)a.B, c.stream));
+            if (impl) {
+                k_info_lcount<true><<<nb(nU), LTB, 0, c.stream>>>(a, ilc);
+                k_info_lfill<true><<<nb(nU), LTB, 0, c.stream>>>(a, ilc, ilc + a.B, ill);
+            } else {
+                k_info_lcount<false><<<nb(nU), LTB, 0, c.stream>>>(a, ilc);
+                k_info_lfill<false><<<nb(nU), LTB, 0, c.stream>>>(a, ilc, ilc + a.B, ill);
+            }
+            h_icnt.resize(a.B);
+            FC_HIP(hipMemcpyAsync(h_icnt.data(), ilc, 4 * (size_t)a.B, hipMemcpyDeviceToHost, c.stream));
+            sync(c);
+        }
+        int64_t ioff = 0;
         for (int b = 0; b < a.B; ++b) {
+            if (listed) {
+                a.ilist = ill + ioff;
+                a.icnt = h_icnt[b];
+                ioff += h_icnt[b];
+                nblk = (int)nb(a.icnt);
+            }
             const uint32_t stamp = ++stamp_ctr;   // unique per bucket launch of this run (mvt)
             FC_HIP(hipMemsetAsync(hcnt, 0, 4 * NTIER, c.stream));
             // (timed per launch into spans 5 / 6 when timing is on: lv decide / lv heavy)
@@ -1272,6 +1388,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
     do {                                                                                         \
         const int t5 = timer_begin(c);                                                           \
         if (max_deg <= 64) k_lv_decide<IM, MD, 512, 4><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);  \
+        else if (max_deg <= 128 && lv_g2) k_lv_decide<IM, MD, 512, 2><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
         else if (max_deg <= LWS_SMALL / 2) k_lv_decide<IM, MD, LWS_SMALL, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp); \
         else k_lv_decide<IM, MD, LWS, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);               \
         timer_end(c, 5, t5);                                                                     \
@@ -1293,6 +1410,7 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             else LV_LAUNCH(false, MODE_INFO);
 #undef LV_LAUNCH
         }
+        a.ilist = nullptr;
         std::vector<unsigned long long> hm(MSH);
         FC_HIP(hipMemcpyAsync(hm.data(), moves, 8 * MSH, hipMemcpyDeviceToHost, c.stream));
         sync(c);
@@ -1322,7 +1440,14 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
             for (int sw = 0; sw < c.max_sweeps; ++sw) {
                 ++lv_sweeps;
                 FC_HIP(hipMemsetAsync(rmv, 0, 8 * (size_t)n_r, c.stream));
+                if (c.trace && sw == 0) { sync(c); trace_dt_us(true); }
                 const unsigned long long mvs = sweep(MODE_INFO, level, sw);   // syncs
+                if (c.trace) {
+                    int na = 0;
+                    for (int r = 0; r < n_r; ++r) na += !h_lvd[r];
+                    fprintf(stderr, "[fc] infomap level %d pass %d: %d replicas, %llu moves, %.0f us\n", level, sw, na,
+                            mvs, trace_dt_us(false));
+                }
                 if (mvs == 0) break;
                 FC_HIP(hipMemcpy(h_rmv.data(), rmv, 8 * (size_t)n_r, hipMemcpyDeviceToHost));
                 for (int r = 0; r < n_r; ++r) h_lvd[r] |= h_rmv[r] == 0;
