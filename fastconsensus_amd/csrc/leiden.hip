@@ -716,7 +716,7 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
         const int64_t xr = IMPL ? x - base : x;
         const int32_t xo = a.mvo[x];
         const int64_t re = a.rowptr[xr + 1];
-        long long dq = 0;
+        long long dq = 0, sxo = 0, st = 0;   // this lane's deltas of xo's and t's exits
         for (int64_t j = a.rowptr[xr] + lane; j < re; j += GL) {
             const int64_t y = base + a.col[j];
             const long long w = a.w ? a.w[j] : 1;
@@ -729,23 +729,28 @@ __device__ __forceinline__ void lv_move(const LvArgs& a, int64_t x, int32_t t, u
             } else {
                 yo = yn = a.P[y];
             }
-            // (module, delta) pairs: -w at xo and yo if the edge was cut, +w at t and yn if it is;
-            // a module on both sides cancels (y staying in a third module: 2 atomics, not 4)
-            int32_t m[4];
-            long long d[4];
-            int nm = 0;
-            auto add = [&](int32_t mod, long long dv) {
-                for (int k = 0; k < nm; ++k)
-                    if (m[k] == mod) { d[k] += dv; return; }
-                m[nm] = mod; d[nm] = dv; ++nm;
-            };
-            if (xo != yo) { add(xo, -w); add(yo, -w); dq -= 2 * w; }
-            if (t != yn) { add(t, w); add(yn, w); dq += 2 * w; }
-            for (int k = 0; k < nm; ++k)
-                if (d[k]) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)m[k] + 1], (unsigned long long)d[k]);
+            // -w at xo and yo if the edge was cut, +w at t and yn if it is.  xo's and t's deltas
+            // are summed over the row (two atomics per mover); y's modules take an atomic only when
+            // they are neither (a neighbour staying in a third module: none, its -w and +w cancel)
+            long long dyo = 0, dyn = 0;
+            if (xo != yo) { sxo -= w; dyo -= w; dq -= 2 * w; }
+            if (t != yn) { st += w; dyn += w; dq += 2 * w; }
+            if (yo == yn) { dyo += dyn; dyn = 0; }
+            if (yo == xo) { sxo += dyo; dyo = 0; } else if (yo == t) { st += dyo; dyo = 0; }
+            if (yn == xo) { sxo += dyn; dyn = 0; } else if (yn == t) { st += dyn; dyn = 0; }
+            if (dyo) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)yo + 1], (unsigned long long)dyo);
+            if (dyn) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)yn + 1], (unsigned long long)dyn);
         }
-        for (int off = GL / 2; off; off >>= 1) dq += __shfl_xor(dq, off);
-        if (lane == 0 && dq) atomicAdd((unsigned long long*)&a.qrep[rep_of<IMPL>(a, x)], (unsigned long long)dq);
+        for (int off = GL / 2; off; off >>= 1) {
+            dq += __shfl_xor(dq, off);
+            sxo += __shfl_xor(sxo, off);
+            st += __shfl_xor(st, off);
+        }
+        if (lane == 0) {
+            if (sxo) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)xo + 1], (unsigned long long)sxo);
+            if (st) atomicAdd((unsigned long long*)&a.mod[2 * (int64_t)t + 1], (unsigned long long)st);
+            if (dq) atomicAdd((unsigned long long*)&a.qrep[rep_of<IMPL>(a, x)], (unsigned long long)dq);
+        }
     }
     if (MODE == MODE_MOVE) {
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
