@@ -1220,20 +1220,21 @@ __global__ __launch_bounds__(NTH) void k_cd_tail(CDArgs a, int sweep0, int max_s
 // moves commute (distinct vertices, integer atomics), so entries land in any order.
 // Pass 1 counts the flagged vertices per bucket, the plan sizes the rounds, pass 2 fills the
 // per-replica lists [n_r][PN] and clears the flags.  Dynamic LDS: 2 * B ints.
-static constexpr int LB_PER = 16;        // vertices per thread in k_list_count / k_list_fill
 __device__ __forceinline__ uint32_t vertex_bucket(const CDArgs& a, const Perm& P, uint32_t v) {
     const uint32_t pos = vertex_pos(a, P, v);
     return pos / (uint32_t)a.S;
 }
+// The flag scans take one 32-bit word (32 vertices) per thread and walk its set bits: in a
+// late filtered sweep almost every word is zero (C5's LPA tie regime: ~0.8 % of the vertices
+// flagged), and a thread per vertex paid a load, a test and a branch for each of them
+// (k_list_count + k_list_fill were 86 ms of a C5 step).
 // Hybrid: each filtered replica's affected flags (its list size this sweep, rep_dense).
 __global__ __launch_bounds__(256) void k_aff_count(CDArgs a, int32_t* vcnt) {
     const int r = blockIdx.y;
     if (!a.active[r] || rep_full(a, r)) return;   // block-uniform
     const uint32_t* aff = a.aff + (int64_t)r * a.aw;
-    int c = 0;
-    for (int64_t v = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x; v < a.N && v < (int64_t)(blockIdx.x + 1) * TB * LB_PER;
-         v += TB)
-        c += aff_get(aff, v) ? 1 : 0;
+    const int64_t w = (int64_t)blockIdx.x * TB + threadIdx.x;
+    int c = w < a.aw ? __popc(aff[w]) : 0;
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(vcnt + r, c);
 }
@@ -1245,11 +1246,12 @@ __global__ __launch_bounds__(256) void k_list_count(CDArgs a, int sweep, int32_t
     __syncthreads();
     const Perm P = sweep_perm(a, order_rg(a, r, rep_dense(a, r)), sweep);
     const uint32_t* aff = a.aff + (int64_t)r * a.aw;
-    const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < LB_PER; ++i) {
-        const int64_t v = v0 + (int64_t)i * TB;
-        if (v < a.N && aff_get(aff, v)) atomicAdd(&s_lb[vertex_bucket(a, P, (uint32_t)v)], 1);
+    const int64_t w = (int64_t)blockIdx.x * TB + threadIdx.x;
+    uint32_t bits = w < a.aw ? aff[w] : 0u;
+    while (bits) {
+        const int64_t v = w * 32 + (__ffs(bits) - 1);
+        bits &= bits - 1;
+        if (v < a.N) atomicAdd(&s_lb[vertex_bucket(a, P, (uint32_t)v)], 1);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < B; k += TB)
@@ -1336,30 +1338,28 @@ __global__ __launch_bounds__(256) void k_list_fill(CDArgs a, int sweep, const in
     const int g = gco[r];
     const Perm P = sweep_perm(a, order_rg(a, r, rep_dense(a, r)), sweep);
     uint32_t* aff = a.aff + (int64_t)r * a.aw;
-    int bk[LB_PER], loc[LB_PER];
-    const int64_t v0 = (int64_t)blockIdx.x * TB * LB_PER + threadIdx.x;   // a multiple of 32 at lanes 0, 32
-#pragma unroll
-    for (int i = 0; i < LB_PER; ++i) {
-        const int64_t v = v0 + (int64_t)i * TB;
-        bk[i] = -1;
-        if (v >= a.N || !aff_get(aff, v)) continue;   // filter: vertices whose neighbour moved last sweep
-        bk[i] = (int)vertex_bucket(a, P, (uint32_t)v) / g;
-        loc[i] = atomicAdd(&s_cnt[bk[i]], 1);
+    const int64_t w = (int64_t)blockIdx.x * TB + threadIdx.x;   // one word: 32 vertices
+    const uint32_t word = w < a.aw ? aff[w] : 0u;
+    // pass 1: the block's count per round; pass 2 (after the block's bases are reserved) places
+    // the entries -- entries within a round may land in any order (see above)
+    for (uint32_t bits = word; bits; bits &= bits - 1) {
+        const int64_t v = w * 32 + (__ffs(bits) - 1);
+        if (v < a.N) atomicAdd(&s_cnt[(int)vertex_bucket(a, P, (uint32_t)v) / g], 1);
     }
-    // clear the words read: a word's 32 vertices are 32 lanes of one wave, which read it above
-#pragma unroll
-    for (int i = 0; i < LB_PER; ++i) {
-        const int64_t v = v0 + (int64_t)i * TB;
-        if (v < a.N && (v & 31) == 0) aff[v >> 5] = 0u;
-    }
+    if (word) aff[w] = 0u;   // flags consumed (filter: vertices whose neighbour moved last sweep)
     __syncthreads();
-    for (int k = threadIdx.x; k < B; k += TB)
+    for (int k = threadIdx.x; k < B; k += TB) {
         s_base[k] = s_cnt[k] ? atomicAdd(&cursor[(int64_t)r * B + k], s_cnt[k]) : 0;
+        s_cnt[k] = 0;
+    }
     __syncthreads();
     int32_t* lr = list + (int64_t)r * a.PN;
-#pragma unroll
-    for (int i = 0; i < LB_PER; ++i)
-        if (bk[i] >= 0) lr[s_base[bk[i]] + loc[i]] = (int32_t)(v0 + (int64_t)i * TB);
+    for (uint32_t bits = word; bits; bits &= bits - 1) {
+        const int64_t v = w * 32 + (__ffs(bits) - 1);
+        if (v >= a.N) continue;
+        const int k = (int)vertex_bucket(a, P, (uint32_t)v) / g;
+        lr[s_base[k] + atomicAdd(&s_cnt[k], 1)] = (int32_t)v;
+    }
 }
 // One bucket: decide (light + heavy rows) against the state left by earlier buckets, apply.
 // Every grid is fixed and every size is read on the device, so a sweep never waits on
@@ -1530,7 +1530,7 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
     // of rounds (coarse buckets) and the largest per-replica round (decide item slots), so
     // every launch is sized exactly, plus the active count left by the previous sweep.
     const bool hv = g.max_deg > LIGHT_MAX_DEG;
-    const unsigned lb_grid = (unsigned)((N + (int64_t)TB * LB_PER - 1) / ((int64_t)TB * LB_PER));
+    const unsigned lb_grid = (unsigned)((aw + TB - 1) / TB);   // flag scans: one 32-vertex word per thread
     int32_t* hinfo = (int32_t*)(c.hpin + 8);   // info[0..4] | n_active[0] at [6]
     const int sweep0 = h ? h->sweep0 : 0;
     int sweep = sweep0;

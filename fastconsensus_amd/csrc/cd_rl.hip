@@ -1233,13 +1233,21 @@ __global__ __launch_bounds__(RTB) void k_rl_mark_lm(RL a) {
             rb = (int64_t)(uint32_t)vr.x;
             d = vr.y;
         }
+        // four entries' column and label loads in flight at a time (a row walk one entry per
+        // iteration was a chain of dependent round trips: 13 ms per call at C5)
         const int dmax = wave_max(d);
-        for (int j = 0; j < dmax; ++j) {
-            const bool in = j < d;
-            const int32_t nb = in ? a.col[rb + j] : 0;
-            const bool diff = mine && in && a.lab[(int64_t)nb * a.ldT + rr] != dl;
-            const uint64_t bs = (__ballot(diff) >> (s * LG)) & gmask;
-            if (in && rl == 0 && bs) atomicOr((unsigned long long*)&a.aff[(int64_t)bank * a.N + nb], (unsigned long long)bs);
+        for (int j0 = 0; j0 < dmax; j0 += 4) {
+            int32_t nb[4], lb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nb[u] = j0 + u < d ? a.col[rb + j0 + u] : -1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) lb[u] = (mine && nb[u] >= 0) ? a.lab[(int64_t)nb[u] * a.ldT + rr] : dl;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t bs = (__ballot(lb[u] != dl) >> (s * LG)) & gmask;
+                if (nb[u] >= 0 && rl == 0 && bs)
+                    atomicOr((unsigned long long*)&a.aff[(int64_t)bank * a.N + nb[u]], (unsigned long long)bs);
+            }
         }
     }
 }
