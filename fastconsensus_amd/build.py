@@ -13,6 +13,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(OUT_DIR, "libfastconsensus_amd.so")
 SRC_HASH = LIB + ".srchash"     # the source hash the library was built from (profiles are matched to it)
+BUILD_REC = os.path.join(OUT_DIR, "BUILD.json")   # what the last build() did (provenance record)
 SOURCES = ["graph.hip", "consensus.hip", "cd.hip", "cd_rl.hip", "leiden.hip", "capi.cpp", "gen.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -51,29 +52,53 @@ def built_hash():
 
 
 def _compile(src):
+    """-> (object path, whether it was compiled now)"""
     path = os.path.join(CSRC, src)
     obj = _obj(src)
     newest = max(os.path.getmtime(d) for d in _deps())
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest:
-        return obj
+        return obj, False
     lang = ["-x", "hip"] if src.endswith(".hip") else []
     cmd = [HIPCC] + FLAGS + lang + ["-c", path, "-o", obj]
     subprocess.check_call(cmd)
-    return obj
+    return obj, True
+
+
+def _record(compiled, linked):
+    """BUILD.json: the build mode of the last build() -- which objects were compiled, whether the
+    library was relinked -- and the source hash it stands for."""
+    import json
+    import time
+    try:
+        ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True, timeout=60).stdout
+        ver = next((l.strip() for l in ver.splitlines() if "HIP version" in l), ver.strip()[:80])
+    except (OSError, subprocess.SubprocessError):
+        ver = None
+    rec = {"source_hash": source_hash(), "built_hash": built_hash(), "arch": ARCH, "hipcc": ver,
+           "compiled": compiled, "relinked": linked,
+           "build_mode": "compiled" if compiled else ("relinked" if linked else "up-to-date"),
+           "utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+    with open(BUILD_REC, "w") as f:
+        json.dump(rec, f, indent=1)
+    return rec
 
 
 def build(verbose=True, jobs=None):
     os.makedirs(os.path.join(OUT_DIR, "obj"), exist_ok=True)
     jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2), 8)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, SOURCES))
+        res = list(ex.map(_compile, SOURCES))
+    objs = [o for o, _ in res]
+    compiled = [src for src, (_, c) in zip(SOURCES, res) if c]
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs) \
             and built_hash() == source_hash():
+        _record(compiled, False)
         return LIB
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
     subprocess.check_call(cmd)
     with open(SRC_HASH, "w") as f:
         f.write(source_hash() + "\n")
+    _record(compiled, True)
     if verbose:
         print("built", LIB, file=sys.stderr)
     return LIB

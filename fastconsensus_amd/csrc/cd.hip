@@ -939,13 +939,21 @@ __global__ __launch_bounds__(256) void k_mark_lm(CDArgs a) {
     const int64_t v0 = v - lane;
     const int32_t* labr = a.lab + (int64_t)r * a.N;
     uint32_t* aff = a.aff + (int64_t)r * a.aw;
+    // four movers at a time, 16 lanes each (rows of ~20-30 entries left most of a 64-lane wave
+    // idle through each mover's chain of loads); the flags are ORs, so the order is free
+    const int grp = lane >> 4, gl = lane & 15;
     while (m) {
-        const int b = __ffsll((long long)m) - 1;
-        m &= m - 1;
+        int b = -1;
+        for (int g = 0; g < 4 && m; ++g) {        // group g takes the g-th remaining mover
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            if (g == grp) b = l;
+        }
+        if (b < 0) continue;
         const int4 vr = a.vrec[v0 + b];
         const int32_t d = labr[vr.w];
         const int64_t rb = (int64_t)(uint32_t)vr.x, re = rb + vr.y;
-        for (int64_t j = rb + lane; j < re; j += 64)
+        for (int64_t j = rb + gl; j < re; j += 16)
             if (labr[a.colp[j]] != d) aff_set(aff, a.col[j]);
     }
 }

@@ -1398,12 +1398,25 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         else k_lv_decide<IM, MD, LWS, 1><<<nblk, LTB, 0, c.stream>>>(a, b, stamp);               \
         timer_end(c, 5, t5);                                                                     \
         if (max_deg > LIGHT) {   /* tiers by row length (heavy_tier); tier 3: global tables */  \
-            const int t6 = timer_begin(c);                                                       \
+            /* one timer span per kernel launch, as rocprofv3 counts them */                     \
+            int t6 = timer_begin(c);                                                             \
             k_lv_heavy<IM, MD, 2048><<<2048, LTB, 0, c.stream>>>(a, stamp, 0);                   \
-            if (max_deg > 1024) k_lv_heavy<IM, MD, 4096><<<1280, LTB, 0, c.stream>>>(a, stamp, 1); \
-            if (max_deg > 2048) k_lv_heavy<IM, MD, HLS><<<512, LTB, 0, c.stream>>>(a, stamp, 2); \
-            if (max_deg > 4096) k_lv_heavy<IM, MD, 2048><<<hg, LTB, 0, c.stream>>>(a, stamp, 3); \
             timer_end(c, 6, t6);                                                                 \
+            if (max_deg > 1024) {                                                                \
+                t6 = timer_begin(c);                                                             \
+                k_lv_heavy<IM, MD, 4096><<<1280, LTB, 0, c.stream>>>(a, stamp, 1);               \
+                timer_end(c, 6, t6);                                                             \
+            }                                                                                    \
+            if (max_deg > 2048) {                                                                \
+                t6 = timer_begin(c);                                                             \
+                k_lv_heavy<IM, MD, HLS><<<512, LTB, 0, c.stream>>>(a, stamp, 2);                 \
+                timer_end(c, 6, t6);                                                             \
+            }                                                                                    \
+            if (max_deg > 4096) {                                                                \
+                t6 = timer_begin(c);                                                             \
+                k_lv_heavy<IM, MD, 2048><<<hg, LTB, 0, c.stream>>>(a, stamp, 3);                 \
+                timer_end(c, 6, t6);                                                             \
+            }                                                                                    \
         }                                                                                        \
         k_lv_apply<IM, MD><<<nblk + (max_deg > LIGHT ? hblk : 0), LTB, 0, c.stream>>>(a, nblk, hblk, stamp); \
     } while (0)
