@@ -323,34 +323,40 @@ __device__ __forceinline__ uint32_t tsize(int64_t d) {
 }
 
 // Wave-level candidate scan over table slots [0, ts): best (score, tie, community) and the
-// weight to the own community, reduced over the wave.
+// weight to the own community, reduced over the wave.  The occupied slots are packed to the
+// front of the table first (as in wave_scan_info): a table of ts >= 2d slots is at least half
+// empty, and each pass over GL slots is one dependent round trip (LDS read, Sigma gather).
 template <int GL = 64>
-__device__ __forceinline__ void wave_scan(const LvArgs& a, const int32_t* keys, const int32_t* vals, uint32_t ts,
+__device__ __forceinline__ void wave_scan(const LvArgs& a, int32_t* keys, int32_t* vals, uint32_t ts,
                                           int32_t own, long long kvx, int32_t r, int64_t x, long long& bs,
                                           uint32_t& bh, int32_t& bc, long long& wown, int& ncand) {
-    const int gl = threadIdx.x & (GL - 1);
+    const int lane = threadIdx.x & 63, gl = lane & (GL - 1);
     bs = LLONG_MIN; bh = 0; bc = -1;   // wown: this lane's own-community weight (not in the table)
-    constexpr int UNR = 1;
-    for (uint32_t s0 = gl; s0 < ts; s0 += GL * UNR) {
-        int32_t k[UNR];
-        long long val[UNR], tk[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            const uint32_t s = s0 + u * GL;
-            k[u] = s < ts ? keys[s] : -1;
-            val[u] = s < ts ? vals[s] : 0;
+    const unsigned long long gmask = GL == 64 ? ~0ull : (((1ull << GL) - 1) << (lane & ~(GL - 1)));
+    const unsigned long long below = gmask & ((1ull << lane) - 1);
+    uint32_t n = 0;
+    for (uint32_t s0 = 0; s0 < ts; s0 += GL) {   // ts: a power of two >= 64 >= GL
+        const int32_t k = keys[s0 + gl], v = vals[s0 + gl];
+        const bool ok = k >= 0;
+        const unsigned long long b = __ballot(ok) & gmask;
+        if (ok) {
+            const uint32_t p = n + (uint32_t)__popcll(b & below);
+            keys[p] = k;
+            vals[p] = v;
         }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) tk[u] = k[u] >= 0 ? a.tot[k[u]] : 0;
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-            if (k[u] < 0) continue;
-            ++ncand;
-            const long long sc = val[u] * a.M2 - kvx * tk[u];
-            const uint32_t h = tie_of(a, r, x, k[u]);
-            if (lv_better(sc, h, k[u], bs, bh, bc)) { bs = sc; bh = h; bc = k[u]; }
-        }
+        n += (uint32_t)__popcll(b);
     }
+    wsync();
+    for (uint32_t ci = gl; ci < n; ci += GL) {
+        const int32_t k = keys[ci];
+        const long long val = vals[ci];
+        const long long tk = a.tot[k];
+        ++ncand;
+        const long long sc = val * a.M2 - kvx * tk;
+        const uint32_t h = tie_of(a, r, x, k);
+        if (lv_better(sc, h, k, bs, bh, bc)) { bs = sc; bh = h; bc = k; }
+    }
+    (void)own;
     for (int off = GL / 2; off; off >>= 1) {
         const long long s2 = __shfl_xor(bs, off);
         const uint32_t h2 = __shfl_xor(bh, off);
@@ -899,6 +905,14 @@ __global__ void k_ag_memb(int64_t total, int64_t N, const uint8_t* done, const i
     memb[i] = nid[R[memb[i]]];
 }
 
+// Lanes per member row when aggregating: the power of two >= the members' average row length,
+// 4..cap (rows are walked by groups side by side; one group per member at a time)
+__device__ __forceinline__ int ag_group(int64_t entries, int32_t members, int cap) {
+    const int64_t avg = members > 0 ? (entries + members - 1) / members : 1;
+    int g = 4;
+    while (g < cap && g < avg) g <<= 1;
+    return g;
+}
 // Aggregate rows: new vertex xn = refined community; its row = the members' rows mapped
 // through nid[R[.]], self loops dropped, weights summed.  One wave per light new vertex
 // (LDS table), heavy ones (member-row sum > LIGHT) are listed for k_ag_rows_heavy.  Rows
@@ -921,11 +935,15 @@ __global__ __launch_bounds__(LTB) void k_ag_rows(LvArgs a, int64_t nUn, const in
     const uint32_t ts = tsize(ubo[xn + 1] - ubo[xn]);
     for (uint32_t s = lane; s < ts; s += 64) { keys[s] = -1; vals[s] = 0; }
     wsync();
-    for (int32_t q = moff[xn]; q < moff[xn + 1]; ++q) {
+    // members side by side: groups of ga lanes (the member rows' average length, 4..64), so a
+    // module of many short rows does not walk them one at a time
+    const int ga = ag_group(ubo[xn + 1] - ubo[xn], moff[xn + 1] - moff[xn], 64);
+    const int grp = lane / ga, gl = lane & (ga - 1);
+    for (int32_t q = moff[xn] + grp; q < moff[xn + 1]; q += 64 / ga) {
         const int64_t x = mlist[q];
         const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
         const int64_t xr = IMPL ? x - base : x;
-        for (int64_t j = a.rowptr[xr] + lane; j < a.rowptr[xr + 1]; j += 64) {
+        for (int64_t j = a.rowptr[xr] + gl; j < a.rowptr[xr + 1]; j += ga) {
             const int32_t yn = nid[a.R[base + a.col[j]]];
             if (yn != (int32_t)xn) tins(keys, vals, ts, true, yn, a.w ? a.w[j] : 1);
         }
@@ -968,11 +986,13 @@ __global__ __launch_bounds__(LTB) void k_ag_rows_heavy(LvArgs a, const int32_t* 
         if (lds)
             for (uint32_t s = threadIdx.x; s < ts; s += LTB) { lkey[s] = -1; lval[s] = 0; }
         __syncthreads();
-        for (int32_t q = moff[xn]; q < moff[xn + 1]; ++q) {
+        const int ga = ag_group(ubn, moff[xn + 1] - moff[xn], LTB);   // lanes per member (see k_ag_rows)
+        const int grp = threadIdx.x / ga, gl = threadIdx.x & (ga - 1);
+        for (int32_t q = moff[xn] + grp; q < moff[xn + 1]; q += LTB / ga) {
             const int64_t x = mlist[q];
             const int64_t base = IMPL ? (x / a.N0) * a.N0 : 0;
             const int64_t xr = IMPL ? x - base : x;
-            for (int64_t j = a.rowptr[xr] + threadIdx.x; j < a.rowptr[xr + 1]; j += LTB) {
+            for (int64_t j = a.rowptr[xr] + gl; j < a.rowptr[xr + 1]; j += ga) {
                 const int32_t yn = nid[a.R[base + a.col[j]]];
                 if (yn == (int32_t)xn) continue;
                 const int s = tins(keys, vals, ts, true, yn, a.w ? a.w[j] : 1);
