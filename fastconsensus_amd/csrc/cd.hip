@@ -1558,7 +1558,8 @@ void cd_run(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iterati
         if (rounds == 0 || (sweep > sweep0 && hinfo[6] == 0)) break;   // every replica has stopped
         // small sweeps (every replica visits <= tail_visits vertices): hand every remaining
         // sweep to the per-replica tail kernel (it takes the flags as its first worklist)
-        if (c.tail_visits > 0 && (int64_t)hinfo[4] <= c.tail_visits && B <= TAIL_MAXB) {
+        const int64_t tail_thr = c.tail_visits >= 0 ? c.tail_visits : (louv ? 1024 : 4096);
+        if (tail_thr > 0 && (int64_t)hinfo[4] <= tail_thr && B <= TAIL_MAXB) {
             int32_t* tbuf = ensure<int32_t>(c.tailbuf, (size_t)rcount * 3 * N);
             int32_t* tmark = ensure<int32_t>(c.tailmark, (size_t)rcount * N);
             FC_HIP(hipMemsetAsync(tmark, 0, 4 * (size_t)rcount * N, c.stream));

@@ -190,8 +190,9 @@ struct Ctx {
     int64_t apply_blocks = getenv("FC_APPLY_BLOCKS") ? atoll(getenv("FC_APPLY_BLOCKS")) : 32;   // per replica
     std::vector<hipEvent_t> sweep_ev;   // per-sweep completion ring (cd_run)
     DevBuf tailbuf, tailmark;       // CD tail kernel: worklists [n_r][3N], epoch marks [n_r][N]
-    // per replica; 0 = off.  1024 since round 5 (n_p = 8 share 45.5 -> 44.4 ms; 4096 before)
-    int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : 1024;
+    // per replica; 0 = off; -1 (default) = per algorithm: 1024 for Louvain (n_p = 8 share 45.5 ->
+    // 44.4 ms against 4096), 4096 for LPA (C3 lpm 24.1 -> 22.2 ms against 1024; profiles/r05_tail_ab.txt)
+    int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : -1;
     bool order_pass = false;        // store_order()'s CD run (int64 totals, see there)
     int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
     int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 4;   // sweeps of that pass

@@ -121,8 +121,8 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_PRUNE 5       /* 1 (default): once a sweep moves < n/4 vertices, later sweeps visit only vertices with a moved
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 #define FC_OPT_TAIL_VISITS 7 /* once no replica visits more than this many vertices in a sweep,
-                                the remaining sweeps run in one workgroup per replica (default
-                                4096; 0 = off).  Same results either way.                       */
+                                the remaining sweeps run in one workgroup per replica (default:
+                                1024 for Louvain, 4096 for LPA; 0 = off).  Same results either way. */
 #define FC_OPT_COARSEN 8    /* gmax (default 8; 0 = off): a filtered sweep of V vertices runs its buckets in
                                 rounds of g (the largest power of two <= gmax, <= buckets, with V*g <= n),
                                 so a small sweep is not 32 latency-bound rounds.  Measured neutral on
