@@ -318,13 +318,53 @@ def host_workers():
     return max(1, min(8, cpus))
 
 
+ADJ_DEADLINE_S = 30.0            # forked read: workers still running after this (+0.2 us per entry) are killed
+
+
+def _fork_safe():
+    """The forked read runs only in a process with no other Python thread (a thread could hold
+    an interpreter-level lock -- import, logging, a user lock -- that a child would wait on
+    forever) and when FC_HOST_FORK is not 0.  Native runtime threads (a HIP runtime started by
+    an earlier Engine) do not block it: the children run dict iteration and numpy only (the
+    interpreter's allocator under the GIL, glibc malloc, which resets its locks at fork), never
+    touch the GPU and leave through os._exit; the deadline in _reap covers the rest."""
+    import threading
+    return os.environ.get("FC_HOST_FORK", "1") != "0" and threading.active_count() == 1
+
+
+def _reap(pids, deadline):
+    """Wait for the forked workers with WNOHANG polling until `deadline` (time.monotonic());
+    past it the rest are killed and reaped.  True iff every worker exited with status 0."""
+    import signal
+    import time
+    ok, left = True, list(pids)
+    while left:
+        for pid in list(left):
+            done, status = os.waitpid(pid, os.WNOHANG)
+            if done:
+                left.remove(pid)
+                ok = ok and status == 0
+        if left and time.monotonic() > deadline:
+            for pid in left:
+                try:
+                    os.kill(pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                os.waitpid(pid, 0)
+            return False
+        if left:
+            time.sleep(0.002)
+    return ok
+
+
 def read_adjacency(rows, lens, key=None):
     """The keys of the dicts `rows` (row i has lens[i] keys), concatenated into int64, each
     through `key` when given.  Reading 27.5 M dict keys is CPython-bound (~0.1 us per key, most
     of it a cache miss on the key object), so large adjacencies are read by forked workers,
     each chaining a contiguous range of rows into a shared anonymous mapping (no pickling: the
-    children see the parent's dicts copy-on-write).  Any worker failure falls back to the
-    serial read."""
+    children see the parent's dicts copy-on-write).  Any worker failure, or workers still
+    running at the deadline (killed), falls back to the serial read; a process with other
+    Python threads reads serially (_fork_safe)."""
     import itertools
     tot = int(lens.sum())
     W = host_workers() if hasattr(os, "fork") else 1
@@ -333,9 +373,10 @@ def read_adjacency(rows, lens, key=None):
         it = itertools.chain.from_iterable(rows[lo:hi])
         return np.fromiter(it if key is None else map(key, it), np.int64, count=cnt)
 
-    if W <= 1 or tot < ADJ_PARALLEL_MIN:
+    if W <= 1 or tot < ADJ_PARALLEL_MIN or not _fork_safe():
         return serial(0, len(rows), tot)
     import mmap
+    import time
     off = np.zeros(len(rows) + 1, np.int64)
     np.cumsum(lens, out=off[1:])
     cut = np.searchsorted(off, np.linspace(0, tot, W + 1).astype(np.int64))
@@ -358,9 +399,7 @@ def read_adjacency(rows, lens, key=None):
                     os._exit(code)
             pids.append(pid)
     finally:
-        ok = True
-        for pid in pids:
-            ok = os.waitpid(pid, 0)[1] == 0 and ok
+        ok = _reap(pids, time.monotonic() + ADJ_DEADLINE_S + tot * 2e-7)
     if len(pids) == 0 or not ok:
         del flat
         buf.close()

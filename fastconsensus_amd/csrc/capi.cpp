@@ -210,7 +210,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_RL_MIN_REPLICAS: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_replicas >= 1"); c.rl_min_replicas = value; break;
         case FC_OPT_RL_MIN_VERTICES: FC_REQUIRE(value >= 1, FC_EINVAL, "rl_min_vertices >= 1"); c.rl_min_vertices = value; break;
         case FC_OPT_DENSE_DIV: FC_REQUIRE(value >= 0 && value <= 64, FC_EINVAL, "dense_div must be 0..64"); c.dense_div = (int)value; break;
-        case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= 0, FC_EINVAL, "tail_visits >= 0"); c.tail_visits = value; break;
+        case FC_OPT_TAIL_VISITS: FC_REQUIRE(value >= -1, FC_EINVAL, "tail_visits >= 0, or -1 (per algorithm)"); c.tail_visits = value; break;
         default: throw FcError{FC_EINVAL, "unknown option"};
     }
     FC_API_END

@@ -768,7 +768,7 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
         const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
         rl_push_slow(a, slow, e, h.rr);
         const bool tied = !LOUV && c_cand >= 2u;                 // this visit's candidates (see k_rl_decide)
-        if (!LOUV && valid && tied && a.track[h.rr]) rl_tie_flag(a, h.rr, h.v);
+        if (!LOUV && FC_LPA_TIES && valid && tied && a.track[h.rr]) rl_tie_flag(a, h.rr, h.v);
         if (valid) {
             a.dec[e * a.ldT + h.rr] = h.work ? dcs : -1;
             if (c_dq) atomicAdd(rl_red(a, h.rr, 0), c_dq);
@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_lds(RL a, int k, int sweep) {
                     c_unst += (kown != (long long)vm) ? 1 : 0;
                     dcs = best_c != own ? best_c : -1;
                 }
-                if (nc >= 2 && a.track[rr]) rl_tie_flag(a, rr, v);
+                if (FC_LPA_TIES && nc >= 2 && a.track[rr]) rl_tie_flag(a, rr, v);
             }
         }
         if (work) { c_vis += 1; c_ent += (unsigned long long)d; }
@@ -1439,9 +1439,13 @@ void rl_layout(int n_r, int* LG, int* VPW, int* banks, int* ldT) {
 // the graph and options the replica-lane kernels handle (int32 totals, 32-bit row offsets)
 static bool cd_rl_fits(const Ctx& c, int algo) {
     // int32 community totals (louvain only: LPA ignores the weights, so a heavily weighted
-    // consensus graph -- 2M past 2^31 at SBM-4M, n_p = 128 -- still fits its label propagation)
+    // consensus graph -- 2M past 2^31 at SBM-4M, n_p = 128 -- still fits its label propagation);
+    // the sweep record (boff | voff | n_active, one pinned DMA per sweep) must fit the pinned
+    // scratch: B * NCLS segments, i.e. B <= 253 buckets -- more go to cd.hip (same semantics)
+    const int64_t nseg = (int64_t)cd_buckets(c, algo) * NCLS;
     return !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && (!is_louvain(algo) || c.g.M2 <= 0x7fffffffll) &&
-           c.g.m < (int64_t(1) << 31) && (c.chunk == 0 || c.chunk == RL_CHUNK);
+           c.g.m < (int64_t(1) << 31) && (c.chunk == 0 || c.chunk == RL_CHUNK) &&
+           16 + 2 * (nseg + 1) + 2 <= 2 * (int64_t)FC_HPIN_I64;
 }
 bool cd_rl_supported(const Ctx& c, int algo) { return c.cd_engine == 1 && cd_rl_fits(c, algo); }
 

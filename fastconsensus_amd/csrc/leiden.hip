@@ -1406,6 +1406,9 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
                 ioff += h_icnt[b];
                 nblk = (int)nb(a.icnt);
             }
+            // an empty bucket (coarse levels with one or two replicas still moving) has
+            // nothing to decide, list as heavy or apply: no zero-block launches
+            if (nblk == 0) continue;
             const uint32_t stamp = ++stamp_ctr;   // unique per bucket launch of this run (mvt)
             FC_HIP(hipMemsetAsync(hcnt, 0, 4 * NTIER, c.stream));
             // (timed per launch into spans 5 / 6 when timing is on: lv decide / lv heavy)

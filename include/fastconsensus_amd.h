@@ -121,8 +121,9 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_PRUNE 5       /* 1 (default): once a sweep moves < n/4 vertices, later sweeps visit only vertices with a moved
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 #define FC_OPT_TAIL_VISITS 7 /* once no replica visits more than this many vertices in a sweep,
-                                the remaining sweeps run in one workgroup per replica (default:
-                                1024 for Louvain, 4096 for LPA; 0 = off).  Same results either way. */
+                                the remaining sweeps run in one workgroup per replica (-1, the
+                                default: per algorithm, 1024 for Louvain, 4096 for LPA; 0 = off).
+                                Same results either way.                                          */
 #define FC_OPT_COARSEN 8    /* gmax (default 8; 0 = off): a filtered sweep of V vertices runs its buckets in
                                 rounds of g (the largest power of two <= gmax, <= buckets, with V*g <= n),
                                 so a small sweep is not 32 latency-bound rounds.  Measured neutral on
@@ -149,13 +150,13 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
                                 that moves < n/4 vertices.                                       */
 #define FC_OPT_INFOMAP_TRIALS 13 /* independent Infomap runs per replica, the smallest codelength kept
                                     (default 10, igraph community_infomap's trials)              */
-#define FC_OPT_CD_ENGINE 14  /* louvain / lpm CD batches.  0 (default): the classic engine, a random
+#define FC_OPT_CD_ENGINE 14  /* louvain / lpm CD batches.  0: the classic engine, a random
                                 visit order per replica (FC_OPT_COARSEN / FC_OPT_TAIL_VISITS
                                 apply).  1: the replica-lane engine (cd_rl.hip) -- every replica of
                                 a batch visits the vertices in ONE shared random order per sweep
                                 (ties broken per replica), labels node-major, one wave deciding a
                                 vertex for up to 64 replicas; no coarse rounds or tail kernel.
-                                2: the hybrid -- a replica's sweeps visit the batch's shared order
+                                2 (default): the hybrid -- a replica's sweeps visit the batch's shared order
                                 while they are full and its own order from its first filtered
                                 (pruned) sweep on; the replica-lane engine runs the full sweeps of a
                                 batch of >= FC_OPT_RL_MIN_REPLICAS replicas, cd.hip everything else.

@@ -251,6 +251,23 @@ def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen,
     eng.close()
 
 
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cd_hybrid_many_buckets_falls_back(fcmod, algo):
+    """FC_OPT_BUCKETS past what the replica-lane sweep record holds (253 buckets x 4 degree
+    classes in the pinned scratch): the hybrid runs the batch on cd.hip with the same
+    semantics instead of failing, bit-exact against the twin."""
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=61)
+    kw = _engine(eng, 2, 0, 0)
+    eng.set_params(buckets=512)
+    eng.set_option("chunk", 0)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    eng.cd(algo, 0, 9, 9, 2)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, 9, 0, 2, 61, buckets=512, chunk=0, prune=1, **kw)
+    np.testing.assert_array_equal(eng.get_labels(9), exp)
+    eng.close()
+
+
 @pytest.mark.parametrize("engine", [2, 3])
 @pytest.mark.parametrize("dense_div", [0, 2, 4, 16])
 @pytest.mark.parametrize("algo", [0, 1])
