@@ -148,7 +148,7 @@ def cpu_baseline(n, u, v, cfg, seed):
     orc.check(kept.w, reps, cfg["delta"])
     t["threshold"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    pairs = orc.closure_sample_pairs(kept, g.m, seed, 0)
+    pairs = orc.closure_sample_pairs(kept, g.m, seed, 0, orc.closure_rounds(algo))
     cu, cv, cw, cf = orc.closure_from_pairs(algo, kept, pairs, lab, reps)
     closure = orc.EdgeGraph(n, cu, cv, cw, (np.int64(1) << orc.AGE_ITER_SHIFT) + cf)
     t["closure"] = time.perf_counter() - t0

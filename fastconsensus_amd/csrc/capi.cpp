@@ -203,7 +203,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
         case FC_OPT_STORE: c.store_order = value != 0; break;
         case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
         case FC_OPT_SEED: c.seed = (uint64_t)value; break;
-        case FC_OPT_CLOSURE_ROUNDS: FC_REQUIRE(value >= 1, FC_EINVAL, "closure_rounds >= 1"); c.closure_rounds = (int)value; break;
+        case FC_OPT_CLOSURE_ROUNDS: FC_REQUIRE(value >= 0, FC_EINVAL, "closure_rounds >= 1, or 0 (per algorithm)"); c.closure_rounds = (int)value; break;
         case FC_OPT_PRUNE_MARK: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "prune_mark must be 0, 1 or 2"); c.prune_mark = (int)value; break;
         case FC_OPT_INFOMAP_TRIALS: FC_REQUIRE(value >= 1, FC_EINVAL, "infomap trials >= 1"); c.infomap_trials = (int)value; break;
         case FC_OPT_CD_ENGINE: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "cd_engine must be 0, 1 or 2"); c.cd_engine = (int)value; break;

@@ -164,6 +164,7 @@ __global__ void k_krowptr(int64_t n, const int64_t* rowptr, const int64_t* p2, i
 void consensus_apply(Ctx& c, int algo, int n_p, double tau, const int32_t* partial, int64_t* kept_out,
                      int64_t* unconv_out) {
     c.clo_next = -1;   // a sharded closure sequence (fc_closure_begin ...) read the previous kept graph
+    c.clo_algo = algo;   // the closure's block count follows the loop (closure_blocks)
     const int sl = timer_begin(c);
     Graph& g = c.g;
     const int64_t m = g.m, cap = m + 1;
@@ -455,7 +456,7 @@ struct Clo {
 static Clo clo_bufs(Ctx& c, int64_t attempts) {
     Clo b;
     const int64_t cap = attempts > 0 ? attempts : 1;
-    b.R = (int)std::max<int64_t>(1, std::min<int64_t>(c.closure_rounds, cap));
+    b.R = (int)std::max<int64_t>(1, std::min<int64_t>(closure_blocks(c), cap));
     b.rcap = (cap + b.R - 1) / b.R + 1;                            // attempts per block (at most)
     const int64_t N = c.N;
     b.hsize = 1024;

@@ -174,7 +174,8 @@ struct Ctx {
     int clo_pack = getenv("FC_CLO_PACK") ? atoi(getenv("FC_CLO_PACK")) : 1;
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
         clo_nrow, clo_ncol;
-    int closure_rounds = 4;         // FC_OPT_CLOSURE_ROUNDS (round 3: 8; DESIGN, closure)
+    int closure_rounds = 0;         // FC_OPT_CLOSURE_ROUNDS; 0 = per algorithm (closure_blocks below)
+    int clo_algo = 0;               // algorithm of the last consensus_apply (the kept graph the closure samples)
     // sharded closure (fc_closure_begin / _block_sample / _block_add / _finish): the run's
     // attempts and block count, the next block to add (blocks go in order), -1 = not begun
     int64_t clo_attempts = 0;
@@ -248,6 +249,17 @@ struct CDHandoff {
 // edge its bucketed batches must stay within 0.25 of sequential LPA's structured fraction
 // (tests/test_gpu_cd_parity.py), and 16 buckets measured 0.28 off (profiles/r04_buckets_ab.txt)
 constexpr int CD_BUCKETS_LOUVAIN = 16, CD_BUCKETS_LPA = 32;
+// Closure blocks per algorithm (DESIGN, "Triadic closure"): the reference's sampler sees every
+// earlier attempt's edge; a block sees only the earlier blocks'.  Louvain's closure edges carry
+// co-membership weights and 4 blocks keep its consensus at or above the reference loop's
+// (C2 / C3 gates); lpm's (and infomap's) weight-0 closure edges are topology for the next LPA,
+// and 4 blocks (+1.7 % candidates vs sequential on the sparse C3 graph) cost 0.0008 consensus
+// NMI there -- 16 blocks (+0.5 %) match the reference loop (tools/lpm_ablate.py).
+constexpr int CLOSURE_ROUNDS_LOUVAIN = 4, CLOSURE_ROUNDS_LPM = 16;
+inline int closure_blocks(const Ctx& c) {
+    return c.closure_rounds > 0 ? c.closure_rounds
+                                : (is_louvain(c.clo_algo) ? CLOSURE_ROUNDS_LOUVAIN : CLOSURE_ROUNDS_LPM);
+}
 inline int cd_buckets(const Ctx& c, int algo) {
     return c.buckets > 0 ? c.buckets : (is_louvain(algo) ? CD_BUCKETS_LOUVAIN : CD_BUCKETS_LPA);
 }

@@ -137,8 +137,10 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_SEED 10       /* replace the seed fc_create took; everything random after the call
                                 (the next fc_load_graph's numbering, CD, closure) follows it     */
 #define FC_OPT_CLOSURE_ROUNDS 11  /* triadic closure (:175-190, :292-304) samples from a GROWING graph; the
-                                L attempts run in this many consecutive blocks (default 4), each drawing
-                                from the post-threshold graph plus the earlier blocks' closure edges.
+                                L attempts run in this many consecutive blocks, each drawing from the
+                                post-threshold graph plus the earlier blocks' closure edges.  0 (the
+                                default): per algorithm -- 4 for louvain / louvain_nc, 16 for lpm and
+                                infomap (whose weight-0 closure edges shape the next LPA's topology);
                                 1 = every attempt from the post-threshold graph only.             */
 #define FC_OPT_PRUNE_MARK 12 /* which neighbours a tracked move marks for the next (filtered) sweep.
                                 1 (default): on consensus graphs (weights > 1; Louvain and LPA)

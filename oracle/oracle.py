@@ -193,10 +193,16 @@ def closure_from_pairs(algo, g, pairs, labels, n_p):
     return ou[:k].copy(), ov[:k].copy(), ow[:k].copy(), of[:k].copy()
 
 
-CLOSURE_ROUNDS = 4   # the engine's default (fc_ctx.h closure_rounds, FC_OPT_CLOSURE_ROUNDS)
+# the engine's default closure blocks per algorithm (fc_ctx.h CLOSURE_ROUNDS_LOUVAIN / _LPM,
+# FC_OPT_CLOSURE_ROUNDS = 0): louvain loops 4, lpm / infomap loops 16
+CLOSURE_ROUNDS_LOUVAIN, CLOSURE_ROUNDS_LPM = 4, 16
 
 
-def closure_sample_pairs(kept, attempts, seed, iteration, rounds=CLOSURE_ROUNDS):
+def closure_rounds(algo):
+    return CLOSURE_ROUNDS_LOUVAIN if algo in (LOUVAIN, LOUVAIN_NC) else CLOSURE_ROUNDS_LPM
+
+
+def closure_sample_pairs(kept, attempts, seed, iteration, rounds=CLOSURE_ROUNDS_LOUVAIN):
     """Engine's device sampler, restated: the (a, b) pair of every attempt (or (-1, -1)), the
     attempts in `rounds` blocks, each drawing from the kept graph plus the earlier blocks'
     closure edges (orc_closure_sample)."""

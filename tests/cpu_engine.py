@@ -28,6 +28,7 @@ class OracleEngine:
         self.dense_div = dense_div
         self.sigma = None if sigma is None else np.asarray(sigma, np.int32)
         self.lab = None
+        self.algo = 0                                 # the last consensus_apply's (engine: Ctx::clo_algo)
 
     # graph -----------------------------------------------------------------------------
     def load_graph(self, n, u, v):
@@ -92,11 +93,12 @@ class OracleEngine:
         nw = nw.astype(np.int32)
         keep = orc.threshold(nw, tau, n_p)
         self.kept = orc.EdgeGraph(g.N, g.u[keep], g.v[keep], nw[keep], g.age[keep])
+        self.algo = algo                              # the closure's block count follows the loop
         conv, cnt = orc.check(self.kept.w, n_p, delta)
         return (conv if algo in (0, 2) else False), self.kept.m, cnt   # louvain loops have check #1
 
     def closure_sample(self, attempts, iteration):
-        pairs = orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration)
+        pairs = orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration, orc.closure_rounds(self.algo))
         dummy = np.zeros((1, self.g.N), np.int32)
         cu, cv, _, cf = orc.closure_from_pairs(1, self.kept, pairs, dummy, 1)
         order = np.lexsort((cv, cu))                  # the device keeps candidates key-sorted
@@ -107,10 +109,11 @@ class OracleEngine:
     # (key, first attempt) pairs, the gathered lists re-assembled into the attempt-indexed pair
     # array, first occurrences kept -- the same candidates as closure_sample by construction
     def closure_begin(self, attempts, iteration):
-        self._clo = (orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration), int(attempts))
+        rounds = orc.closure_rounds(self.algo)
+        self._clo = (orc.closure_sample_pairs(self.kept, attempts, self.seed, iteration, rounds), int(attempts))
         self._clo_got = []
         self._clo_next = 0
-        return max(1, min(orc.CLOSURE_ROUNDS, max(int(attempts), 1)))
+        return max(1, min(rounds, max(int(attempts), 1)))
 
     def closure_block_sample(self, block, lo, hi, out):
         assert block == self._clo_next, "closure blocks go in order"

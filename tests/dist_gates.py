@@ -9,10 +9,11 @@ device engine is held to the reference's DISTRIBUTION, not only to its mean:
 * lower tail      10th percentile >= the reference's - 0.03
 * stochastic order  one-sided two-sample KS test (H1: the device's values are smaller) at
                   alpha = 0.01 -- a device distribution that is only shifted UP (better NMI)
-                  passes; the two-sided p-value is printed beside it.  Asserted where the
-                  distribution is wide (C2: sd ~0.03); at C3 (sd ~0.0005, 40 vs 64 runs) it
-                  flags offsets far below any practical difference (0.0008 NMI), so there the
-                  mean / spread / lower-tail gates decide and the KS p-value is printed.
+                  passes; the two-sided p-value is printed beside it.  Asserted at C2 (sd
+                  ~0.03) and, since round 6, at C3 too (sd ~0.0005, 40 device vs 64 reference
+                  runs), where it resolves offsets of ~0.0003 NMI: round 5's C3 lpm shift of
+                  0.0008 (p ~ 0) came from the closure's block count (DESIGN, "Triadic
+                  closure").  C3 also tightens the lower tail to p10 >= reference - 0.0005.
 
 nmi() is sklearn's normalized_mutual_info_score (arithmetic mean of the entropies) computed
 from a bincount contingency table: the same value (tests/test_dist_gates.py), ~20x faster on
@@ -55,7 +56,7 @@ def describe(x):
     return "mean %.4f sd %.4f p10 %.4f min %.4f (%d runs)" % (x.mean(), x.std(), np.percentile(x, 10), x.min(), x.size)
 
 
-def check(got, ref, tol_mean, label="", ks=True):
+def check(got, ref, tol_mean, label="", ks=True, p10_slack=P10_SLACK):
     """Returns the printed summary; raises AssertionError naming the failed gate."""
     from scipy.stats import ks_2samp
     got = np.asarray(got, np.float64)
@@ -68,7 +69,7 @@ def check(got, ref, tol_mean, label="", ks=True):
     print(msg)
     assert got.mean() >= ref.mean() - tol_mean, "mean gate: " + msg
     assert ratio <= SD_RATIO_MAX, "spread gate: " + msg
-    assert np.percentile(got, 10) >= np.percentile(ref, 10) - P10_SLACK, "lower-tail gate: " + msg
+    assert np.percentile(got, 10) >= np.percentile(ref, 10) - p10_slack, "lower-tail gate: " + msg
     if ks:
         assert ks1 >= KS_ALPHA, "KS gate: " + msg
     return msg

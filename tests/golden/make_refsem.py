@@ -23,6 +23,7 @@ Usage:  python tests/golden/make_refsem.py            the LFR-1k records (30 see
         python tests/golden/make_refsem.py c3         the round-3 LFR-100k records
         python tests/golden/make_refsem.py c3v2       LFR-100k louvain over 64 seeds and lpm on the
                                                       average-degree-8 graph over 32 (see run_c3)
+        python tests/golden/make_refsem.py c3lpm64    that lpm record extended to 64 seeds
 """
 import importlib.util
 import json
@@ -199,6 +200,35 @@ def run_c3(algorithm, tau, seeds, n_p=64, mu=0.5, avg_deg=None, max_deg=50, tag=
     print(name, "mean %.4f sd %.4f" % (rec["nmi_mean"], rec["nmi_sd"]))
 
 
+def extend_c3(name, algorithm, tau, seeds, n_p=64, mu=0.5, avg_deg=None, max_deg=50):
+    """Add reference-loop runs for `seeds` to an existing refsem_<name>.json (same graph and
+    settings as run_c3 recorded), so the distribution gates see more reference samples."""
+    from sklearn.metrics import normalized_mutual_info_score as nmi
+    from fastconsensus_amd import synth
+    path = os.path.join(HERE, "refsem_%s.json" % name)
+    with open(path) as f:
+        rec = json.load(f)
+    kw = {} if avg_deg is None else {"avg_deg": avg_deg, "max_deg": max_deg}
+    u, v, planted = synth.lfr(100_000, mu, seed=42, **kw)
+    g = orc.EdgeGraph.from_lines(100_000, np.stack([u, v], 1))
+    assert int(g.m) == rec["m"] and rec["algorithm"] == algorithm and rec["n_p"] == n_p
+    algo = 0 if algorithm == "louvain" else 1
+    for seed in seeds:
+        if seed in rec["seeds"]:
+            continue
+        lab, it = orc.refsem_run(algo, g, n_p, tau, 0.02, seed=seed, nthreads=8)
+        rec["seeds"].append(seed)
+        rec["nmi"].append(float(np.mean([nmi(planted, x) for x in lab])))
+        rec["k"].append(float(np.mean([len(np.unique(x)) for x in lab])))
+        rec["iterations"].append(int(it))
+        print(name, seed, "NMI %.4f iterations %d" % (rec["nmi"][-1], it), flush=True)
+        rec["nmi_mean"] = float(np.mean(rec["nmi"]))
+        rec["nmi_sd"] = float(np.std(rec["nmi"]))
+        with open(path, "w") as f:                  # after every seed: an interrupted run keeps its samples
+            json.dump(rec, f, indent=1)
+    print(name, "%d seeds, mean %.4f sd %.4f" % (len(rec["nmi"]), rec["nmi_mean"], rec["nmi_sd"]))
+
+
 def _c2_worker(seeds):
     fc = load_reference()
     rec = {}
@@ -259,6 +289,10 @@ def main():
         # reference loop does not sit at NMI 1.0 (C3's mu = 0.5 at average degree 8: ~0.956)
         run_c3("louvain", 0.2, list(range(64)))
         run_c3("lpm", 0.8, list(range(32)), mu=0.5, avg_deg=8, max_deg=25, tag="_sparse")
+        return
+    if sys.argv[1:] == ["c3lpm64"]:
+        # round 6: the sparse lpm record extended to 64 reference seeds
+        extend_c3("lfr100k_sparse_lpm_np64", "lpm", 0.8, list(range(64)), avg_deg=8, max_deg=25)
         return
     if sys.argv[1:2] == ["c2"]:
         run_c2_many(int(sys.argv[2]) if len(sys.argv) > 2 else 128)

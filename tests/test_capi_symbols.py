@@ -83,6 +83,9 @@ def test_cpu_twin_defaults_match_engine_defaults():
         assert twin[k].default == v, k
         if k in model:
             assert model[k].default == v, k
-    rounds = int(re.search(r"\bclosure_rounds = (\d+)", src).group(1))
-    assert orc.CLOSURE_ROUNDS == rounds
-    assert inspect.signature(orc.closure_sample_pairs).parameters["rounds"].default == rounds
+    assert int(re.search(r"\bclosure_rounds = (\d+)", src).group(1)) == 0      # 0: per algorithm
+    m = re.search(r"CLOSURE_ROUNDS_LOUVAIN = (\d+), CLOSURE_ROUNDS_LPM = (\d+)", src)
+    assert (orc.CLOSURE_ROUNDS_LOUVAIN, orc.CLOSURE_ROUNDS_LPM) == (int(m.group(1)), int(m.group(2)))
+    assert [orc.closure_rounds(a) for a in (0, 1, 2, 4)] == [int(m.group(1)), int(m.group(2)), int(m.group(1)),
+                                                            int(m.group(2))]
+    assert inspect.signature(orc.closure_sample_pairs).parameters["rounds"].default == orc.CLOSURE_ROUNDS_LOUVAIN

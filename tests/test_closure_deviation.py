@@ -39,7 +39,7 @@ def _measure(name, seeds=8):
         kept = tr["kept"]
         cnt, wmean = [], []
         for s in range(seeds):
-            pairs = orc.closure_sample_pairs(kept, L, s, it)
+            pairs = orc.closure_sample_pairs(kept, L, s, it, orc.closure_rounds(case.algo))
             cu, _, cw, _ = orc.closure_from_pairs(case.algo, kept, pairs, case.cd_batches[it], case.n_p)
             cnt.append(len(cu))
             wmean.append(float(cw.mean()) if len(cw) else 0.0)
@@ -71,7 +71,7 @@ def test_closure_small_graph_printed():
 
 
 def test_blocked_vs_sequential_closure_at_c3():
-    """BASELINE configs[2] scale (LFR n=100k mu=0.5): the engine's blocked sampler (orc.CLOSURE_ROUNDS blocks,
+    """BASELINE configs[2] scale (LFR n=100k mu=0.5): the engine's blocked sampler (orc.CLOSURE_ROUNDS_LOUVAIN blocks,
     orc_closure_sample = the device's, bit for bit) against the reference's SEQUENTIAL sampler
     over the growing graph (orc_closure_sequential: fast_consensus.py:175-184, its distribution
     with the oracle's RNG) on the same post-threshold graph of a 16-replica louvain consensus

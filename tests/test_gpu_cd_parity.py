@@ -315,14 +315,20 @@ def test_c3_consensus_distribution_default_engine(fcmod, request, alg):
     communities (mean of the n_p final partitions, fast_consensus.py:383-392) over 40 device
     seeds against the reference loop's distribution at the same size (orc.refsem_run, the
     golden-pinned loop with the sequential CD restatements and the reference's sequential
-    closure; make_refsem.py c3v2: 64 seeds louvain, 32 lpm), with tests/dist_gates.py's
-    gates (mean >= reference - 0.01)."""
+    closure; make_refsem.py c3v2 / c3lpm64: 64 seeds each), with tests/dist_gates.py's gates:
+    mean >= reference - 0.0005, sd <= 1.3 x, 10th percentile >= reference's - 0.0005 and the
+    one-sided KS test at alpha 0.01 (H1: device NMI stochastically smaller).  Round 5 ran
+    this without KS and a 0.01 mean margin, and the lpm case sat 0.0008 below the reference
+    (KS p ~ 0); the cause was the closure's 4 blocks (lpm's weight-0 closure edges are the
+    next LPA's topology), fixed by 16 blocks for lpm (DESIGN, "Triadic closure")."""
     from tests import dist_gates
     algo, name, tau, graph = C3_CASES[alg]
     n, e, planted = request.getfixturevalue(graph)
     ref = refsem(name)
+    assert len(ref["nmi"]) >= 64
     got = device_runs(fcmod, algo, n, e, 64, tau, 0.02, planted, range(300, 340), nmi_fn=dist_gates.nmi)
-    dist_gates.check(got, ref["nmi"], 0.01, "C3 %s consensus NMI (default engine)" % name, ks=False)
+    dist_gates.check(got, ref["nmi"], 0.0005, "C3 %s consensus NMI (default engine)" % name, ks=True,
+                     p10_slack=0.0005)
 
 
 def test_c3_consensus_nmi_other_engines(fcmod, lfr100k, lfr100k_sparse, engine_opts):
@@ -412,7 +418,7 @@ def test_device_closure_sampler_is_the_measured_one(fcmod, name, pack, monkeypat
         kept = traces[0]["kept"]
         L = graphs[0].m
         nc = eng.closure_sample(L, 0)
-        pairs = orc.closure_sample_pairs(kept, L, seed, 0)
+        pairs = orc.closure_sample_pairs(kept, L, seed, 0, orc.closure_rounds(case.algo))
         cu, cv, cw, cfirst = orc.closure_from_pairs(case.algo, kept, pairs, case.cd_batches[0], case.n_p)
         assert nc == len(cu)
         # the candidates themselves: keys, first attempts (the edge age the adjacency model

@@ -788,7 +788,7 @@ def test_closure_block_api_errors(fcmod):
     with pytest.raises(FastConsensusError):
         eng.closure_block_sample(0, 0, 10, buf)                    # before closure_begin
     blocks = eng.closure_begin(g.m, 0)
-    assert blocks == orc.CLOSURE_ROUNDS                             # the default block count (fc_ctx.h closure_rounds)
+    assert blocks == orc.closure_rounds(0)                          # the default block count (fc_ctx.h closure_blocks)
     t1 = g.m // blocks
     with pytest.raises(FastConsensusError):
         eng.closure_block_sample(1, t1, t1 + 5, buf)               # block 0 not added yet

@@ -12,6 +12,7 @@ deviations can be switched off on the CPU, one at a time, inside the same sharde
     b<k>      k buckets per LPA sweep instead of 32
     noprune   every sweep visits every vertex
     seqclo    the reference's sequential closure sampler instead of the blocked one
+    clo<k>    the blocked sampler in k blocks instead of 4
     seqcd     the sequential LPA restatement (orc_lpa, as refsem) instead of the bucketed twin
     refsem    orc.refsem_run itself (reference loop, sequential CD and closure)
 
@@ -58,6 +59,17 @@ def make_engine(variant, seed):
     if variant == "seqclo":
         def closure_sample(attempts, iteration, eng=eng):
             pairs = orc.closure_sequential_pairs(eng.kept, attempts, eng.seed * 7919 + iteration)
+            dummy = np.zeros((1, eng.g.N), np.int32)
+            cu, cv, _, cf = orc.closure_from_pairs(1, eng.kept, pairs, dummy, 1)
+            order = np.lexsort((cv, cu))
+            eng.cand = (cu[order], cv[order], cf[order])
+            return len(cu)
+        eng.closure_sample = closure_sample
+    if variant.startswith("clo"):                 # clo<k>: the blocked sampler in k blocks
+        k = int(variant[3:])
+
+        def closure_sample(attempts, iteration, eng=eng, k=k):
+            pairs = orc.closure_sample_pairs(eng.kept, attempts, eng.seed, iteration, rounds=k)
             dummy = np.zeros((1, eng.g.N), np.int32)
             cu, cv, _, cf = orc.closure_from_pairs(1, eng.kept, pairs, dummy, 1)
             order = np.lexsort((cv, cu))
