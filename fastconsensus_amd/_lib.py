@@ -24,7 +24,7 @@ ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "EHIP", -4: "ESTATE", -5: "ELIMIT"}
 
 # Every symbol declared in include/fastconsensus_amd.h (checked by tests/test_capi_symbols.py)
 SYMBOLS = [
-    "fc_last_error", "fc_version", "fc_create", "fc_destroy", "fc_set_stream", "fc_synchronize", "fc_set_timing",
+    "fc_last_error", "fc_version", "fc_build_hash", "fc_create", "fc_destroy", "fc_set_stream", "fc_synchronize", "fc_set_timing",
     "fc_collect_timing", "fc_set_params", "fc_set_option", "fc_load_graph", "fc_graph_info", "fc_get_node_map", "fc_reset_graph", "fc_get_graph", "fc_get_nextgraph", "fc_run",
     "fc_cd", "fc_set_labels", "fc_replica_info", "fc_get_labels", "fc_consensus_partial", "fc_consensus_apply",
     "fc_closure_sample", "fc_closure_set_pairs", "fc_closure_begin", "fc_closure_block_sample",
@@ -75,6 +75,7 @@ def load():
     P = ctypes.POINTER
     L.fc_last_error.restype = ctypes.c_char_p
     L.fc_version.restype = ctypes.c_char_p
+    L.fc_build_hash.restype = ctypes.c_char_p
     L.fc_create.argtypes = [c_int, u64, P(vp)]
     L.fc_destroy.argtypes = [vp]
     L.fc_destroy.restype = None

@@ -31,9 +31,12 @@ def _deps():
 
 
 def source_hash():
-    """sha256 (16 hex) over the library's sources and header, by name: what a PMC profile under
-    profiles/ records, so bench.py attaches traffic only from a profile of the same code."""
+    """sha256 (16 hex) over the library's sources and header, by name, and the compile flags and
+    target: what a PMC profile under profiles/ records (bench.py attaches traffic only from a
+    profile of the same code), and what the library embeds (fc_build_hash, compiled into
+    capi.cpp), so a binary built from other sources OR other flags is detected."""
     h = hashlib.sha256()
+    h.update(" ".join(FLAGS + ["--offload-arch=" + ARCH]).encode())
     for d in sorted(_deps(), key=os.path.basename):
         if os.path.isfile(d):
             h.update(os.path.basename(d).encode())
@@ -60,6 +63,8 @@ def _compile(src):
         return obj, False
     lang = ["-x", "hip"] if src.endswith(".hip") else []
     cmd = [HIPCC] + FLAGS + lang + ["-c", path, "-o", obj]
+    if src == "capi.cpp":   # the library reports what it was built from (fc_build_hash)
+        cmd += ['-DFC_BUILD_HASH="%s"' % source_hash()]
     subprocess.check_call(cmd)
     return obj, True
 

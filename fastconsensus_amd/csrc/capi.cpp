@@ -104,6 +104,10 @@ extern "C" {
 
 const char* fc_last_error(void) { return g_err.c_str(); }
 const char* fc_version(void) { return "fastconsensus_amd 0.1.0 (gfx950)"; }
+#ifndef FC_BUILD_HASH
+#define FC_BUILD_HASH "unknown"
+#endif
+const char* fc_build_hash(void) { return FC_BUILD_HASH; }
 
 int fc_create(int device, uint64_t seed, fc_ctx** out) {
     if (!out) { set_error("null out"); return FC_EINVAL; }

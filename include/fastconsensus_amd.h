@@ -92,6 +92,9 @@ typedef struct fc_stats {
 /* ---- lifecycle ---------------------------------------------------------------- */
 const char* fc_last_error(void);
 const char* fc_version(void);
+/* Provenance: the 16-hex hash of the sources, header, compile flags and target the library was
+ * compiled from (fastconsensus_amd/build.py source_hash, embedded at compile time). */
+const char* fc_build_hash(void);
 /* device: HIP ordinal; seed: drives every random choice (CD order/ties, closure). */
 int fc_create(int device, uint64_t seed, fc_ctx** out);
 void fc_destroy(fc_ctx* ctx);
