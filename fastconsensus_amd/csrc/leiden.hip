@@ -366,6 +366,16 @@ __device__ __forceinline__ void wave_scan(const LvArgs& a, int32_t* keys, int32_
     }
 }
 
+#ifndef FC_LV_XCD
+#define FC_LV_XCD 1                     // XCD-contiguous chunks of the Infomap pass lists (A/B switch)
+#endif
+// Block b of a grid of nb -> chunk index, a bijection of [0, nb): the blocks of XCD x = b % 8
+// (the hardware dispatches workgroups round-robin over the 8 XCDs) take the contiguous chunk
+// range that starts at x * (nb / 8) + min(x, nb % 8).
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t nb) {
+    const uint32_t x = b & 7, q = nb >> 3, rem = nb & 7;
+    return x * q + min(x, rem) + (b >> 3);
+}
 // One bucket's decisions.  Each lane owns one union vertex; a wave ballots the eligible
 // ones and decides them one at a time cooperatively: the row over the 64 lanes into an LDS
 // table sized for it (64..LWS slots).  Rows longer than LIGHT go to k_lv_heavy.  Movers are
@@ -394,6 +404,10 @@ __global__ __launch_bounds__(LTB) void k_lv_decide(LvArgs a, int bucket, uint32_
     int64_t x0 = (int64_t)blockIdx.x * LTB + threadIdx.x;
     const bool listed = MODE == MODE_INFO && a.ilist != nullptr;
     if (listed) {
+        // the pass list is replica-major inside a bucket; XCD x (blocks b % 8 == x, round-robin
+        // dispatch) takes one contiguous run of its chunks, so an XCD's L2 serves few replicas'
+        // module and label rows at a time (decide block slots blist / bcnt stay by blockIdx)
+        if (FC_LV_XCD) x0 = (int64_t)xcd_chunk(blockIdx.x, gridDim.x) * LTB + threadIdx.x;
         x0 = x0 < a.icnt ? (int64_t)a.ilist[x0] : a.nU;
     } else if (IMPL && a.bmap) {
         const int64_t loc = (int64_t)(blockIdx.x % a.bpr) * LTB + threadIdx.x;
@@ -1123,42 +1137,43 @@ __global__ __launch_bounds__(LTB) void k_info_codelen(const uint8_t* fin, const 
 // Decisions within a bucket are pure functions of the state before it and the apply's updates
 // are integer atomics, so the order inside a list does not change any result.
 constexpr int ILIST_MAXB = 1024;
+// The pass lists in two passes over contiguous ranges of the union (block k takes [k*span,
+// (k+1)*span)): per-block bucket counts, an exclusive scan of them bucket-major, then each block
+// writes its vertices at its own offsets -- a bucket's list stays in union (replica-major) order
+// up to the order inside one block's range, and no global atomic is shared by the blocks (a
+// block per 256 vertices with one atomic per bucket each was 1.7 ms per pass at LFR-100k:
+// 250 k blocks on 32 hot counters).  cnt: [B][gridDim.x] (+1 for the scan).
 template <bool IMPL>
-__global__ __launch_bounds__(LTB) void k_info_lcount(LvArgs a, int32_t* cnt) {
+__global__ __launch_bounds__(LTB) void k_info_lcount(LvArgs a, int64_t span, int32_t* cnt) {
     __shared__ int32_t h[ILIST_MAXB];
     for (int i = threadIdx.x; i < a.B; i += LTB) h[i] = 0;
     __syncthreads();
-    const int64_t x = (int64_t)blockIdx.x * LTB + threadIdx.x;
-    if (x < a.nU) {
+    const int64_t lo = (int64_t)blockIdx.x * span, hi = min(a.nU, lo + span);
+    for (int64_t x = lo + threadIdx.x; x < hi; x += LTB) {
         const int32_t r = rep_of<IMPL>(a, x);
         if (!a.done[r] && !a.lvdone[r]) atomicAdd(&h[bucket_of(a, r, x)], 1);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < a.B; i += LTB)
-        if (h[i]) atomicAdd(&cnt[i], h[i]);
+    for (int i = threadIdx.x; i < a.B; i += LTB) cnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
 }
-// cnt: the counts (read), cur: per-bucket cursors (zeroed), list: [sum cnt] bucket-major
+// off: the exclusive scan of cnt; list: [sum cnt] bucket-major
 template <bool IMPL>
-__global__ __launch_bounds__(LTB) void k_info_lfill(LvArgs a, const int32_t* cnt, int32_t* cur, int32_t* list) {
-    __shared__ int32_t off[ILIST_MAXB], h[ILIST_MAXB];
-    if (threadIdx.x == 0) {   // B is small (32 by default): one thread scans the counts
-        int32_t s = 0;
-        for (int i = 0; i < a.B; ++i) { off[i] = s; s += cnt[i]; }
-    }
-    for (int i = threadIdx.x; i < a.B; i += LTB) h[i] = 0;
+__global__ __launch_bounds__(LTB) void k_info_lfill(LvArgs a, int64_t span, const int32_t* off, int32_t* list) {
+    __shared__ int32_t base[ILIST_MAXB];
+    for (int i = threadIdx.x; i < a.B; i += LTB) base[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
     __syncthreads();
-    const int64_t x = (int64_t)blockIdx.x * LTB + threadIdx.x;
-    int b = -1, pos = 0;
-    if (x < a.nU) {
+    const int64_t lo = (int64_t)blockIdx.x * span, hi = min(a.nU, lo + span);
+    for (int64_t x = lo + threadIdx.x; x < hi; x += LTB) {
         const int32_t r = rep_of<IMPL>(a, x);
-        if (!a.done[r] && !a.lvdone[r]) { b = bucket_of(a, r, x); pos = atomicAdd(&h[b], 1); }
+        if (!a.done[r] && !a.lvdone[r]) list[atomicAdd(&base[bucket_of(a, r, x)], 1)] = (int32_t)x;
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.B; i += LTB)
-        if (h[i]) h[i] = atomicAdd(&cur[i], h[i]);   // the block's base in bucket i
-    __syncthreads();
-    if (b >= 0) list[off[b] + h[b] + pos] = (int32_t)x;
 }
+// the B bucket sizes (one host read per pass)
+__global__ void k_info_lsizes(int B, int nblk, const int32_t* off, int32_t* icnt) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B) icnt[b] = off[(int64_t)(b + 1) * nblk] - off[(int64_t)b * nblk];
+}
+constexpr int ILIST_BLOCKS = 2048;      // list-build blocks (ranges of the union)
 
 // Buffers (Ctx::lv).
 enum {
@@ -1384,18 +1399,22 @@ static void multilevel(Ctx& c, bool info, int rbegin, int rcount, int n_p_total,
         int32_t* ill = nullptr;
         a.ilist = nullptr;
         if (listed) {
-            int32_t* ilc = I32(B_ILC, 2 * (int64_t)a.B);
+            const int lblk = (int)std::min<int64_t>(ILIST_BLOCKS, nb(nU));
+            const int64_t span = (nU + lblk - 1) / lblk;
+            const int64_t nc = (int64_t)a.B * lblk;
+            int32_t* ilc = I32(B_ILC, 2 * (nc + 1) + a.B);   // counts | their scan | bucket sizes
+            int32_t* ioff = ilc + nc + 1;
+            int32_t* isz = ioff + nc + 1;
             ill = I32(B_ILL, nU);
-            FC_HIP(hipMemsetAsync(ilc, 0, 8 * (size_t)a.B, c.stream));
-            if (impl) {
-                k_info_lcount<true><<<nb(nU), LTB, 0, c.stream>>>(a, ilc);
-                k_info_lfill<true><<<nb(nU), LTB, 0, c.stream>>>(a, ilc, ilc + a.B, ill);
-            } else {
-                k_info_lcount<false><<<nb(nU), LTB, 0, c.stream>>>(a, ilc);
-                k_info_lfill<false><<<nb(nU), LTB, 0, c.stream>>>(a, ilc, ilc + a.B, ill);
-            }
+            if (impl) k_info_lcount<true><<<lblk, LTB, 0, c.stream>>>(a, span, ilc);
+            else k_info_lcount<false><<<lblk, LTB, 0, c.stream>>>(a, span, ilc);
+            FC_HIP(hipMemsetAsync(ilc + nc, 0, sizeof(int32_t), c.stream));
+            exclusive_scan(c, (const int32_t*)ilc, ioff, nc + 1);
+            if (impl) k_info_lfill<true><<<lblk, LTB, 0, c.stream>>>(a, span, ioff, ill);
+            else k_info_lfill<false><<<lblk, LTB, 0, c.stream>>>(a, span, ioff, ill);
+            k_info_lsizes<<<nb(a.B), LTB, 0, c.stream>>>(a.B, lblk, ioff, isz);
             h_icnt.resize(a.B);
-            FC_HIP(hipMemcpyAsync(h_icnt.data(), ilc, 4 * (size_t)a.B, hipMemcpyDeviceToHost, c.stream));
+            FC_HIP(hipMemcpyAsync(h_icnt.data(), isz, 4 * (size_t)a.B, hipMemcpyDeviceToHost, c.stream));
             sync(c);
         }
         int64_t ioff = 0;
