@@ -36,7 +36,8 @@ def source_hash():
     profile of the same code), and what the library embeds (fc_build_hash, compiled into
     capi.cpp), so a binary built from other sources OR other flags is detected."""
     h = hashlib.sha256()
-    h.update(" ".join(FLAGS + ["--offload-arch=" + ARCH]).encode())
+    # the flags without the include path (absolute, so it differs between checkouts)
+    h.update(" ".join([f for f in FLAGS if not f.startswith("-I")] + ["--offload-arch=" + ARCH]).encode())
     for d in sorted(_deps(), key=os.path.basename):
         if os.path.isfile(d):
             h.update(os.path.basename(d).encode())
@@ -59,13 +60,24 @@ def _compile(src):
     path = os.path.join(CSRC, src)
     obj = _obj(src)
     newest = max(os.path.getmtime(d) for d in _deps())
-    if os.path.exists(obj) and os.path.getmtime(obj) >= newest:
+    stamp = obj + ".hash"                       # capi.cpp embeds the source hash (fc_build_hash)
+    fresh = os.path.exists(obj) and os.path.getmtime(obj) >= newest
+    if fresh and src == "capi.cpp":
+        try:
+            with open(stamp) as f:
+                fresh = f.read().strip() == source_hash()
+        except OSError:
+            fresh = False
+    if fresh:
         return obj, False
     lang = ["-x", "hip"] if src.endswith(".hip") else []
     cmd = [HIPCC] + FLAGS + lang + ["-c", path, "-o", obj]
     if src == "capi.cpp":   # the library reports what it was built from (fc_build_hash)
         cmd += ['-DFC_BUILD_HASH="%s"' % source_hash()]
     subprocess.check_call(cmd)
+    if src == "capi.cpp":
+        with open(stamp, "w") as f:
+            f.write(source_hash() + "\n")
     return obj, True
 
 
