@@ -320,6 +320,8 @@ def main():
         r0, r1 = shard(cfg["n_p"], rank, world)
         eng.set_option("store", store_order_pays(r1 - r0, ALGORITHMS[cfg["algo"]],
                                                 int(dict(kv.split("=", 1) for kv in args.opt).get("cd_engine", 2))))
+        from fastconsensus_amd.core import relabel_for
+        eng.set_option("relabel", relabel_for(ALGORITHMS[cfg["algo"]]))
         if args.buckets:
             eng.set_params(buckets=args.buckets)
         for name in ("chunk", "prune", "relabel", "store", "coarsen"):

@@ -203,7 +203,7 @@ int fc_set_option(fc_ctx* ctx, int option, int64_t value) {
             c.chunk = (int)value;
             break;
         case FC_OPT_PRUNE: c.prune = value != 0; break;
-        case FC_OPT_RELABEL: c.relabel = value != 0; break;
+        case FC_OPT_RELABEL: FC_REQUIRE(value >= 0 && value <= 2, FC_EINVAL, "relabel 0, 1 or 2"); c.relabel = (int)value; break;
         case FC_OPT_STORE: c.store_order = value != 0; break;
         case FC_OPT_COARSEN: FC_REQUIRE(value >= 0, FC_EINVAL, "coarsen >= 0"); c.coarsen = (int)value; break;
         case FC_OPT_SEED: c.seed = (uint64_t)value; break;

@@ -98,6 +98,19 @@ int64_t read_i64(Ctx& c, const int64_t* dev) {
 // ------------------------------------------------------------------ ingest kernels
 // Internal numbering sigma[node] (a seeded Feistel bijection, or the identity), its inverse,
 // and the identity label storage (store_order() replaces it).
+// relabel = 2, second ingest: sigma'[node] = spos[sigma[node]] -- the numbering follows the
+// storage order (community order of the one-replica ordering run), the storage is the identity
+__global__ void k_sigma_compose(int64_t n, int32_t* sigma, int32_t* npos, int32_t* spos) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = spos[sigma[i]];
+    sigma[i] = s;
+    npos[s] = (int32_t)i;
+}
+__global__ void k_identity(int64_t n, int32_t* p) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (int32_t)i;
+}
 __global__ void k_sigma(int64_t n, Perm P, int relabel, int32_t* sigma, int32_t* npos, int32_t* spos) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -181,6 +194,9 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
                                           c.relabel ? 1 : 0, sigma, npos, spos);
     int bits = 1;
     while ((int64_t(1) << bits) < n) ++bits;
+    Graph& g = c.g;
+    // canonical keys in the numbering sigma, sort + dedupe, CSR (run twice with relabel = 2)
+    auto ingest = [&]() {
     uint64_t* k1 = ensure<uint64_t>(c.mkey, mm);
     uint64_t* k2 = ensure<uint64_t>(c.mkey2, mm);
     int64_t* i1 = ensure<int64_t>(c.midx, mm);
@@ -195,8 +211,6 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
     mark("upload+keys");
     c.N = n;
     c.key_bits = bits;
-    c.h_sigma.resize(n);
-    FC_HIP(hipMemcpyAsync(c.h_sigma.data(), sigma, 4 * n, hipMemcpyDeviceToHost, c.stream));
     sort_pairs(c, k1, k2, i1, i2, m, 2 * bits);
     k_unique_flags<<<nblk(m), TB, 0, c.stream>>>(m, k2, bits, fl);
     exclusive_scan(c, fl, ps, m);
@@ -209,7 +223,6 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
         last_flag = c.hpin[1];
     }
     int64_t mu = last_pos + last_flag;
-    Graph& g = c.g;
     g.m = mu;
     int64_t cap = mu > 0 ? mu : 1;
     ensure<int32_t>(g.eu, cap); ensure<int32_t>(g.ev, cap); ensure<int32_t>(g.ew, cap); ensure<int64_t>(g.eage, cap);
@@ -220,7 +233,32 @@ void graph_load(Ctx& c, int64_t n, int64_t m, const int32_t* u, const int32_t* v
     graph_build_csr(c, g);
     slot_maps(c);        // identity storage (the ordering pass below runs on it)
     mark("csr");
-    if (c.store_order && g.M2 > 0) {
+    };
+    ingest();
+    if (c.relabel == 2 && g.M2 > 0) {
+        // FC_OPT_RELABEL = 2: the internal numbering in community order (the storage-order run's
+        // communities), for kernels that gather neighbour state by internal id -- Infomap's
+        // union levels (leiden.hip), whose buckets are hashes of the id, not chunks of the visit
+        // order (cd.hip / cd_rl.hip need a random numbering: chunked visit orders would put
+        // neighbours in one bucket).  The storage is the identity afterwards.
+        store_order(c);
+        sigma = ensure<int32_t>(c.sigma, n);
+        npos = ensure<int32_t>(c.npos, n);
+        spos = ensure<int32_t>(c.spos, n);
+        k_sigma_compose<<<nblk(n), TB, 0, c.stream>>>(n, sigma, npos, spos);
+        k_identity<<<nblk(n), TB, 0, c.stream>>>(n, spos);
+        du = ensure<int32_t>(c.cu, mm);
+        dv = ensure<int32_t>(c.cv, mm);
+        if (m > 0) {   // the ordering run may have reused the upload buffers: upload again
+            FC_HIP(hipMemcpyAsync(du, u, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+            FC_HIP(hipMemcpyAsync(dv, v, sizeof(int32_t) * m, hipMemcpyHostToDevice, c.stream));
+        }
+        ingest();
+        mark("relabel");
+    }
+    c.h_sigma.resize(n);
+    FC_HIP(hipMemcpyAsync(c.h_sigma.data(), sigma, 4 * n, hipMemcpyDeviceToHost, c.stream));
+    if (c.store_order && c.relabel != 2 && g.M2 > 0) {
         store_order(c);
         graph_slots(c, g);
     }

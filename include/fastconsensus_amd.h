@@ -120,7 +120,11 @@ int fc_set_params(fc_ctx* ctx, int buckets, int max_sweeps, int max_iters);
 #define FC_OPT_MAX_ITERS 3   /* cap on consensus iterations (default 1000)                  */
 #define FC_OPT_CHUNK 4       /* CD visit order granularity: 0 per vertex, 16 (default) chunks */
 #define FC_OPT_RELABEL 6     /* 1 (default): engine-internal random vertex numbering (set it
-                                before fc_load_graph); results are reported in node order     */
+                                before fc_load_graph); results are reported in node order.
+                                2: numbered in community order (a one-replica Louvain run at
+                                load), for infomap runs, whose union levels gather neighbour
+                                state by internal id (louvain / lpm need the random numbering:
+                                their visit orders are chunks of consecutive ids).  0: identity */
 #define FC_OPT_PRUNE 5       /* 1 (default): once a sweep moves < n/4 vertices, later sweeps visit only vertices with a moved
                                 neighbour (GVE-Louvain-style pruning); 0: every vertex       */
 #define FC_OPT_TAIL_VISITS 7 /* once no replica visits more than this many vertices in a sweep,

@@ -573,7 +573,8 @@ def test_closure_sampler_properties(fcmod):
                          [(0, 10, 0.2, 0, 0, 0, 0), (0, 12, 0.2, 16, 0, 1, 16384), (1, 4, 0.8, 0, 0, 0, 16384),
                           (0, 20, 0.2, 0, 0, 1, 0), (0, 10, 0.2, 0, 1, 1, 16384), (1, 6, 0.8, 16, 1, 1, 0),
                           (1, 6, 0.8, 16, 1, 1, 16384), (0, 10, 0.2, 16, 1, 1, 0), (0, 10, 0.2, 16, 1, 1, 16384),
-                          (2, 10, 0.2, 16, 1, 1, 16384), (2, 12, 0.2, 0, 0, 0, 0)])
+                          (2, 10, 0.2, 16, 1, 1, 16384), (2, 12, 0.2, 0, 0, 0, 0),
+                          (0, 10, 0.2, 16, 1, 2, 0), (1, 6, 0.8, 16, 1, 2, 16384)])
 @pytest.mark.parametrize("engine", ENGINES)
 def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel, tail, engine):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same

@@ -215,6 +215,39 @@ def test_infomap_one_replica_empty_bucket_lists(fcmod, graph):
 
 
 @pytest.mark.gpu
+def test_infomap_community_ordered_numbering(fcmod):
+    """FC_OPT_RELABEL = 2 (the numbering infomap runs use, core.relabel_for): the internal ids
+    follow the communities of a one-replica ordering run -- a bijection, neighbours mostly
+    numbered close together -- and the device Infomap on it stays within the tolerances of
+    test_infomap_lfr1k_vs_restatement (mean codelength within 0.5 %, NMI >= restatement - 0.02);
+    a whole infomap run on it equals the sharded driver's."""
+    from fastconsensus_amd.distributed import run_sharded
+    n, e, planted = lfr(1000, 0.4)
+    g = orc.EdgeGraph.from_lines(n, e)
+    with fcmod.Engine(seed=11) as eng:
+        eng.set_option("relabel", 2)
+        eng.load_graph(n, e[:, 0], e[:, 1])
+        sigma = eng.node_map()
+        assert np.array_equal(np.sort(sigma), np.arange(n))
+        gap = np.median(np.abs(sigma[e[:, 0]] - sigma[e[:, 1]]))
+        eng.cd(4, 0, 16, 16, 0)
+        dev = eng.get_labels(16)
+        eng.set_option("infomap_trials", 2)
+        labels, st = eng.run(4, 8, 0.6, 0.02)
+        sh, st2 = run_sharded(eng, 4, 8, 0.6, 0.02)
+    ref = [orc.infomap(g, seed=s)[0] for s in range(8)]
+    Ld = np.mean([codelength(n, e, x) for x in dev])
+    Lr = np.mean([codelength(n, e, x) for x in ref])
+    nd = np.mean([nmi(planted, x) for x in dev])
+    nr = np.mean([nmi(planted, x) for x in ref])
+    print("relabel 2: median neighbour id gap %d (random numbering ~%d); L %.4f vs %.4f, NMI %.4f vs %.4f"
+          % (gap, n // 3, Ld, Lr, nd, nr))
+    assert gap < n // 10
+    assert abs(Ld - Lr) <= 0.005 * Lr and nd >= nr - 0.02
+    assert np.array_equal(labels, sh) and st2["iterations"] == st["iterations"]
+
+
+@pytest.mark.gpu
 def test_infomap_sharding_independent_and_deterministic(fcmod):
     n, e, _ = lfr(1000, 0.4)
     full = device_infomap(fcmod, n, e, 6, seed=99, trials=3)

@@ -24,11 +24,15 @@ def child(lib, config, reps):
     import fastconsensus_amd as fc
     from fastconsensus_amd import core
     cfg = dict(bench.CONFIGS[config])
-    n, u, v, _ = bench.make_graph(cfg, 42)
+    n, u, v, planted = bench.make_graph(cfg, 42)
     algo = core.algo_id(cfg["algo"])
     host = np.zeros((cfg["n_p"], n), np.int32)
     out = {"lib": lib, "config": config}
     with fc.Engine(seed=42) as eng:
+        # FC_AB_OPTS="name=value;...": engine options of this variant (fc_set_option)
+        for kv in filter(None, os.environ.get("FC_AB_OPTS", "").split(";")):
+            k, _, val = kv.partition("=")
+            eng.set_option(k, int(val))
         eng.load_graph(n, u, v)
         eng.run(algo, cfg["n_p"], cfg["tau"], cfg["delta"], out=host)      # warm
         runs = []
@@ -40,6 +44,19 @@ def child(lib, config, reps):
         out["run_ms"] = min(runs)
         out["runs_ms"] = [round(x, 1) for x in runs]
         out["labels_sha"] = hashlib.sha1(host.tobytes()).hexdigest()[:16]
+        # quality of one CD batch on the input graph (variants that change the random streams
+        # are compared by it): mean NMI to the planted communities, and for infomap the mean
+        # two-level codelength
+        from tests import dist_gates
+        eng.reset_graph()
+        eng.cd(algo, 0, 8, 8, 0)
+        lab = eng.get_labels(8)
+        out["cd_nmi"] = round(float(np.mean([dist_gates.nmi(planted, x) for x in lab])), 5)
+        if cfg["algo"] == "infomap":
+            from tests.test_infomap import codelength
+            e = np.stack([u, v], 1).astype(np.int64)
+            out["cd_codelength"] = round(float(np.mean([codelength(n, e, x) for x in lab])), 5)
+        out["final_nmi"] = round(float(np.mean([dist_gates.nmi(planted, x) for x in host[:8]])), 5)
     print(json.dumps(out), flush=True)
 
 
