@@ -151,7 +151,7 @@ void fc_destroy(fc_ctx* ctx) {
                       &c.cage, &c.deg_next, &c.iso, &c.isoflag, &c.target, &c.tw, &c.active, &c.active2,
                       &c.hit, &c.mkey, &c.mkey2, &c.midx, &c.midx2, &c.sort_tmp, &c.nodetmp, &c.nodetmp2,
                       &c.nodetmp3, &c.part, &c.ccount, &c.tailbuf, &c.tailmark, &c.sigma, &c.npos, &c.spos, &c.sinv, &c.tpos, &c.snpos, &c.st_u, &c.st_v, &c.st_w, &c.st_age,
-                      &c.st_lab, &c.clo_rec, &c.clo_hkey, &c.clo_hval, &c.clo_list, &c.clo_cnt, &c.clo_akey, &c.clo_aval, &c.clo_rowptr, &c.clo_col, &c.clo_rowptr2, &c.clo_col2, &c.clo_nrow, &c.clo_ncol, &c.mvf};
+                      &c.st_lab, &c.clo_rec, &c.clo_hkey, &c.clo_hval, &c.clo_list, &c.clo_cnt, &c.clo_akey, &c.clo_aval, &c.clo_rowptr, &c.clo_col, &c.clo_rowptr2, &c.clo_col2, &c.clo_nrow, &c.clo_ncol, &c.clo_own, &c.clo_own2, &c.mvf};
     for (auto* b : bufs) b->release();
     for (auto e : c.timer.pool) (void)hipEventDestroy(e);
     for (auto e : c.sweep_ev) (void)hipEventDestroy(e);

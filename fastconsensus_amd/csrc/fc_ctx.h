@@ -173,7 +173,7 @@ struct Ctx {
     // 2^31 entries; FC_CLO_PACK=0 lets the tests run it at small sizes)
     int clo_pack = getenv("FC_CLO_PACK") ? atoi(getenv("FC_CLO_PACK")) : 1;
     DevBuf clo_hkey, clo_hval, clo_list, clo_cnt, clo_akey, clo_aval, clo_rowptr, clo_col, clo_rowptr2, clo_col2,
-        clo_nrow, clo_ncol;
+        clo_nrow, clo_ncol, clo_own, clo_own2;
     int closure_rounds = 0;         // FC_OPT_CLOSURE_ROUNDS; 0 = per algorithm (closure_blocks below)
     int clo_algo = 0;               // algorithm of the last consensus_apply (the kept graph the closure samples)
     // sharded closure (fc_closure_begin / _block_sample / _block_add / _finish): the run's
