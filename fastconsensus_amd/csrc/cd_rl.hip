@@ -662,6 +662,97 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
     return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
 }
 
+// ---- one unit per wave (LG = 64: every lane deciding the same vertex, VPW = 1; C4 / C5) ----
+// The unit's record and row are wave-uniform, so the row is not K per-lane broadcast loads:
+// lane j holds entry j of the NEXT item's row (one coalesced load issued an item ahead, in
+// flight while this item sorts), and the label gathers take each neighbour id with a
+// readlane -- a scalar row base (saddr) plus the lane's replica offset, no per-entry address
+// arithmetic and the neighbour-id stage off the item's dependent chain.  Same decisions.
+struct RowPre {
+    int32_t col;                 // lane j: entry j's neighbour id (colw: id << wbits | weight)
+    int32_t w;                   // WM_WIDE: entry j's weight
+    int32_t own;                 // this lane's label of the unit's vertex
+};
+__device__ __forceinline__ Rec rl_fetch_u(const RL& a, const Unit& u) {
+    Rec r = rl_fetch(a, u);      // every lane fetched the same record: make that visible
+    r.e.x = __builtin_amdgcn_readfirstlane(r.e.x);
+    r.e.y = __builtin_amdgcn_readfirstlane(r.e.y);
+    r.e.z = __builtin_amdgcn_readfirstlane(r.e.z);
+    r.e.w = __builtin_amdgcn_readfirstlane(r.e.w);
+    r.msk = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(r.msk >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)r.msk);
+    return r;
+}
+template <int WM>
+__device__ __forceinline__ RowPre rl_row_pre(const RL& a, const Unit& u, const Rec& r) {
+    RowPre p;
+    p.col = 0; p.w = 0; p.own = 0;
+    const uint32_t lane = threadIdx.x & 63;
+    if (r.e.x >= 0) {            // u.valid (uniform)
+        const int d = r.e.z;
+        if (d > 0 && d <= DM) {  // lanes past the row repeat entry 0 (same line; masked by the decide)
+            const uint32_t j = lane < (uint32_t)d ? lane : 0u;
+            p.col = ld_off(WM == WM_W8 ? a.colw : a.col, (uint32_t)r.e.y + j);
+            if (WM == WM_WIDE) p.w = ld_off(a.cw, (uint32_t)r.e.y + j);
+        }
+        p.own = ld_off(a.lab, (uint32_t)r.e.x * (uint32_t)a.ldT + (uint32_t)(u.bank * 64) + lane);
+    }
+    return p;
+}
+template <bool LOUV, int K, int WM>
+__device__ __forceinline__ int32_t rl_sorted_u1(const RL& a, const Hdr& h, int sweep, const RowPre& pre,
+                                                unsigned long long& c_dq, uint32_t& c_unst, uint32_t& c_cand,
+                                                bool& slow_out) {
+    constexpr bool UNITW = WM == WM_UNIT;
+    slow_out = false;
+    const uint32_t rr = (uint32_t)h.rr, ldT = (uint32_t)a.ldT;
+    const int wb = UNITW ? 0 : a.wbits;
+    const int32_t wm = (1 << wb) - 1;
+    const bool wk = h.work;
+    const int ds = h.ds;                                        // wave-uniform: the row's length or 0
+    if (ds == 0) return -1;                                     // past the list, heavy, idle unit, empty row
+    const uint32_t home = (uint32_t)h.v * ldT + rr;
+    const int32_t own = wk ? pre.own : -1;
+    int32_t x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        // entries past the row repeat entry 0 (same line, a hit) and are masked below
+        const int32_t cj = __builtin_amdgcn_readlane(pre.col, j);
+        const uint32_t id = (uint32_t)(WM == WM_W8 ? (cj >> wb) : cj);
+        x[j] = ld_off(a.lab, id * ldT + rr);                    // id * ldT scalar: one VALU add per entry
+    }
+    int32_t tot_own = 0;
+    if (LOUV) {
+        const int32_t t0 = ld_off(a.tot, wk ? (uint32_t)own * ldT + rr : home);
+        tot_own = wk ? t0 : 0;
+    }
+    long long kown = 0;
+    int ko = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const bool live = wk && j < ds;
+        int32_t wj = 1;
+        if (WM == WM_W8) wj = __builtin_amdgcn_readlane(pre.col, j) & wm;
+        else if (WM == WM_WIDE) wj = __builtin_amdgcn_readlane(pre.w, j);
+        const bool mine = (LOUV || FC_RL_LPA_OWN) && live && x[j] == own;
+        ko += mine ? wj : 0;
+        x[j] = (mine || !live) ? -1 : (UNITW ? x[j] : ((x[j] << wb) | wj));
+    }
+    kown = ko;
+    if (LOUV) {
+        const long long kvl = h.kvi;
+        const bool settled = !wk || (kvl - 2 * kown) * a.M2 + kvl * ((long long)tot_own - kvl) <= 0;
+        if (__ballot(!settled) == 0) return -1;                 // wave-uniform
+    } else if (FC_RL_LPA_OWN) {
+        const bool settled = !wk || 2 * kown > (long long)ds;
+        if (__ballot(!settled) == 0) {
+            if (wk) c_cand += 1u;                               // the own label, the one candidate
+            return -1;
+        }
+    }
+    return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
+}
+
 // Light rows with sortable keys (label and weight fit 31 bits): no LDS, one sorting network
 // per lane, K chosen per wave from its longest row.
 // Append the wave's slow visits to the exact kernel's list (one atomic per wave).
@@ -682,8 +773,12 @@ __device__ __forceinline__ void rl_push_slow(const RL& a, bool slow, int64_t e, 
 #ifndef FC_RLW32
 #define FC_RLW32 1
 #endif
-template <bool LOUV, int K, int WM>
-__global__ __launch_bounds__(RTB) __attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 32 ? FC_RLW32 : 1)))
+template <bool LOUV, int K, int WM, bool U1>
+#ifndef FC_RLW32U
+#define FC_RLW32U 4
+#endif
+__global__ __launch_bounds__(RTB)
+__attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 32 ? (U1 ? FC_RLW32U : FC_RLW32) : 1)))
 void k_rl_decide(RL a, int seg, int sweep) {
     const int lane = threadIdx.x & 63;
     const int64_t e0 = a.boff[seg], e1 = a.boff[seg + 1];
@@ -709,17 +804,33 @@ void k_rl_decide(RL a, int seg, int sweep) {
         c_dq = 0;
         c_unst = c_vis = c_ent = c_cand = c_units = 0;
     };
-    Rec nxt = rl_fetch(a, rl_unit(a, e0, e1, blockIdx.x));
+    // records two items ahead; U1: the next item's row and own labels one item ahead
+    Rec nxt = U1 ? rl_fetch_u(a, rl_unit(a, e0, e1, blockIdx.x)) : rl_fetch(a, rl_unit(a, e0, e1, blockIdx.x));
+    Rec nx2 = nxt;
+    RowPre pre;
+    pre.col = pre.w = pre.own = 0;
+    if constexpr (U1) {
+        pre = rl_row_pre<WM>(a, rl_unit(a, e0, e1, blockIdx.x), nxt);
+        nx2 = rl_fetch_u(a, rl_unit(a, e0, e1, (int64_t)blockIdx.x + gridDim.x));
+    }
     for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
         const Unit u = rl_unit(a, e0, e1, w);
         if (a.banks > 1 && u.r != last_r) flush(last_r);
         last_r = a.banks > 1 ? u.r : (lane & (LG - 1));
         const Rec cur = nxt;
-        nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
+        RowPre pc = pre;
+        if constexpr (U1) {
+            nxt = nx2;
+            pre = rl_row_pre<WM>(a, rl_unit(a, e0, e1, w + gridDim.x), nxt);   // in flight while this item runs
+            nx2 = rl_fetch_u(a, rl_unit(a, e0, e1, w + 2 * (int64_t)gridDim.x));
+        } else {
+            nxt = rl_fetch(a, rl_unit(a, e0, e1, w + gridDim.x));   // in flight while this item runs
+        }
         const Hdr h = rl_header(a, u, cur);
         bool slow;
         const uint32_t cc0 = c_cand;
-        const int32_t dcs = rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
+        const int32_t dcs = U1 ? rl_sorted_u1<LOUV, K, WM>(a, h, sweep, pc, c_dq, c_unst, c_cand, slow)
+                               : rl_sorted<LOUV, K, WM>(a, h, sweep, c_dq, c_unst, c_cand, slow);
         rl_push_slow(a, slow, u.e, h.rr);
         // LPA: the visit's candidates are the labels at the top count (rl_runs adds them to
         // c_cand; a settled lane adds 1), so >= 2 of them is a tie.  Read off the counter rather
@@ -788,12 +899,12 @@ __global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
 // generations of 4-5 items, the last one on two thirds of the SIMDs.  LPA keeps the 8192 cap:
 // its items' cost varies more (most waves settled, a few sorting) and the extra blocks balance
 // it (SBM-4M 687 vs 695 ms).
-template <bool LOUV, int K, int WM>
+template <bool LOUV, int K, int WM, bool U1>
 static int64_t rl_decide_slots() {
     static int64_t slots = 0;
     if (!slots) {
         int nb = 0, dev = 0;
-        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM>, RTB, 0));
+        FC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_rl_decide<LOUV, K, WM, U1>, RTB, 0));
         FC_HIP(hipGetDevice(&dev));
         int cus = 0;
         FC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1165,25 +1276,50 @@ __global__ __launch_bounds__(RTB) void k_rl_apply(RL a, int k) {
         moves = 0;
     };
     const uint64_t gmask = LG == 64 ? ~0ull : ((1ull << LG) - 1ull);
-    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+    // items pipelined: entry record and decision two items ahead, the mover's old label one
+    // ahead (a wave's items were a chain list -> decision -> label -> atomics each)
+    struct Ap {
+        int4 er;
+        uint64_t msk;
+        int32_t t;
+    };
+    auto fetch = [&](int64_t w) {
+        Ap p;
+        p.er = make_int4(-1, 0, 0, 0);
+        p.msk = 0;
+        p.t = -1;
+        const Unit u = rl_unit(a, e0, e1, w);
+        if (u.valid) {
+            p.er = a.list[u.e];
+            p.msk = a.lmask[u.e * a.banks + u.bank];
+            if (u.r < a.n_r) p.t = a.dec[u.e * a.ldT + u.r];   // every visit slot was written (-1: none)
+        }
+        return p;
+    };
+    auto old_of = [&](const Ap& p, int64_t w) -> int32_t {
+        const Unit u = rl_unit(a, e0, e1, w);
+        const bool mv = u.valid && ((p.msk >> u.rl) & 1ull) && p.t >= 0;
+        return mv ? a.lab[(int64_t)p.er.x * a.ldT + u.r] : -1;
+    };
+    const int64_t G = gridDim.x;
+    Ap p1 = fetch(blockIdx.x), p2 = fetch(blockIdx.x + G);
+    int32_t o1 = old_of(p1, blockIdx.x);
+    for (int64_t w = blockIdx.x; w < items; w += G) {
         const Unit u = rl_unit(a, e0, e1, w);
         if (a.banks > 1 && u.r != last_r) flush(last_r);
         last_r = a.banks > 1 ? u.r : (lane & (LG - 1));
         const int rr = u.r;
-        int32_t t = -1, v = -1, kvr = 0;
-        int4 er = make_int4(-1, 0, 0, 0);
-        if (u.valid) {
-            er = a.list[u.e];
-            v = er.x;
-            kvr = er.w;
-            const uint64_t msk = a.lmask[u.e * a.banks + u.bank];
-            if (rr < a.n_r && ((msk >> u.rl) & 1ull)) t = a.dec[u.e * a.ldT + rr];
-        }
+        const Ap cur = p1;
+        const int32_t old = o1;
+        p1 = p2;
+        o1 = old_of(p1, w + G);
+        p2 = fetch(w + 2 * G);
+        const int4 er = cur.er;
+        const int32_t v = er.x, kvr = er.w;
+        const int32_t t = (u.valid && ((cur.msk >> u.rl) & 1ull)) ? cur.t : -1;
         const bool moved = t >= 0;
         if (moved) {
-            const int64_t lrow = (int64_t)v * a.ldT + rr;
-            const int32_t old = a.lab[lrow];
-            a.lab[lrow] = t;
+            a.lab[(int64_t)v * a.ldT + rr] = t;
             if (LOUV) {
                 atomicAdd(&a.tot[(int64_t)old * a.ldT + rr], -kvr);
                 atomicAdd(&a.tot[(int64_t)t * a.ldT + rr], kvr);
@@ -1595,6 +1731,8 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             exclusive_scan(c, (const int32_t*)nvv, nvv + n_ent + 1, n_ent);
             k_rl_visits_fill<<<nb(n_ent, LTB), LTB, 0, c.stream>>>(a, n_ent, nvv + n_ent + 1);
         }
+        // one unit per wave: rows read as wave-uniform, an item ahead (rl_sorted_u1)
+        const bool u1 = VPW == 1 && c.rl_u1;
         auto grid_of = [&](int64_t n) {
             const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
             return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
@@ -1625,15 +1763,16 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     const int64_t n = hb[seg + 1] - hb[seg];
                     if (n <= 0) continue;
                     const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
-#define RL_LAUNCH(L, KK, U)                                                                                        \
+#define RL_LAUNCH_1(L, KK, U, U1)                                                                                  \
     do {                                                                                                           \
         const unsigned grid = (c.rl_grid_mul > 0 && L)                                                             \
-            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U>() * c.rl_grid_mul)) \
+            ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U, U1>() * c.rl_grid_mul)) \
             : grid_of(n);                                                                                          \
         const int ev = timer_begin(c);                                                                             \
-        k_rl_decide<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                          \
+        k_rl_decide<L, KK, U, U1><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                      \
         timer_end(c, 7, ev);                                                                                       \
     } while (0)
+#define RL_LAUNCH(L, KK, U) do { if (u1) RL_LAUNCH_1(L, KK, U, true); else RL_LAUNCH_1(L, KK, U, false); } while (0)
 #define RL_LAUNCH_K(L, U) \
     do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
@@ -1642,6 +1781,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
                     else RL_LAUNCH_K(false, WM_UNIT);
 #undef RL_LAUNCH_K
 #undef RL_LAUNCH
+#undef RL_LAUNCH_1
                 }
             } else {
                 const int64_t n = hb[k * NCLS + NCLS - 1] - hb[k * NCLS];

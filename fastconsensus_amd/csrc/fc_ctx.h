@@ -223,6 +223,9 @@ struct Ctx {
     fc_stats acc{};                 // accumulated during a run (fc_run)
     fc_stats prof{};                // accumulated since the last fc_collect_timing
     int64_t* hpin = nullptr;        // pinned host scratch (FC_HPIN_I64 int64)
+    // cd_rl.hip decide with one unit per wave (64 local replicas or more): the row as one
+    // coalesced load an item ahead, neighbour ids by readlane (A/B switch; same decisions)
+    int rl_u1 = getenv("FC_RL_U1") ? atoi(getenv("FC_RL_U1")) : 1;
 };
 
 struct Ctx;

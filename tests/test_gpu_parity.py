@@ -419,6 +419,40 @@ def _weighted_consensus_engine(fcmod, seed):
     return case, eng
 
 
+@pytest.mark.parametrize("u1", ["0", "1"])
+@pytest.mark.parametrize("n_r", [64, 70])
+def test_cd_replica_lanes_wide_weights_bit_exact(fcmod, n_r, u1, monkeypatch):
+    """Consensus weights past 8 bits (300 labelings: weights up to 300) take the replica-lane
+    decide's separate weight row (WM_WIDE); with >= 64 local replicas one unit per wave, its row
+    read an item ahead (FC_RL_U1=1) or per lane (0): both bit-exact against the twin."""
+    monkeypatch.setenv("FC_RL_U1", u1)
+    case = golden_io.load("lfr1k_louvain_np20")
+    eng = fcmod.Engine(seed=53)
+    e = case.edges_file
+    eng.load_graph(case.N, e[:, 0], e[:, 1])
+    n_w = 300
+    eng.set_labels(np.tile(case.cd_batches[0], (n_w // case.n_p, 1)))
+    part = dev_i32(eng.m)
+    eng.consensus_partial(0, part)
+    eng.consensus_apply(0, n_w, case.tau, case.delta, part)
+    nc = eng.closure_set_pairs(case.pair_batches[0], 0)
+    cnt = dev_i32(nc)
+    eng.closure_partial(cnt)
+    eng.closure_apply(0, n_w, case.delta, cnt, 0)
+    eng.set_option("cd_engine", 1)
+    u, v, w, _ = eng.get_graph()
+    assert w.max() >= 256, "no weight past 8 bits"
+    sigma = eng.node_map()
+    a_, b_ = sigma[u], sigma[v]
+    lo, hi = np.minimum(a_, b_), np.maximum(a_, b_)
+    o = np.lexsort((hi, lo))
+    g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
+    eng.cd(0, 0, n_r, n_r, 3)
+    exp, _ = orc.engine_cd(0, g_int, n_r, 0, 3, 53, shared=1, coarsen=0)
+    np.testing.assert_array_equal(eng.get_labels(n_r), exp[:, sigma])
+    eng.close()
+
+
 @pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("coarsen", [0, 8])
 @pytest.mark.parametrize("tail", TAILS)
@@ -574,7 +608,9 @@ def test_closure_sampler_properties(fcmod):
                           (0, 20, 0.2, 0, 0, 1, 0), (0, 10, 0.2, 0, 1, 1, 16384), (1, 6, 0.8, 16, 1, 1, 0),
                           (1, 6, 0.8, 16, 1, 1, 16384), (0, 10, 0.2, 16, 1, 1, 0), (0, 10, 0.2, 16, 1, 1, 16384),
                           (2, 10, 0.2, 16, 1, 1, 16384), (2, 12, 0.2, 0, 0, 0, 0),
-                          (0, 10, 0.2, 16, 1, 2, 0), (1, 6, 0.8, 16, 1, 2, 16384)])
+                          (0, 10, 0.2, 16, 1, 2, 0), (1, 6, 0.8, 16, 1, 2, 16384),
+                          # 64 replicas: one unit per wave in the replica-lane decide (rl_sorted_u1)
+                          (0, 64, 0.2, 16, 1, 1, 0), (1, 64, 0.8, 16, 1, 1, 0)])
 @pytest.mark.parametrize("engine", ENGINES)
 def test_full_run_bit_exact_vs_cpu_model(fcmod, algo, n_p, tau, chunk, prune, relabel, tail, engine):
     """fc_run on the device == the oracle-backed CPU model of the engine driven by the same
