@@ -61,9 +61,14 @@ constexpr int SLOW_GRID = 256;         // k_rl_exact blocks for the slow visits 
 constexpr int LTB = 256;                // list kernels
 constexpr int LPER = 8;                 // vertices per thread in the list kernels
 // Degree classes of a bucket's entries (the list is bucket-major, class-minor): rows of <= 16,
-// <= 32, <= DM entries are decided by sorting networks of that width, longer ones by k_rl_exact.
-constexpr int NCLS = 4;
-__host__ __device__ __forceinline__ int rl_class(int d) { return d <= 16 ? 0 : d <= 32 ? 1 : d <= DM ? 2 : 3; }
+// <= 24, <= 32, <= 48, <= DM entries are decided by sorting networks of that width (24 and 48:
+// the 32- and 64-input odd-even merge networks without the comparators past the width, 132 and
+// 384 compare-exchanges against 191 and 543), longer ones by k_rl_exact.  LFR-1M (tau1 = 3,
+// degrees ~19..50): ~44 % of the rows have 19..24 entries and ~23 % 33..48.
+constexpr int NCLS = 6;
+__host__ __device__ __forceinline__ int rl_class(int d) {
+    return d <= 16 ? 0 : d <= 24 ? 1 : d <= 32 ? 2 : d <= 48 ? 3 : d <= DM ? 4 : 5;
+}
 
 struct RL {
     int64_t N, S, PN;
@@ -502,11 +507,13 @@ __device__ __forceinline__ int32_t rl_runs(const RL& a, const Hdr& h, int sweep,
             int32_t tq[SB];
 #pragma unroll
             for (int i = 0; i < SB; ++i) {                     // non-candidates read the lane's own slot (a hit)
+                if (c0 + i >= K) break;                        // K = 24: the last batch is half
                 const bool b = (bits >> i) & 1u;
                 tq[i] = ld_off(a.tot, b ? (uint32_t)(x[c0 + i] >> wb) * ldT + rr : home);
             }
 #pragma unroll
             for (int i = 0; i < SB; ++i) {
+                if (c0 + i >= K) break;
                 const bool b = (bits >> i) & 1u;
                 const uint32_t hh = hash32(tvh ^ (uint32_t)(x[c0 + i] >> wb));
                 const uint64_t key = ((uint64_t)(kv ? (uint32_t)tq[i] : 0u) << 32) | (uint32_t)~hh;
@@ -777,11 +784,15 @@ template <bool LOUV, int K, int WM, bool U1>
 #ifndef FC_RLW32U
 #define FC_RLW32U 4
 #endif
+#ifndef FC_RLW24U
+#define FC_RLW24U 4
+#endif
 __global__ __launch_bounds__(RTB)
-__attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 32 ? (U1 ? FC_RLW32U : FC_RLW32) : 1)))
-void k_rl_decide(RL a, int seg, int sweep) {
+__attribute__((amdgpu_waves_per_eu(K <= 16 ? FC_RLW16 : K <= 24 ? (U1 ? FC_RLW24U : FC_RLW32) :
+                                   K <= 32 ? (U1 ? FC_RLW32U : FC_RLW32) : 1)))
+void k_rl_decide(RL a, int seg, int ns, int sweep) {
     const int lane = threadIdx.x & 63;
-    const int64_t e0 = a.boff[seg], e1 = a.boff[seg + 1];
+    const int64_t e0 = a.boff[seg], e1 = a.boff[seg + ns];   // degree classes seg .. seg + ns - 1
     const int64_t items = rl_items(a, e1 - e0);
     const int LG = a.LG;
     unsigned long long c_dq = 0;                                // 32-bit counts: one block's items
@@ -853,8 +864,8 @@ void k_rl_decide(RL a, int seg, int sweep) {
 // sparse sweeps where most replicas of an entry are idle and a wave per entry would run mostly
 // empty lanes.  Same decision code; counters go straight to the per-replica shards.
 template <bool LOUV, int K, int WM>
-__global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int sweep) {
-    const int64_t v0 = a.voff[seg], v1 = a.voff[seg + 1];
+__global__ __launch_bounds__(RTB) void k_rl_decide_v(RL a, int seg, int ns, int sweep) {
+    const int64_t v0 = a.voff[seg], v1 = a.voff[seg + ns];
     for (int64_t base = (int64_t)blockIdx.x * 64; base < v1 - v0; base += (int64_t)gridDim.x * 64) {
         const int64_t i = base + (threadIdx.x & 63);
         const bool valid = i < v1 - v0;
@@ -1577,7 +1588,7 @@ static bool cd_rl_fits(const Ctx& c, int algo) {
     // int32 community totals (louvain only: LPA ignores the weights, so a heavily weighted
     // consensus graph -- 2M past 2^31 at SBM-4M, n_p = 128 -- still fits its label propagation);
     // the sweep record (boff | voff | n_active, one pinned DMA per sweep) must fit the pinned
-    // scratch: B * NCLS segments, i.e. B <= 253 buckets -- more go to cd.hip (same semantics)
+    // scratch: B * NCLS segments, i.e. B <= 339 buckets -- more go to cd.hip (same semantics)
     const int64_t nseg = (int64_t)cd_buckets(c, algo) * NCLS;
     return !c.order_pass && (is_louvain(algo) || algo == FC_ALGO_LPM) && (!is_louvain(algo) || c.g.M2 <= 0x7fffffffll) &&
            c.g.m < (int64_t(1) << 31) && (c.chunk == 0 || c.chunk == RL_CHUNK) &&
@@ -1733,6 +1744,15 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         }
         // one unit per wave: rows read as wave-uniform, an item ahead (rl_sorted_u1)
         const bool u1 = VPW == 1 && c.rl_u1;
+        // degree classes -> decide launches (sorting-network widths): every class on its own,
+        // or neighbouring classes merged into the wider network (fewer, larger launches)
+        struct ClsGroup { int c0, c1, K; };
+        static const ClsGroup G3[] = {{0, 1, 16}, {1, 3, 32}, {3, 5, 64}};
+        static const ClsGroup G4[] = {{0, 1, 16}, {1, 3, 32}, {3, 4, 48}, {4, 5, 64}};
+        static const ClsGroup G5[] = {{0, 1, 16}, {1, 2, 24}, {2, 3, 32}, {3, 4, 48}, {4, 5, 64}};
+        const int gsel = louv ? c.rl_groups_louv : c.rl_groups_lpa;
+        const ClsGroup* groups = gsel <= 3 ? G3 : gsel == 4 ? G4 : G5;
+        const int ngroups = gsel <= 3 ? 3 : gsel == 4 ? 4 : 5;
         auto grid_of = [&](int64_t n) {
             const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
             return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
@@ -1742,14 +1762,18 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             if (nb_all <= 0) continue;
             // each decide launch timed on its own (span 7: one span per launch, as rocprofv3 counts them)
             if (pack && vmode) {
-                for (int cls = 0; cls < NCLS - 1; ++cls) {
-                    const int seg = k * NCLS + cls;
-                    const int64_t n = hb[nseg + 1 + seg + 1] - hb[nseg + 1 + seg];
+                for (int gi = 0; gi < ngroups; ++gi) {
+                    const int seg = k * NCLS + groups[gi].c0, ns = groups[gi].c1 - groups[gi].c0, KG = groups[gi].K;
+                    const int64_t n = hb[nseg + 1 + seg + ns] - hb[nseg + 1 + seg];
                     if (n <= 0) continue;
                     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 63) / 64, 8192));
-#define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide_v<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, sweep); timer_end(c, 7, ev); } while (0)
-#define RL_LAUNCH_K(L, U) \
-    do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
+#define RL_LAUNCH(L, KK, U) do { const int ev = timer_begin(c); k_rl_decide_v<L, KK, U><<<grid, RTB, 0, c.stream>>>(a, seg, ns, sweep); timer_end(c, 7, ev); } while (0)
+#define RL_LAUNCH_K(L, U)                                                                            \
+    do {                                                                                             \
+        if (KG == 16) RL_LAUNCH(L, 16, U); else if (KG == 24) RL_LAUNCH(L, 24, U);                   \
+        else if (KG == 32) RL_LAUNCH(L, 32, U); else if (KG == 48) RL_LAUNCH(L, 48, U);              \
+        else RL_LAUNCH(L, 64, U);                                                                    \
+    } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
                     else if (louv && a.colw) RL_LAUNCH_K(true, WM_W8);
                     else if (louv) RL_LAUNCH_K(true, WM_WIDE);
@@ -1758,9 +1782,9 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
 #undef RL_LAUNCH
                 }
             } else if (pack) {
-                for (int cls = 0; cls < NCLS - 1; ++cls) {
-                    const int seg = k * NCLS + cls;
-                    const int64_t n = hb[seg + 1] - hb[seg];
+                for (int gi = 0; gi < ngroups; ++gi) {
+                    const int seg = k * NCLS + groups[gi].c0, ns = groups[gi].c1 - groups[gi].c0, KG = groups[gi].K;
+                    const int64_t n = hb[seg + ns] - hb[seg];
                     if (n <= 0) continue;
                     const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
 #define RL_LAUNCH_1(L, KK, U, U1)                                                                                  \
@@ -1769,12 +1793,16 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
             ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U, U1>() * c.rl_grid_mul)) \
             : grid_of(n);                                                                                          \
         const int ev = timer_begin(c);                                                                             \
-        k_rl_decide<L, KK, U, U1><<<grid, RTB, 0, c.stream>>>(a, seg, sweep);                                      \
+        k_rl_decide<L, KK, U, U1><<<grid, RTB, 0, c.stream>>>(a, seg, ns, sweep);                                  \
         timer_end(c, 7, ev);                                                                                       \
     } while (0)
 #define RL_LAUNCH(L, KK, U) do { if (u1) RL_LAUNCH_1(L, KK, U, true); else RL_LAUNCH_1(L, KK, U, false); } while (0)
-#define RL_LAUNCH_K(L, U) \
-    do { if (cls == 0) RL_LAUNCH(L, 16, U); else if (cls == 1) RL_LAUNCH(L, 32, U); else RL_LAUNCH(L, 64, U); } while (0)
+#define RL_LAUNCH_K(L, U)                                                                            \
+    do {                                                                                             \
+        if (KG == 16) RL_LAUNCH(L, 16, U); else if (KG == 24) RL_LAUNCH(L, 24, U);                   \
+        else if (KG == 32) RL_LAUNCH(L, 32, U); else if (KG == 48) RL_LAUNCH(L, 48, U);              \
+        else RL_LAUNCH(L, 64, U);                                                                    \
+    } while (0)
                     if (louv && a.unitw) RL_LAUNCH_K(true, WM_UNIT);
                     else if (louv && a.colw) RL_LAUNCH_K(true, WM_W8);
                     else if (louv) RL_LAUNCH_K(true, WM_WIDE);

@@ -226,10 +226,14 @@ struct Ctx {
     // cd_rl.hip decide with one unit per wave (64 local replicas or more): the row as one
     // coalesced load an item ahead, neighbour ids by readlane (A/B switch; same decisions)
     int rl_u1 = getenv("FC_RL_U1") ? atoi(getenv("FC_RL_U1")) : 1;
+    // replica-lane decide launches per bucket: 3 (networks of 16 / 32 / 64 keys), 4 (+48) or 5
+    // (+24 and 48) -- per algorithm (cd_rl.hip, degree classes)
+    int rl_groups_louv = getenv("FC_RL_GROUPS_LOUV") ? atoi(getenv("FC_RL_GROUPS_LOUV")) : 3;
+    int rl_groups_lpa = getenv("FC_RL_GROUPS_LPA") ? atoi(getenv("FC_RL_GROUPS_LPA")) : 4;
 };
 
 struct Ctx;
-constexpr int FC_HPIN_I64 = 1024;   // pinned host scratch: per-sweep records (cd_rl.hip: boff | voff | n_active)
+constexpr int FC_HPIN_I64 = 2048;   // pinned host scratch: per-sweep records (cd_rl.hip: boff | voff | n_active)
 // State the replica-lane engine hands to cd_run at the first filtered sweep of a hybrid batch
 // (FC_OPT_CD_ENGINE=2, cd_rl.hip): fill() writes it in cd.hip's layout on c.stream -- labels
 // [n_r][N] in slot order, int32 totals [n_r][N], affected flags as bit words uint32

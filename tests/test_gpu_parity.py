@@ -253,7 +253,7 @@ def test_cd_bit_exact_vs_twin(fcmod, algo, buckets, chunk, prune, tail, coarsen,
 
 @pytest.mark.parametrize("algo", [0, 1])
 def test_cd_hybrid_many_buckets_falls_back(fcmod, algo):
-    """FC_OPT_BUCKETS past what the replica-lane sweep record holds (253 buckets x 4 degree
+    """FC_OPT_BUCKETS past what the replica-lane sweep record holds (339 buckets x 6 degree
     classes in the pinned scratch): the hybrid runs the batch on cd.hip with the same
     semantics instead of failing, bit-exact against the twin."""
     case, g = _lfr1k_graph()
@@ -417,6 +417,40 @@ def _weighted_consensus_engine(fcmod, seed):
     eng.closure_partial(cnt)
     eng.closure_apply(0, case.n_p, case.delta, cnt, 0)
     return case, eng
+
+
+@pytest.mark.parametrize("groups", ["3", "4", "5"])
+@pytest.mark.parametrize("n_r", [6, 64])
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cd_replica_lanes_class_groups_bit_exact(fcmod, algo, n_r, groups, monkeypatch):
+    """The replica-lane decide's degree classes (16 | 24 | 32 | 48 | 64 keys) launched one per
+    class or merged into the wider network (FC_RL_GROUPS_LOUV / _LPA = 3, 4, 5): the same
+    decisions whichever network sorts a row -- bit-exact against the twin, per-lane rows (6
+    replicas) and one unit per wave (64), on the input graph and a weighted consensus graph."""
+    monkeypatch.setenv("FC_RL_GROUPS_LOUV", groups)
+    monkeypatch.setenv("FC_RL_GROUPS_LPA", groups)
+    case, g = _lfr1k_graph()
+    eng = fcmod.Engine(seed=71)
+    kw = _engine(eng, 1)
+    eng.load_graph(case.N, case.edges_file[:, 0], case.edges_file[:, 1])
+    deg = np.bincount(case.edges_file.ravel(), minlength=case.N)
+    assert deg.max() > 24 and ((deg > 16) & (deg <= 24)).any() and ((deg > 32) & (deg <= 48)).any()
+    eng.cd(algo, 0, n_r, n_r, 2)
+    exp, _ = _twin(eng, algo, case.N, case.edges_file, n_r, 0, 2, 71, **kw)
+    np.testing.assert_array_equal(eng.get_labels(n_r), exp)
+    eng.close()
+    case, eng = _weighted_consensus_engine(fcmod, 73)
+    eng.set_option("cd_engine", 1)
+    u, v, w, _ = eng.get_graph()
+    sigma = eng.node_map()
+    a_, b_ = sigma[u], sigma[v]
+    lo, hi = np.minimum(a_, b_), np.maximum(a_, b_)
+    o = np.lexsort((hi, lo))
+    g_int = orc.EdgeGraph(case.N, lo[o], hi[o], w[o], np.zeros(len(o), np.int64))
+    eng.cd(algo, 0, n_r, n_r, 3)
+    exp, _ = orc.engine_cd(algo, g_int, n_r, 0, 3, 73, shared=1, coarsen=0)
+    np.testing.assert_array_equal(eng.get_labels(n_r), exp[:, sigma])
+    eng.close()
 
 
 @pytest.mark.parametrize("u1", ["0", "1"])
