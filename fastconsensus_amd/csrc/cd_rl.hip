@@ -669,6 +669,9 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
     return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
 }
 
+#ifndef FC_RL_SPLIT
+#define FC_RL_SPLIT 2                   // one-unit-per-wave decide, narrower network for short rows: 1 in the 32-key kernel, 2 in the 64-key one (A/B switch)
+#endif
 // ---- one unit per wave (LG = 64: every lane deciding the same vertex, VPW = 1; C4 / C5) ----
 // The unit's record and row are wave-uniform, so the row is not K per-lane broadcast loads:
 // lane j holds entry j of the NEXT item's row (one coalesced load issued an item ahead, in
@@ -755,6 +758,21 @@ __device__ __forceinline__ int32_t rl_sorted_u1(const RL& a, const Hdr& h, int s
         if (__ballot(!settled) == 0) {
             if (wk) c_cand += 1u;                               // the own label, the one candidate
             return -1;
+        }
+    }
+    // The row length is wave-uniform here, so a row of <= 3K/4 entries is sorted by the narrower
+    // network (24 keys in the 32-key kernel, 48 in the 64-key one: the truncated odd-even merge
+    // networks, 132 / 384 compare-exchanges against 191 / 543) without a launch of its own; the
+    // keys past the row are empty (-1) and empty keys never form a run, so dropping them changes
+    // no decision.  LFR-1M: ~57 % of the 17..32-entry rows have <= 24, ~96 % of the 33..64 ones
+    // <= 48.
+    constexpr int KS = (K == 32 && (FC_RL_SPLIT & 1)) ? 24 : (K == 64 && (FC_RL_SPLIT & 2)) ? 48 : K;
+    if constexpr (KS < K) {
+        if (__builtin_amdgcn_readfirstlane(ds) <= KS) {
+            int32_t y[KS];
+#pragma unroll
+            for (int j = 0; j < KS; ++j) y[j] = x[j];
+            return rl_runs<LOUV, KS, WM>(a, h, sweep, y, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
         }
     }
     return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
