@@ -1790,7 +1790,7 @@ void store_order(Ctx& c) {
     } pass(c);
     // The first sweeps place almost every vertex (LFR-1M: 89 % and 52 % of the vertices move
     // in sweeps 0 and 1, < 6 % from sweep 3 on), so a few sweeps give the storage order; the
-    // remaining one-replica sweeps would only pay latency (FC_ORDER_SWEEPS, default 4).
+    // remaining one-replica sweeps would only pay latency (FC_ORDER_SWEEPS, default 3; profiles/r06_ab.txt).
     const int ms = c.max_sweeps, mb = c.buckets;
     c.max_sweeps = std::max(1, std::min(ms, c.order_sweeps));
     c.buckets = std::max(1, c.order_buckets);

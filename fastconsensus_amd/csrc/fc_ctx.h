@@ -196,7 +196,7 @@ struct Ctx {
     int64_t tail_visits = getenv("FC_TAIL_VISITS") ? atoll(getenv("FC_TAIL_VISITS")) : -1;
     bool order_pass = false;        // store_order()'s CD run (int64 totals, see there)
     int store_order = 1;            // FC_OPT_STORE: label rows in community order (slot spos[v])
-    int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 4;   // sweeps of that pass
+    int order_sweeps = getenv("FC_ORDER_SWEEPS") ? atoi(getenv("FC_ORDER_SWEEPS")) : 3;   // sweeps of that pass (4 until round 6: LFR-1M load -0.37 ms at 3, same run time)
     // its buckets per sweep: the pass only permutes label storage (results are identical), and
     // 4 big launches per sweep beat 32 small ones (LFR-1M load 9.9 -> 8.0 ms, tools/r03_ordb.sh)
     int order_buckets = getenv("FC_ORDER_BUCKETS") ? atoi(getenv("FC_ORDER_BUCKETS")) : 4;
