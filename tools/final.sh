@@ -1,12 +1,12 @@
 #!/bin/bash
 # Final verification of a round: the whole GPU suite + smoke, then the bench line of every config
 # (the headline with its CPU baseline) into gpurun_out/<tag>final/<name>.json, and a kernel trace
-# of the n_p = 8 share (gpurun_out/<tag>final/np8tr).  Run tools/pmc_all.sh first and copy its
+# of the n_p = 8 share (gpurun_out/<tag>final/np8tr) and of the C4 step (c4tr).  Run tools/pmc_all.sh first and copy its
 # summaries into profiles/, so that every line carries traffic from a same-source PMC profile.
 # Usage: tools/final.sh <tag> [name...]   (names: suite, the bench lines below, np8trace)
 set -u
 TAG=$1; shift
-NAMES=${*:-"suite lfr1m lfr100k lfr100k_lpm np8 np16 sbm4m leiden infomap np8trace"}
+NAMES=${*:-"suite lfr1m lfr100k lfr100k_lpm np8 np16 sbm4m leiden infomap np8trace c4trace"}
 OUT=gpurun_out/${TAG}final
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -39,6 +39,11 @@ for n in $NAMES; do
             python3 tools/trace_gaps.py $(find $OUT/np8tr -name "*kernel_trace.csv" | head -1) > $OUT/np8_trace_gaps.txt && head -8 $OUT/np8_trace_gaps.txt
             find $OUT/np8tr -name "*kernel_trace.csv" -size +8M -delete
             echo "np8 trace ok" ;;
+        c4trace)   # the same kernel trace at n_p = 64 (the headline C4 step)
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c4tr -o c4 --output-format csv -- python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline > $OUT/c4tr.log 2>&1 || { echo c4 trace failed; tail -5 $OUT/c4tr.log; exit 1; }
+            python3 tools/trace_gaps.py $(find $OUT/c4tr -name "*kernel_trace.csv" | head -1) > $OUT/c4_trace_gaps.txt && head -8 $OUT/c4_trace_gaps.txt
+            find $OUT/c4tr -name "*kernel_trace.csv" -size +8M -delete
+            echo "c4 trace ok" ;;
         *) echo "unknown $n"; exit 1 ;;
     esac
 done
