@@ -29,10 +29,12 @@ int timer_begin(Ctx& c) {
     FC_HIP(hipEventRecord(t.pool[idx], c.stream));
     return idx;
 }
-void timer_end(Ctx& c, int slot, int b) {
-    if (b < 0) return;
+void timer_end(Ctx& c, int slot, int b) { (void)timer_end_ev(c, slot, b); }
+int timer_end_ev(Ctx& c, int slot, int b) {
+    if (b < 0) return -1;
     const int e = timer_begin(c);
     c.timer.spans[slot].push_back({b, e});
+    return e;
 }
 void timer_collect(Ctx& c, fc_stats* st) {
     Timer& t = c.timer;

@@ -670,7 +670,7 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
 }
 
 #ifndef FC_RL_SPLIT
-#define FC_RL_SPLIT 2                   // one-unit-per-wave decide, narrower network for short rows: 1 in the 32-key kernel, 2 in the 64-key one (A/B switch)
+#define FC_RL_SPLIT 6                   // one-unit-per-wave decide, narrower networks for short rows (A/B switch bits): 4 = 16 keys and 1 = 24 keys in the 32-key kernel, 2 = 48 keys in the 64-key one
 #endif
 // ---- one unit per wave (LG = 64: every lane deciding the same vertex, VPW = 1; C4 / C5) ----
 // The unit's record and row are wave-uniform, so the row is not K per-lane broadcast loads:
@@ -766,6 +766,15 @@ __device__ __forceinline__ int32_t rl_sorted_u1(const RL& a, const Hdr& h, int s
     // keys past the row are empty (-1) and empty keys never form a run, so dropping them changes
     // no decision.  LFR-1M: ~57 % of the 17..32-entry rows have <= 24, ~96 % of the 33..64 ones
     // <= 48.
+    constexpr int KS1 = (K == 32 && (FC_RL_SPLIT & 4)) ? 16 : K;   // 16-entry rows in the 32-key kernel
+    if constexpr (KS1 < K) {
+        if (__builtin_amdgcn_readfirstlane(ds) <= KS1) {
+            int32_t y[KS1];
+#pragma unroll
+            for (int j = 0; j < KS1; ++j) y[j] = x[j];
+            return rl_runs<LOUV, KS1, WM>(a, h, sweep, y, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
+        }
+    }
     constexpr int KS = (K == 32 && (FC_RL_SPLIT & 1)) ? 24 : (K == 64 && (FC_RL_SPLIT & 2)) ? 48 : K;
     if constexpr (KS < K) {
         if (__builtin_amdgcn_readfirstlane(ds) <= KS) {
@@ -1765,12 +1774,14 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         // degree classes -> decide launches (sorting-network widths): every class on its own,
         // or neighbouring classes merged into the wider network (fewer, larger launches)
         struct ClsGroup { int c0, c1, K; };
+        static const ClsGroup G2[] = {{0, 3, 32}, {3, 5, 64}};   // one unit per wave only (in-kernel widths)
         static const ClsGroup G3[] = {{0, 1, 16}, {1, 3, 32}, {3, 5, 64}};
         static const ClsGroup G4[] = {{0, 1, 16}, {1, 3, 32}, {3, 4, 48}, {4, 5, 64}};
         static const ClsGroup G5[] = {{0, 1, 16}, {1, 2, 24}, {2, 3, 32}, {3, 4, 48}, {4, 5, 64}};
         const int gsel = louv ? c.rl_groups_louv : c.rl_groups_lpa;
-        const ClsGroup* groups = gsel <= 3 ? G3 : gsel == 4 ? G4 : G5;
-        const int ngroups = gsel <= 3 ? 3 : gsel == 4 ? 4 : 5;
+        const bool g2 = gsel == 2 && u1;
+        const ClsGroup* groups = g2 ? G2 : gsel <= 3 ? G3 : gsel == 4 ? G4 : G5;
+        const int ngroups = g2 ? 2 : gsel <= 3 ? 3 : gsel == 4 ? 4 : 5;
         auto grid_of = [&](int64_t n) {
             const int64_t items = banks == 1 ? (n + VPW - 1) / VPW : n * banks;
             return (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
@@ -1800,6 +1811,9 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
 #undef RL_LAUNCH
                 }
             } else if (pack) {
+                // a bucket's decide launches follow each other with nothing between them: the end
+                // event of one is the start event of the next (one event record per launch)
+                int chain_ev = -1;
                 for (int gi = 0; gi < ngroups; ++gi) {
                     const int seg = k * NCLS + groups[gi].c0, ns = groups[gi].c1 - groups[gi].c0, KG = groups[gi].K;
                     const int64_t n = hb[seg + ns] - hb[seg];
@@ -1810,9 +1824,10 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         const unsigned grid = (c.rl_grid_mul > 0 && L)                                                             \
             ? (unsigned)std::max<int64_t>(1, std::min<int64_t>(items, rl_decide_slots<L, KK, U, U1>() * c.rl_grid_mul)) \
             : grid_of(n);                                                                                          \
-        const int ev = timer_begin(c);                                                                             \
+        const int ev = chain_ev >= 0 ? chain_ev : timer_begin(c);                                                  \
         k_rl_decide<L, KK, U, U1><<<grid, RTB, 0, c.stream>>>(a, seg, ns, sweep);                                  \
-        timer_end(c, 7, ev);                                                                                       \
+        const int ee = timer_end_ev(c, 7, ev);                                                                     \
+        if (c.timer_chain) chain_ev = ee;                                                                          \
     } while (0)
 #define RL_LAUNCH(L, KK, U) do { if (u1) RL_LAUNCH_1(L, KK, U, true); else RL_LAUNCH_1(L, KK, U, false); } while (0)
 #define RL_LAUNCH_K(L, U)                                                                            \

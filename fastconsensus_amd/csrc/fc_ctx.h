@@ -226,10 +226,14 @@ struct Ctx {
     // cd_rl.hip decide with one unit per wave (64 local replicas or more): the row as one
     // coalesced load an item ahead, neighbour ids by readlane (A/B switch; same decisions)
     int rl_u1 = getenv("FC_RL_U1") ? atoi(getenv("FC_RL_U1")) : 1;
+    // timed decide launches of one bucket share their boundary events (FC_TIMER_CHAIN=0: two each)
+    int timer_chain = getenv("FC_TIMER_CHAIN") ? atoi(getenv("FC_TIMER_CHAIN")) : 1;
     // replica-lane decide launches per bucket: 3 (networks of 16 / 32 / 64 keys), 4 (+48) or 5
-    // (+24 and 48) -- per algorithm (cd_rl.hip, degree classes)
-    int rl_groups_louv = getenv("FC_RL_GROUPS_LOUV") ? atoi(getenv("FC_RL_GROUPS_LOUV")) : 3;
-    int rl_groups_lpa = getenv("FC_RL_GROUPS_LPA") ? atoi(getenv("FC_RL_GROUPS_LPA")) : 4;
+    // (+24 and 48) -- per algorithm (cd_rl.hip, degree classes); 2: one launch for the rows of
+    // <= 32 and one for 33..64, the one-unit-per-wave kernels picking the network per row
+    // (FC_RL_SPLIT; other layouts run 3)
+    int rl_groups_louv = getenv("FC_RL_GROUPS_LOUV") ? atoi(getenv("FC_RL_GROUPS_LOUV")) : 2;
+    int rl_groups_lpa = getenv("FC_RL_GROUPS_LPA") ? atoi(getenv("FC_RL_GROUPS_LPA")) : 2;
 };
 
 struct Ctx;
@@ -315,6 +319,7 @@ int64_t count_unconverged(Ctx& c, const int32_t* w, int64_t m, int n_p);
 // timing helpers
 int timer_begin(Ctx& c);
 void timer_end(Ctx& c, int slot, int begin_ev);
+int timer_end_ev(Ctx& c, int slot, int begin_ev);   // timer_end, returning the end event (-1: off)
 void timer_collect(Ctx& c, fc_stats* st);
 // scratch helpers
 template <class T> inline T* ensure(DevBuf& b, size_t count) {

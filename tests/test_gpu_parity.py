@@ -419,7 +419,7 @@ def _weighted_consensus_engine(fcmod, seed):
     return case, eng
 
 
-@pytest.mark.parametrize("groups", ["3", "4", "5"])
+@pytest.mark.parametrize("groups", ["2", "3", "4", "5"])
 @pytest.mark.parametrize("n_r", [6, 64])
 @pytest.mark.parametrize("algo", [0, 1])
 def test_cd_replica_lanes_class_groups_bit_exact(fcmod, algo, n_r, groups, monkeypatch):
