@@ -46,6 +46,12 @@ constexpr int VPWMAX = 8;               // sub-groups per wave (lane groups of >
 constexpr int RL_CHUNK = 16;            // = cd.hip CHUNK (chunked visit orders)
 // slow-visit and visit-mode list entries pack the local replica in 14 bits ((e << 14) | rr)
 constexpr int RL_MAX_REPLICAS = 16384;
+// Narrower sorting networks for short rows inside one decide launch (A/B switch bits): one unit
+// per wave -- 4: 16 keys and 1: 24 keys in the 32-key kernel, 2: 48 keys in the 64-key one; per-lane
+// rows (by the wave's longest) -- 8: 16 keys in the 32-key kernel, 16: 48 keys in the 64-key one
+#ifndef FC_RL_SPLIT
+#define FC_RL_SPLIT 30
+#endif
 #ifndef FC_LPA_TIES
 #define FC_LPA_TIES 1                   // LPA tie revisits under pruning (oracle tw_replica); 0: bisect builds only
 #endif
@@ -666,12 +672,21 @@ __device__ __forceinline__ int32_t rl_sorted(const RL& a, const Hdr& h, int swee
             return -1;
         }
     }
+    // per-lane rows (several vertices per wave): the wave's longest row picks the network (a
+    // bucket's list is class-minor, so a wave's rows mostly share their class), which lets one
+    // launch serve the rows of <= 32 and one those of 33..64 (FC_RL_SPLIT bits 8 / 16)
+    constexpr int KN = (K == 32 && (FC_RL_SPLIT & 8)) ? 16 : (K == 64 && (FC_RL_SPLIT & 16)) ? 48 : K;
+    if constexpr (KN < K) {
+        if (__builtin_amdgcn_readfirstlane(wave_max(dsw)) <= KN) {
+            int32_t y[KN];
+#pragma unroll
+            for (int j = 0; j < KN; ++j) y[j] = x[j];
+            return rl_runs<LOUV, KN, WM>(a, h, sweep, y, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
+        }
+    }
     return rl_runs<LOUV, K, WM>(a, h, sweep, x, own, kown, tot_own, home, c_dq, c_unst, c_cand, slow_out);
 }
 
-#ifndef FC_RL_SPLIT
-#define FC_RL_SPLIT 6                   // one-unit-per-wave decide, narrower networks for short rows (A/B switch bits): 4 = 16 keys and 1 = 24 keys in the 32-key kernel, 2 = 48 keys in the 64-key one
-#endif
 // ---- one unit per wave (LG = 64: every lane deciding the same vertex, VPW = 1; C4 / C5) ----
 // The unit's record and row are wave-uniform, so the row is not K per-lane broadcast loads:
 // lane j holds entry j of the NEXT item's row (one coalesced load issued an item ahead, in
@@ -1779,7 +1794,7 @@ void cd_run_rl(Ctx& c, int algo, int rbegin, int rcount, int n_p_total, int iter
         static const ClsGroup G4[] = {{0, 1, 16}, {1, 3, 32}, {3, 4, 48}, {4, 5, 64}};
         static const ClsGroup G5[] = {{0, 1, 16}, {1, 2, 24}, {2, 3, 32}, {3, 4, 48}, {4, 5, 64}};
         const int gsel = louv ? c.rl_groups_louv : c.rl_groups_lpa;
-        const bool g2 = gsel == 2 && u1;
+        const bool g2 = gsel == 2 && (u1 || (FC_RL_SPLIT & 24) == 24);
         const ClsGroup* groups = g2 ? G2 : gsel <= 3 ? G3 : gsel == 4 ? G4 : G5;
         const int ngroups = g2 ? 2 : gsel <= 3 ? 3 : gsel == 4 ? 4 : 5;
         auto grid_of = [&](int64_t n) {
